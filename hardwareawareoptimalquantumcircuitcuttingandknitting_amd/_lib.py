@@ -1,0 +1,76 @@
+"""ctypes binding of ``libqknit.so`` (declared in ``include/qknit.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``hipcc
+--offload-arch=gfx950``). There is no fallback: if the shared object is missing
+or fails to load, :func:`lib` raises, and so does every GPU entry point.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libqknit.so")
+
+c_i32, c_i64, c_u32, c_u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64
+c_vp, c_dp, c_lp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)
+
+
+class QkPass(ctypes.Structure):
+    _fields_ = [("tile_mask", c_u64), ("group_begin", c_i32), ("group_end", c_i32),
+                ("flags", c_i32), ("traced_local", c_u32)]
+
+
+class QkProgram(ctypes.Structure):
+    _fields_ = [("n", c_i32), ("n_eff", c_i32), ("m", c_i32), ("n_slots", c_i32),
+                ("packed", c_i32), ("n_passes", c_i32), ("passes", ctypes.POINTER(QkPass)),
+                ("ops", c_vp), ("groups", c_vp), ("mats", c_vp)]
+
+
+#: every symbol include/qknit.h declares: name -> (restype, argtypes)
+SIGNATURES = {
+    "qk_version": (ctypes.c_char_p, []),
+    "qk_ctx_create": (c_i32, [ctypes.c_int, ctypes.POINTER(c_vp)]),
+    "qk_ctx_destroy": (c_i32, [c_vp]),
+    "qk_ctx_set_stream": (c_i32, [c_vp, c_vp]),
+    "qk_ctx_synchronize": (c_i32, [c_vp]),
+    "qk_last_error": (ctypes.c_char_p, [c_vp]),
+    "qk_sweep_workspace_bytes": (c_i32, [ctypes.POINTER(QkProgram), c_i64, ctypes.POINTER(c_i64)]),
+    "qk_sweep": (c_i32, [c_vp, ctypes.POINTER(QkProgram), c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "qk_reduce_labels": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "qk_gemm_keyed": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
+                              c_vp, c_i64, c_vp, ctypes.c_int]),
+    "qk_khatri_rao": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "qk_gather_rows": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class QknitError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise QknitError(
+                    f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`"
+                )
+            handle = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+        return _lib
+
+
+def check(ctx, status: int, what: str) -> None:
+    if status != 0:
+        msg = lib().qk_last_error(ctx)
+        raise QknitError(f"{what} failed (status {status}): {msg.decode() if msg else ''}")

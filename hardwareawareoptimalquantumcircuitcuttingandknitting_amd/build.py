@@ -1,0 +1,37 @@
+"""In-tree build of libqknit.so (hipcc, gfx950). Used by __graft_entry__.build() and tests."""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc", "qknit.hip")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "qknit.h")
+OUT = os.path.join(HERE, "libqknit.so")
+ARCH = os.environ.get("QKNIT_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def build_library(force: bool = False, verbose: bool = False) -> str:
+    stale = not os.path.exists(OUT) or any(
+        os.path.getmtime(p) > os.path.getmtime(OUT) for p in (SRC, HEADER)
+    )
+    if not (force or stale):
+        return OUT
+    tmp = OUT + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-result", SRC, "-o", tmp]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{res.stderr}")
+    if verbose and res.stderr:
+        print(res.stderr)
+    os.replace(tmp, OUT)
+    return OUT

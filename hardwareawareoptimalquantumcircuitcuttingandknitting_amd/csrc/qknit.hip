@@ -1,0 +1,708 @@
+// qknit.hip — MI355X (gfx950 / CDNA4) kernels and C ABI of the circuit-knitting engine.
+//
+// Hot path of the reference (thangktran/HardwareAwareOptimalQuantumCircuitCuttingAndKnitting):
+//   * qk_sweep          — batched exact statevector sweep of every cut instantiation of a
+//                         fragment (replaces AerSimulator via third_party/qvm/qvm/run.py:36-58)
+//   * qk_reduce_labels  — signed config-bit folding per label (virtual_gates.py:105-124,179-194)
+//   * qk_gemm_keyed     — fp64 MFMA knit contraction with global-key scatter
+//                         (replaces virtual_circuit.py:50-68,165-171,216-228, quasi_distr.py:55-60)
+// Design notes: DESIGN.md §3 (sweep) and §4 (knit).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/qknit.h"
+
+struct qk_ctx {
+    int device;
+    hipStream_t own;
+    hipStream_t stream;
+    std::string err;
+};
+
+namespace {
+
+constexpr int TILE = 1 << QK_TILE_BITS;  // 4096 amplitudes per tile (64 KiB complex128)
+constexpr int NT = 256;                    // threads per sweep workgroup
+constexpr int PER = TILE / NT;             // 16 amplitudes per thread (= fiber size)
+
+int fail(qk_ctx* ctx, int code, const char* fmt, const char* detail = "") {
+    if (ctx) {
+        char buf[512];
+        snprintf(buf, sizeof(buf), fmt, detail);
+        ctx->err = buf;
+    }
+    return code;
+}
+
+#define QK_HIP(ctx, call)                                                     \
+    do {                                                                      \
+        hipError_t e_ = (call);                                               \
+        if (e_ != hipSuccess) return fail(ctx, QK_EHIP, "%s", hipGetErrorString(e_)); \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------
+// sweep: complex helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double2 cmul(double ar, double ai, double2 b) {
+    return make_double2(fma(ar, b.x, -ai * b.y), fma(ar, b.y, ai * b.x));
+}
+// m0 * a + m1 * b with m given as (re, im) pairs
+__device__ __forceinline__ double2 cmac2(const double* m, double2 a, double2 b) {
+    double re = m[0] * a.x;
+    re = fma(-m[1], a.y, re);
+    re = fma(m[2], b.x, re);
+    re = fma(-m[3], b.y, re);
+    double im = m[0] * a.y;
+    im = fma(m[1], a.x, im);
+    im = fma(m[2], b.y, im);
+    im = fma(m[3], b.x, im);
+    return make_double2(re, im);
+}
+
+// LDS swizzle: XOR the low nibble with the two higher nibbles (bank spread for strided fibers)
+__device__ __forceinline__ int swz(int t) { return t ^ (((t >> 4) ^ (t >> 8)) & 15); }
+
+// Keeps the fiber in VGPRs: without it SimplifyCFG merges the per-position switch cases into
+// loads/stores through a phi'd pointer and the whole fiber is demoted to scratch.
+__device__ __forceinline__ void pin(double2 (&v)[PER]) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) asm volatile("" : "+v"(v[r].x), "+v"(v[r].y));
+}
+
+template <int A>
+__device__ __forceinline__ void ap_u1(double2 (&v)[PER], const double* m) {
+    double mm[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mm[i] = m[i];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if (r & (1 << A)) continue;
+        const double2 a = v[r], b = v[r | (1 << A)];
+        v[r] = cmac2(mm, a, b);
+        v[r | (1 << A)] = cmac2(mm + 4, a, b);
+    }
+}
+
+template <int A>
+__device__ __forceinline__ void ap_d1(double2 (&v)[PER], const double* d) {
+    const double d0r = d[0], d0i = d[1], d1r = d[2], d1i = d[3];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) v[r] = (r & (1 << A)) ? cmul(d1r, d1i, v[r]) : cmul(d0r, d0i, v[r]);
+}
+
+template <int A, int B>
+__device__ __forceinline__ void ap_u2(double2 (&v)[PER], const double* m) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if (r & ((1 << A) | (1 << B))) continue;
+        const int i0 = r, i1 = r | (1 << A), i2 = r | (1 << B), i3 = r | (1 << A) | (1 << B);
+        const double2 x0 = v[i0], x1 = v[i1], x2 = v[i2], x3 = v[i3];
+        double2 y[4];
+#pragma unroll
+        for (int row = 0; row < 4; ++row) {
+            const double* mr = m + row * 8;
+            double2 s = cmac2(mr, x0, x1);
+            const double2 t = cmac2(mr + 4, x2, x3);
+            y[row] = make_double2(s.x + t.x, s.y + t.y);
+        }
+        v[i0] = y[0];
+        v[i1] = y[1];
+        v[i2] = y[2];
+        v[i3] = y[3];
+    }
+}
+
+template <int A, int B>
+__device__ __forceinline__ void ap_d2(double2 (&v)[PER], const double* d) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const int k = ((r >> A) & 1) | (((r >> B) & 1) << 1);
+        v[r] = cmul(d[2 * k], d[2 * k + 1], v[r]);
+    }
+}
+
+template <int C, int T>
+__device__ __forceinline__ void ap_cx(double2 (&v)[PER]) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if (!(r & (1 << C)) || (r & (1 << T))) continue;
+        const double2 t = v[r];
+        v[r] = v[r | (1 << T)];
+        v[r | (1 << T)] = t;
+    }
+}
+
+template <int A, int B>
+__device__ __forceinline__ void ap_swap(double2 (&v)[PER]) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if ((r & (1 << A)) && !(r & (1 << B))) {
+            const int o = (r ^ (1 << A)) | (1 << B);
+            const double2 t = v[r];
+            v[r] = v[o];
+            v[o] = t;
+        }
+    }
+}
+
+__device__ __forceinline__ void dispatch_u1(int a, double2 (&v)[PER], const double* m) {
+    switch (a) {
+        case 0: ap_u1<0>(v, m); pin(v); break;
+        case 1: ap_u1<1>(v, m); pin(v); break;
+        case 2: ap_u1<2>(v, m); pin(v); break;
+        default: ap_u1<3>(v, m); pin(v); break;
+    }
+}
+
+__device__ __forceinline__ void dispatch_d1(int a, double2 (&v)[PER], const double* d) {
+    switch (a) {
+        case 0: ap_d1<0>(v, d); pin(v); break;
+        case 1: ap_d1<1>(v, d); pin(v); break;
+        case 2: ap_d1<2>(v, d); pin(v); break;
+        default: ap_d1<3>(v, d); pin(v); break;
+    }
+}
+
+// pair index for a<b in 0..3: (0,1)=0 (0,2)=1 (0,3)=2 (1,2)=3 (1,3)=4 (2,3)=5
+__device__ __forceinline__ int pair_id(int a, int b) {
+    return a == 0 ? b - 1 : (a == 1 ? b + 1 : 5);
+}
+
+__device__ __forceinline__ void dispatch_u2(int a, int b, double2 (&v)[PER], const double* m) {
+    switch (pair_id(a, b)) {
+        case 0: ap_u2<0, 1>(v, m); pin(v); break;
+        case 1: ap_u2<0, 2>(v, m); pin(v); break;
+        case 2: ap_u2<0, 3>(v, m); pin(v); break;
+        case 3: ap_u2<1, 2>(v, m); pin(v); break;
+        case 4: ap_u2<1, 3>(v, m); pin(v); break;
+        default: ap_u2<2, 3>(v, m); pin(v); break;
+    }
+}
+
+__device__ __forceinline__ void dispatch_d2(int a, int b, double2 (&v)[PER], const double* d) {
+    switch (pair_id(a, b)) {
+        case 0: ap_d2<0, 1>(v, d); pin(v); break;
+        case 1: ap_d2<0, 2>(v, d); pin(v); break;
+        case 2: ap_d2<0, 3>(v, d); pin(v); break;
+        case 3: ap_d2<1, 2>(v, d); pin(v); break;
+        case 4: ap_d2<1, 3>(v, d); pin(v); break;
+        default: ap_d2<2, 3>(v, d); pin(v); break;
+    }
+}
+
+__device__ __forceinline__ void dispatch_swap(int a, int b, double2 (&v)[PER]) {
+    switch (pair_id(a, b)) {
+        case 0: ap_swap<0, 1>(v); pin(v); break;
+        case 1: ap_swap<0, 2>(v); pin(v); break;
+        case 2: ap_swap<0, 3>(v); pin(v); break;
+        case 3: ap_swap<1, 2>(v); pin(v); break;
+        case 4: ap_swap<1, 3>(v); pin(v); break;
+        default: ap_swap<2, 3>(v); pin(v); break;
+    }
+}
+
+__device__ __forceinline__ void dispatch_cx(int c, int t, double2 (&v)[PER]) {
+    switch (c * 4 + t) {
+        case 1: ap_cx<0, 1>(v); pin(v); break;
+        case 2: ap_cx<0, 2>(v); pin(v); break;
+        case 3: ap_cx<0, 3>(v); pin(v); break;
+        case 4: ap_cx<1, 0>(v); pin(v); break;
+        case 6: ap_cx<1, 2>(v); pin(v); break;
+        case 7: ap_cx<1, 3>(v); pin(v); break;
+        case 8: ap_cx<2, 0>(v); pin(v); break;
+        case 9: ap_cx<2, 1>(v); pin(v); break;
+        case 11: ap_cx<2, 3>(v); pin(v); break;
+        case 12: ap_cx<3, 0>(v); pin(v); break;
+        case 13: ap_cx<3, 1>(v); pin(v); break;
+        case 14: ap_cx<3, 2>(v); pin(v); break;
+        default: break;
+    }
+}
+
+struct SweepArgs {
+    const qk_op* ops;
+    const qk_group* groups;
+    const double* mats;
+    const double* job_slots;
+    const double* job_sign;
+    double2* state;  // SPLIT: [n_jobs][2^n]
+    double* pjob;    // FINAL: [n_jobs][2^m]
+    int64_t n_jobs;
+    uint64_t tile_mask;
+    int group_begin, group_end;
+    int flags;
+    uint32_t traced_local;
+    int n, n_eff, m, n_slots;
+};
+
+// Deposit the low bits of `x` into the set bits of `mask` (mask has <= 64 bits).
+__device__ __forceinline__ uint64_t pdep64(uint64_t x, uint64_t mask) {
+    uint64_t r = 0;
+    while (mask) {
+        const uint64_t low = mask & (~mask + 1);
+        if (x & 1) r |= low;
+        x >>= 1;
+        mask ^= low;
+    }
+    return r;
+}
+
+// One pass of the batched sweep. PACKED: a tile = 2^(12-n_eff) whole jobs. SPLIT: a tile =
+// 12 state bits (tile_mask) of one job, 2^(n-12) tiles per job.
+template <bool PACKED>
+__global__ __launch_bounds__(NT) void qk_sweep_pass_kernel(SweepArgs a) {
+    __shared__ double2 lds[TILE];
+    const int tid = threadIdx.x;
+    const bool init = a.flags & 1;
+    const bool final_ = a.flags & 2;
+
+    int64_t job0;        // PACKED: first job of the tile; SPLIT: the job
+    uint64_t tbase = 0;  // SPLIT: state bits outside the tile
+    uint64_t outside = 0;
+    int bitpos[QK_TILE_BITS];
+    if (PACKED) {
+        job0 = (int64_t)blockIdx.x << (QK_TILE_BITS - a.n_eff);
+    } else {
+        const int64_t tiles_per_job = (int64_t)1 << (a.n - QK_TILE_BITS);
+        job0 = (int64_t)blockIdx.x / tiles_per_job;
+        const uint64_t tj = (uint64_t)((int64_t)blockIdx.x % tiles_per_job);
+        const uint64_t nmask = (a.n >= 64) ? ~0ull : ((1ull << a.n) - 1);
+        outside = nmask & ~a.tile_mask;
+        tbase = pdep64(tj, outside);
+        uint64_t mk = a.tile_mask;
+#pragma unroll
+        for (int i = 0; i < QK_TILE_BITS; ++i) {
+            bitpos[i] = __builtin_ctzll(mk);
+            mk &= mk - 1;
+        }
+    }
+    auto local_to_state = [&](int t) -> uint64_t {  // SPLIT only
+        uint64_t s = tbase;
+#pragma unroll
+        for (int i = 0; i < QK_TILE_BITS; ++i) s |= (uint64_t)((t >> i) & 1) << bitpos[i];
+        return s;
+    };
+    const int64_t njobs = a.n_jobs;
+    const int64_t stride_job = PACKED ? 0 : ((int64_t)1 << a.n);
+
+    // ---- load or initialise the tile
+    if (init) {
+        const int nmask = (1 << a.n_eff) - 1;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int t = tid + NT * i;
+            const bool one = PACKED ? ((t & nmask) == 0) : (tbase == 0 && t == 0);
+            lds[swz(t)] = make_double2(one ? 1.0 : 0.0, 0.0);
+        }
+    } else {
+        const double2* src = a.state + job0 * stride_job;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int t = tid + NT * i;
+            lds[swz(t)] = src[local_to_state(t)];
+        }
+    }
+    __syncthreads();
+
+    // ---- fiber groups
+    for (int g = a.group_begin; g < a.group_end; ++g) {
+        const qk_group grp = a.groups[g];
+        const int p0 = grp.pos[0], p1 = grp.pos[1], p2 = grp.pos[2], p3 = grp.pos[3];
+        const int fmask = (1 << p0) | (1 << p1) | (1 << p2) | (1 << p3);
+        // base local index: deposit tid into the 8 non-fiber positions
+        int base = 0;
+        {
+            int x = tid;
+#pragma unroll
+            for (int b = 0; b < QK_TILE_BITS; ++b) {
+                if (!((fmask >> b) & 1)) {
+                    base |= (x & 1) << b;
+                    x >>= 1;
+                }
+            }
+        }
+        int idx[PER];
+#pragma unroll
+        for (int r = 0; r < PER; ++r)
+            idx[r] = base | ((r & 1) << p0) | (((r >> 1) & 1) << p1) | (((r >> 2) & 1) << p2) |
+                     (((r >> 3) & 1) << p3);
+        double2 v[PER];
+#pragma unroll
+        for (int r = 0; r < PER; ++r) v[r] = lds[swz(idx[r])];
+
+        uint64_t sbase;
+        int64_t job;
+        if (PACKED) {
+            sbase = (uint64_t)(base & ((1 << a.n_eff) - 1));
+            job = job0 + (base >> a.n_eff);
+        } else {
+            sbase = local_to_state(base);
+            job = job0;
+        }
+        const int64_t job_c = job < njobs ? job : njobs - 1;  // padded tile slots reuse a valid row
+
+        for (int o = grp.op_begin; o < grp.op_end; ++o) {
+            const qk_op op = a.ops[o];
+            int var = 0;
+            if (op.e1 >= 0) var |= (int)((sbase >> op.e1) & 1);
+            if (op.e2 >= 0) var |= (int)((sbase >> op.e2) & 1) << 1;
+            switch (op.kind) {
+                case QK_U1: dispatch_u1(op.a, v, a.mats + op.mat + 8 * var); break;
+                case QK_D1: dispatch_d1(op.a, v, a.mats + op.mat + 4 * var); break;
+                case QK_SLOT:
+                    dispatch_u1(op.a, v, a.job_slots + (job_c * a.n_slots + op.slot) * 8);
+                    break;
+                case QK_U2: dispatch_u2(op.a, op.b, v, a.mats + op.mat); break;
+                case QK_D2: dispatch_d2(op.a, op.b, v, a.mats + op.mat); break;
+                case QK_CX: dispatch_cx(op.a, op.b, v); break;
+                case QK_SWAP: dispatch_swap(op.a, op.b, v); break;
+                case QK_SCALE: {
+                    const double* s = a.mats + op.mat + 2 * var;
+                    const double sr = s[0], si = s[1];
+#pragma unroll
+                    for (int r = 0; r < PER; ++r) v[r] = cmul(sr, si, v[r]);
+                } break;
+                default: break;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < PER; ++r) lds[swz(idx[r])] = v[r];
+        __syncthreads();
+    }
+
+    // ---- store the tile, or emit signed probabilities
+    if (!final_) {
+        double2* dst = a.state + job0 * stride_job;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int t = tid + NT * i;
+            dst[local_to_state(t)] = lds[swz(t)];
+        }
+        return;
+    }
+    const uint32_t traced = a.traced_local;
+    const uint64_t mmask = (a.m >= 64) ? ~0ull : ((1ull << a.m) - 1);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int t = tid + NT * i;
+        if (t & traced) continue;
+        double acc = 0.0;
+        uint32_t sub = 0;
+        do {
+            const double2 z = lds[swz(t | (int)sub)];
+            acc = fma(z.x, z.x, fma(z.y, z.y, acc));
+            sub = (sub - traced) & traced;
+        } while (sub != 0);
+        int64_t job;
+        uint64_t x;
+        if (PACKED) {
+            job = job0 + (t >> a.n_eff);
+            x = (uint64_t)t & mmask;
+        } else {
+            job = job0;
+            x = local_to_state(t) & mmask;
+        }
+        if (job < njobs) a.pjob[(job << a.m) + (int64_t)x] = a.job_sign[job] * acc;
+    }
+}
+
+__global__ void qk_reduce_labels_kernel(int64_t n_labels, const int64_t* __restrict__ offsets,
+                                        int64_t width, const double* __restrict__ pjob,
+                                        double* __restrict__ q) {
+    const int64_t total = n_labels * width;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t l = e / width, x = e - l * width;
+        double s = 0.0;
+        for (int64_t j = offsets[l]; j < offsets[l + 1]; ++j) s += pjob[j * width + x];
+        q[e] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// knit: fp64 MFMA GEMM, out[keyA[i] + keyB[j]] = sum_k A[k][i] * B[k][j]
+// ------------------------------------------------------------------------------------------
+typedef double d4_t __attribute__((ext_vector_type(4)));
+
+constexpr int GT = 128;      // workgroup tile (M and N)
+constexpr int GK = 16;       // K chunk
+constexpr int GPAD = 16;     // LDS row padding (doubles): 1152-B rows avoid the 2-way conflict
+
+__global__ __launch_bounds__(256) void qk_gemm_keyed_kernel(
+    int64_t M, int64_t N, int64_t K, const double* __restrict__ A, int64_t lda,
+    const double* __restrict__ B, int64_t ldb, const int64_t* __restrict__ keyA, int64_t strideA,
+    const int64_t* __restrict__ keyB, int64_t strideB, double* __restrict__ out, int beta,
+    int tiles_m, int tiles_n) {
+    __shared__ double As[GK][GT + GPAD];
+    __shared__ double Bs[GK][GT + GPAD];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+
+    // XCD-aware mapping: consecutive block ids land on different XCDs (round-robin of 8),
+    // so give each XCD a contiguous run of tiles (shared A/B panels stay in its L2).
+    const int64_t nblk = (int64_t)tiles_m * tiles_n;
+    int64_t bid = blockIdx.x;
+    if (nblk % 8 == 0) bid = (bid % 8) * (nblk / 8) + bid / 8;
+    const int64_t bm = bid % tiles_m, bn = bid / tiles_m;
+    const int64_t m0 = bm * GT, n0 = bn * GT;
+
+    d4_t acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (d4_t){0.0, 0.0, 0.0, 0.0};
+
+    const int lr = tid >> 4;        // chunk row 0..15
+    const int lc = (tid & 15) * 8;  // 8 columns per thread
+    for (int64_t k0 = 0; k0 < K; k0 += GK) {
+        double ra[8], rb[8];
+        const int64_t kr = k0 + lr;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int64_t i = m0 + lc + c, j = n0 + lc + c;
+            ra[c] = (kr < K && i < M) ? A[kr * lda + i] : 0.0;
+            rb[c] = (kr < K && j < N) ? B[kr * ldb + j] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            As[lr][lc + c] = ra[c];
+            Bs[lr][lc + c] = rb[c];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < GK / 4; ++kk) {
+            const int kr2 = kk * 4 + (lane >> 4);
+            double fa[4], fb[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                fa[t] = As[kr2][wm * 64 + t * 16 + (lane & 15)];
+                fb[t] = Bs[kr2][wn * 64 + t * 16 + (lane & 15)];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    // epilogue: f64 16x16 C layout: col = lane & 15, row = (lane >> 4) + 4 * r
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
+                if (row < M && col < N) {
+                    const int64_t o = (keyA ? keyA[row] : row * strideA) + (keyB ? keyB[col] : col * strideB);
+                    const double val = acc[i][j][r];
+                    out[o] = beta ? out[o] + val : val;
+                }
+            }
+        }
+    }
+}
+
+__global__ void qk_khatri_rao_kernel(int64_t K, int64_t M, int64_t N, const double* __restrict__ A,
+                                     int64_t lda, const double* __restrict__ B, int64_t ldb,
+                                     double* __restrict__ out) {
+    const int64_t MN = M * N, total = K * MN;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = e / MN, c = e - k * MN, j = c / M, i = c - j * M;
+        out[e] = A[k * lda + i] * B[k * ldb + j];
+    }
+}
+
+__global__ void qk_gather_rows_kernel(int64_t R, int64_t width, const int64_t* __restrict__ idx,
+                                      const double* __restrict__ coef, const double* __restrict__ src,
+                                      double* __restrict__ dst) {
+    const int64_t total = R * width;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = e / width, x = e - r * width;
+        dst[e] = coef[r] * src[idx[r] * width + x];
+    }
+}
+
+unsigned grid_for(int64_t total, int threads) {
+    int64_t b = (total + threads - 1) / threads;
+    if (b > 8192) b = 8192;
+    if (b < 1) b = 1;
+    return (unsigned)b;
+}
+
+}  // namespace
+
+// ==========================================================================================
+// C ABI
+// ==========================================================================================
+extern "C" {
+
+const char* qk_version(void) { return "qknit 0.1 gfx950"; }
+
+int qk_ctx_create(int device, qk_ctx** out) {
+    if (!out) return QK_EARG;
+    *out = nullptr;
+    if (hipSetDevice(device) != hipSuccess) return QK_EHIP;
+    qk_ctx* c = new qk_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return QK_EHIP;
+    }
+    c->stream = c->own;
+    *out = c;
+    return QK_OK;
+}
+
+int qk_ctx_destroy(qk_ctx* ctx) {
+    if (!ctx) return QK_EARG;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->own);
+    (void)hipStreamDestroy(ctx->own);
+    delete ctx;
+    return QK_OK;
+}
+
+int qk_ctx_set_stream(qk_ctx* ctx, void* s) {
+    if (!ctx) return QK_EARG;
+    ctx->stream = s ? (hipStream_t)s : ctx->own;
+    return QK_OK;
+}
+
+int qk_ctx_synchronize(qk_ctx* ctx) {
+    if (!ctx) return QK_EARG;
+    QK_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return QK_OK;
+}
+
+const char* qk_last_error(qk_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int qk_sweep_workspace_bytes(const qk_program* p, int64_t n_jobs, int64_t* bytes) {
+    if (!p || !bytes || n_jobs < 0) return QK_EARG;
+    *bytes = p->packed ? 0 : n_jobs * ((int64_t)1 << p->n) * (int64_t)sizeof(double2);
+    return QK_OK;
+}
+
+int qk_sweep(qk_ctx* ctx, const qk_program* p, int64_t n_jobs, const double* job_slots,
+             const double* job_sign, void* workspace, int64_t workspace_bytes, double* pjob) {
+    if (!ctx) return QK_EARG;
+    if (!p || !p->passes || p->n_passes < 1) return fail(ctx, QK_EARG, "qk_sweep: empty program%s");
+    if (n_jobs <= 0) return QK_OK;
+    if (!job_sign || !pjob || (p->n_slots > 0 && !job_slots))
+        return fail(ctx, QK_EARG, "qk_sweep: null buffer%s");
+    if (p->m < 0 || p->m > p->n_eff || p->n_eff > 40)
+        return fail(ctx, QK_EARG, "qk_sweep: bad widths%s");
+    if (p->packed) {
+        if (p->n_eff < QK_FIBER_BITS || p->n_eff > QK_TILE_BITS || p->n_passes != 1)
+            return fail(ctx, QK_EARG, "qk_sweep: bad PACKED program%s");
+    } else {
+        if (p->n <= QK_TILE_BITS || p->n_eff != p->n) return fail(ctx, QK_EARG, "qk_sweep: bad SPLIT program%s");
+        int64_t need = 0;
+        qk_sweep_workspace_bytes(p, n_jobs, &need);
+        if (!workspace || workspace_bytes < need) return fail(ctx, QK_EARG, "qk_sweep: workspace too small%s");
+    }
+    if (!(p->passes[p->n_passes - 1].flags & 2) || !(p->passes[0].flags & 1))
+        return fail(ctx, QK_EARG, "qk_sweep: first pass must INIT and last must be FINAL%s");
+    QK_HIP(ctx, hipSetDevice(ctx->device));
+    SweepArgs a{};
+    a.ops = p->ops;
+    a.groups = p->groups;
+    a.mats = p->mats;
+    a.job_slots = job_slots;
+    a.job_sign = job_sign;
+    a.state = (double2*)workspace;
+    a.pjob = pjob;
+    a.n_jobs = n_jobs;
+    a.n = p->n;
+    a.n_eff = p->n_eff;
+    a.m = p->m;
+    a.n_slots = p->n_slots;
+    for (int ip = 0; ip < p->n_passes; ++ip) {
+        const qk_pass& ps = p->passes[ip];
+        if (!p->packed && __builtin_popcountll(ps.tile_mask) != QK_TILE_BITS)
+            return fail(ctx, QK_EARG, "qk_sweep: SPLIT tile must hold 12 state bits%s");
+        a.tile_mask = ps.tile_mask;
+        a.group_begin = ps.group_begin;
+        a.group_end = ps.group_end;
+        a.flags = ps.flags;
+        a.traced_local = ps.traced_local;
+        if (p->packed) {
+            const int64_t per = (int64_t)1 << (QK_TILE_BITS - p->n_eff);
+            const int64_t blocks = (n_jobs + per - 1) / per;
+            if (blocks > 0x7fffffff) return fail(ctx, QK_EARG, "qk_sweep: too many jobs%s");
+            hipLaunchKernelGGL(qk_sweep_pass_kernel<true>, dim3((unsigned)blocks), dim3(NT), 0, ctx->stream, a);
+        } else {
+            const int64_t blocks = n_jobs << (p->n - QK_TILE_BITS);
+            if (blocks > 0x7fffffff) return fail(ctx, QK_EARG, "qk_sweep: too many tiles%s");
+            hipLaunchKernelGGL(qk_sweep_pass_kernel<false>, dim3((unsigned)blocks), dim3(NT), 0, ctx->stream, a);
+        }
+        QK_HIP(ctx, hipGetLastError());
+    }
+    return QK_OK;
+}
+
+int qk_reduce_labels(qk_ctx* ctx, int64_t n_labels, const int64_t* offsets, int64_t width,
+                     const double* pjob, double* q) {
+    if (!ctx) return QK_EARG;
+    if (n_labels < 0 || width < 0) return fail(ctx, QK_EARG, "qk_reduce_labels: negative size%s");
+    if (n_labels == 0 || width == 0) return QK_OK;
+    if (!offsets || !pjob || !q) return fail(ctx, QK_EARG, "qk_reduce_labels: null buffer%s");
+    QK_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(qk_reduce_labels_kernel, dim3(grid_for(n_labels * width, 256)), dim3(256), 0,
+                       ctx->stream, n_labels, offsets, width, pjob, q);
+    QK_HIP(ctx, hipGetLastError());
+    return QK_OK;
+}
+
+int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A, int64_t lda,
+                  const double* B, int64_t ldb, const int64_t* keyA, int64_t strideA,
+                  const int64_t* keyB, int64_t strideB, double* out, int beta) {
+    if (!ctx) return QK_EARG;
+    if (M < 0 || N < 0 || K < 0) return fail(ctx, QK_EARG, "qk_gemm_keyed: negative size%s");
+    if (M == 0 || N == 0) return QK_OK;
+    if (!out || (K > 0 && (!A || !B))) return fail(ctx, QK_EARG, "qk_gemm_keyed: null buffer%s");
+    if (lda < M || ldb < N) return fail(ctx, QK_EARG, "qk_gemm_keyed: leading dimension too small%s");
+    const int64_t tm = (M + GT - 1) / GT, tn = (N + GT - 1) / GT;
+    if (tm * tn > 0x7fffffff) return fail(ctx, QK_EARG, "qk_gemm_keyed: too many tiles%s");
+    QK_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(qk_gemm_keyed_kernel, dim3((unsigned)(tm * tn)), dim3(256), 0, ctx->stream, M, N, K,
+                       A, lda, B, ldb, keyA, strideA, keyB, strideB, out, beta, (int)tm, (int)tn);
+    QK_HIP(ctx, hipGetLastError());
+    return QK_OK;
+}
+
+int qk_khatri_rao(qk_ctx* ctx, int64_t K, int64_t M, int64_t N, const double* A, int64_t lda,
+                  const double* B, int64_t ldb, double* out) {
+    if (!ctx) return QK_EARG;
+    if (K < 0 || M < 0 || N < 0) return fail(ctx, QK_EARG, "qk_khatri_rao: negative size%s");
+    if (K == 0 || M == 0 || N == 0) return QK_OK;
+    if (!A || !B || !out) return fail(ctx, QK_EARG, "qk_khatri_rao: null buffer%s");
+    QK_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(qk_khatri_rao_kernel, dim3(grid_for(K * M * N, 256)), dim3(256), 0, ctx->stream, K,
+                       M, N, A, lda, B, ldb, out);
+    QK_HIP(ctx, hipGetLastError());
+    return QK_OK;
+}
+
+int qk_gather_rows(qk_ctx* ctx, int64_t R, int64_t width, const int64_t* idx, const double* coef,
+                   const double* src, double* dst) {
+    if (!ctx) return QK_EARG;
+    if (R < 0 || width < 0) return fail(ctx, QK_EARG, "qk_gather_rows: negative size%s");
+    if (R == 0 || width == 0) return QK_OK;
+    if (!idx || !coef || !src || !dst) return fail(ctx, QK_EARG, "qk_gather_rows: null buffer%s");
+    QK_HIP(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(qk_gather_rows_kernel, dim3(grid_for(R * width, 256)), dim3(256), 0, ctx->stream, R,
+                       width, idx, coef, src, dst);
+    QK_HIP(ctx, hipGetLastError());
+    return QK_OK;
+}
+
+}  // extern "C"

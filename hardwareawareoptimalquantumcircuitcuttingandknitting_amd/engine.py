@@ -1,0 +1,500 @@
+"""Device-side orchestration: compiled fragments, batched sweep, dense knit.
+
+Everything numeric here runs in ``libqknit.so`` (HIP, gfx950) through the C ABI
+(``include/qknit.h``); torch is used only for device allocations and stream
+ordering. There is no CPU compute path: without the library or without a GPU
+every entry point raises.
+
+Pipeline of one virtual-circuit run (``run.py:23-71`` in the reference):
+
+1. :func:`sweep_fragment` — per fragment: compile (``fragment_program``),
+   schedule (``sweep_plan``), expand labels into branch jobs, ``qk_sweep``
+   (exact probabilities of every instantiation), ``qk_reduce_labels`` (signed
+   config-bit folding) -> ``q_f [L_f, 2^m_f]``.
+2. :func:`knit_dense` — gather/scale fragment rows per global label
+   (``qk_gather_rows``, or the factored transform), then ``qk_gemm_keyed``
+   (fp64 MFMA) writes the dense distribution at global clbit keys.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from .fragment_program import FragmentProgram, JobTable, build_jobs, compile_fragment
+from .knit_plan import LabelSpace, deposit_keys, factor_vgate
+from .sweep_plan import EncodedProgram, encode
+
+_torch = None
+
+
+def torch():
+    global _torch
+    if _torch is None:
+        import torch as t
+
+        _torch = t
+    return _torch
+
+
+def _ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+# ----------------------------------------------------------------------------- context
+class Context:
+    """One ``qk_ctx`` per (thread, device); ops run on torch's current stream."""
+
+    def __init__(self, device: int = 0):
+        T = torch()
+        if not T.cuda.is_available():
+            raise _lib.QknitError("no HIP device available (torch.cuda.is_available() is False)")
+        self.device = device
+        self.lib = _lib.lib()
+        h = ctypes.c_void_p()
+        _lib.check(None, self.lib.qk_ctx_create(device, ctypes.byref(h)), "qk_ctx_create")
+        self.handle = h
+
+    def bind_stream(self) -> None:
+        s = torch().cuda.current_stream(self.device)
+        self.lib.qk_ctx_set_stream(self.handle, ctypes.c_void_p(s.cuda_stream))
+
+    def check(self, status: int, what: str) -> None:
+        _lib.check(self.handle, status, what)
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.qk_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_tls = threading.local()
+
+
+def get_context(device: int = 0) -> Context:
+    cache = getattr(_tls, "ctx", None)
+    if cache is None:
+        cache = _tls.ctx = {}
+    if device not in cache:
+        cache[device] = Context(device)
+    ctx = cache[device]
+    ctx.bind_stream()
+    return ctx
+
+
+# ----------------------------------------------------------------------------- fragments
+@dataclass
+class DeviceProgram:
+    host: FragmentProgram
+    enc: EncodedProgram
+    ops: object  # torch tensors (device) kept alive
+    groups: object
+    mats: object
+    passes: object  # ctypes array (host)
+    struct: _lib.QkProgram = field(default=None)
+
+    @staticmethod
+    def upload(prog: FragmentProgram, device) -> "DeviceProgram":
+        T = torch()
+        enc = encode(prog)
+        dev = T.device("cuda", device)
+
+        def to_dev(arr, dtype):
+            buf = np.ascontiguousarray(arr).view(np.uint8)
+            t = T.empty(max(buf.size, 8), dtype=T.uint8, device=dev)
+            if buf.size:
+                t[: buf.size].copy_(T.from_numpy(buf.copy()))
+            return t
+
+        ops = to_dev(enc.ops, None)
+        groups = to_dev(enc.groups, None)
+        mats = T.from_numpy(enc.mats.copy()).to(dev)
+        np_pass = enc.passes
+        passes = (_lib.QkPass * len(np_pass))()
+        for i, p in enumerate(np_pass):
+            passes[i].tile_mask = int(p["tile_mask"])
+            passes[i].group_begin = int(p["group_begin"])
+            passes[i].group_end = int(p["group_end"])
+            passes[i].flags = int(p["flags"])
+            passes[i].traced_local = int(p["traced_local"])
+        st = _lib.QkProgram(enc.n, enc.n_eff, enc.m, enc.n_slots, int(enc.packed), len(np_pass),
+                            ctypes.cast(passes, ctypes.POINTER(_lib.QkPass)),
+                            ops.data_ptr(), groups.data_ptr(), mats.data_ptr())
+        return DeviceProgram(prog, enc, ops, groups, mats, passes, st)
+
+
+def jobs_to_device(jobs: JobTable, device):
+    T = torch()
+    dev = T.device("cuda", device)
+    slots = np.ascontiguousarray(jobs.slot_mats).view(np.float64).reshape(jobs.n_jobs, -1)
+    slot_t = T.from_numpy(slots.copy()).to(dev) if slots.size else T.zeros(1, dtype=T.float64, device=dev)
+    sign_t = T.from_numpy(jobs.sign.copy()).to(dev)
+    off_t = T.from_numpy(jobs.label_offsets.copy()).to(dev)
+    return slot_t, sign_t, off_t
+
+
+def sweep_jobs(ctx: Context, dprog: DeviceProgram, slot_t, sign_t, n_jobs: int, pjob=None,
+               workspace=None):
+    """``qk_sweep``: per-job signed probabilities ``[n_jobs, 2^m]``."""
+    T = torch()
+    dev = T.device("cuda", ctx.device)
+    width = 1 << dprog.enc.m
+    if pjob is None:
+        pjob = T.empty((n_jobs, width), dtype=T.float64, device=dev)
+    need = ctypes.c_int64()
+    ctx.check(ctx.lib.qk_sweep_workspace_bytes(ctypes.byref(dprog.struct), n_jobs, ctypes.byref(need)),
+              "qk_sweep_workspace_bytes")
+    if need.value and (workspace is None or workspace.numel() < need.value):
+        workspace = T.empty(need.value, dtype=T.uint8, device=dev)
+    ctx.check(ctx.lib.qk_sweep(ctx.handle, ctypes.byref(dprog.struct), n_jobs, slot_t.data_ptr(),
+                               sign_t.data_ptr(), _ptr(workspace) if need.value else None,
+                               need.value, pjob.data_ptr()), "qk_sweep")
+    return pjob, workspace
+
+
+def reduce_labels(ctx: Context, pjob, off_t, n_labels: int, q=None):
+    T = torch()
+    width = pjob.shape[1]
+    if q is None:
+        q = T.empty((n_labels, width), dtype=T.float64, device=pjob.device)
+    ctx.check(ctx.lib.qk_reduce_labels(ctx.handle, n_labels, off_t.data_ptr(), width,
+                                       pjob.data_ptr(), q.data_ptr()), "qk_reduce_labels")
+    return q
+
+
+# ----------------------------------------------------------------------------- GEMM helpers
+def gemm_keyed(ctx: Context, A, B, keyA=None, keyB=None, out=None, strideA: int = 0,
+               strideB: int = 1, beta: int = 0):
+    """out[kA(i) + kB(j)] (=|+=) sum_k A[k, i] * B[k, j] on the GPU (fp64 MFMA).
+
+    ``kA(i) = keyA[i]`` if a key tensor is given, else ``i * strideA`` (same for B).
+    """
+    K, M = A.shape
+    K2, N = B.shape
+    assert K == K2 and A.dtype == B.dtype and A.is_contiguous() and B.is_contiguous()
+    if keyA is not None:
+        assert keyA.shape[0] == M and keyA.dtype == torch().int64
+    if keyB is not None:
+        assert keyB.shape[0] == N and keyB.dtype == torch().int64
+    ctx.check(ctx.lib.qk_gemm_keyed(ctx.handle, M, N, K, A.data_ptr(), M, B.data_ptr(), N,
+                                    _ptr(keyA), strideA, _ptr(keyB), strideB, out.data_ptr(), beta),
+              "qk_gemm_keyed")
+    return out
+
+
+def khatri_rao(ctx: Context, A, B):
+    T = torch()
+    K, M = A.shape
+    _, N = B.shape
+    out = T.empty((K, M * N), dtype=T.float64, device=A.device)
+    ctx.check(ctx.lib.qk_khatri_rao(ctx.handle, K, M, N, A.data_ptr(), M, B.data_ptr(), N,
+                                    out.data_ptr()), "qk_khatri_rao")
+    return out
+
+
+def gather_rows(ctx: Context, src, idx_t, coef_t):
+    T = torch()
+    R = idx_t.shape[0]
+    width = src.shape[1]
+    out = T.empty((R, width), dtype=T.float64, device=src.device)
+    ctx.check(ctx.lib.qk_gather_rows(ctx.handle, R, width, idx_t.data_ptr(), coef_t.data_ptr(),
+                                     src.data_ptr(), out.data_ptr()), "qk_gather_rows")
+    return out
+
+
+# ----------------------------------------------------------------------------- virtual circuits
+def clbit_indexer(circuit):
+    """Map a clbit of the cut circuit to its global index (cregs in order)."""
+    index = {}
+    i = 0
+    for creg in circuit.cregs:
+        for b in creg:
+            index[b] = i
+            i += 1
+    return lambda c: index[c]
+
+
+@dataclass
+class FragmentState:
+    fragment: object
+    labels: list
+    prog: FragmentProgram
+    dprog: DeviceProgram | None
+    jobs: JobTable | None
+    touches: list
+    dropped: bool = False  # reference skips fragments whose counts cannot be read (run.py:57-58)
+
+
+def prepare_fragments(virt, device: int = 0) -> list[FragmentState]:
+    circ = virt.circuit
+    cl = clbit_indexer(circ)
+    vg = virt.vgate_instructions
+    out = []
+    for frag, fcirc in virt.fragment_circuits.items():
+        if len(frag) == 0:
+            continue
+        prog = compile_fragment(fcirc, frag, cl)
+        labels = virt.get_instance_labels(frag)
+        touches = [bool(set(v.qubits) & set(frag)) for v in vg]
+        jobs = build_jobs(prog, labels)
+        # run.py:49-58 drops a fragment whose get_counts() raises, i.e. when some instance of
+        # it measures nothing at all (no data measurement and no config measurement).
+        dropped = prog.m == 0 and _some_label_unmeasured(prog, labels)
+        dp = None if dropped else DeviceProgram.upload(prog, device)
+        out.append(FragmentState(frag, labels, prog, dp, jobs, touches, dropped))
+    return out
+
+
+def _some_label_unmeasured(prog: FragmentProgram, labels: list) -> bool:
+    from .fragment_program import side_branches
+
+    for label in labels:
+        if all(len(side_branches(s.endpoint, label[s.vgate_idx])) == 1 for s in prog.slots):
+            return True
+    return False
+
+
+def sweep_fragment(ctx: Context, fs: FragmentState, label_range=None):
+    """Signed-folded per-label distributions ``q_f`` of one fragment on the GPU.
+
+    ``label_range=(lo, hi)`` restricts the sweep to fragment labels ``[lo, hi)``
+    (multi-GPU sharding); rows are returned for that range only.
+    """
+    T = torch()
+    jobs = fs.jobs
+    lo, hi = (0, len(fs.labels)) if label_range is None else label_range
+    width = 1 << fs.prog.m
+    if fs.dropped:
+        return T.ones((hi - lo, 1), dtype=T.float64, device=T.device("cuda", ctx.device))
+    j0, j1 = int(jobs.label_offsets[lo]), int(jobs.label_offsets[hi])
+    sub = JobTable(jobs.slot_mats[j0:j1], jobs.sign[j0:j1], jobs.label_offsets[lo : hi + 1] - j0,
+                   jobs.branch_bits[j0:j1])
+    slot_t, sign_t, off_t = jobs_to_device(sub, ctx.device)
+    pjob, _ = sweep_jobs(ctx, fs.dprog, slot_t, sign_t, sub.n_jobs)
+    if sub.n_jobs == hi - lo:  # no branching: jobs are labels
+        return pjob
+    return reduce_labels(ctx, pjob, off_t, hi - lo)
+
+
+@dataclass
+class KnitOperands:
+    """Per-fragment knit operands ``W_f`` (contraction rows) and output clbits."""
+
+    rows: list  # per included fragment: np.int64 [R] row index into q_f
+    coefs: list  # per included fragment: np.float64 [R]
+    transforms: list  # per fragment: None (gather) or dense [R, L_f] matrix (factored)
+    clbits: list  # per included fragment: ascending global clbits of its outcome bits
+    num_terms: int
+
+    def key_table(self, i: int) -> np.ndarray:
+        return deposit_keys(self.clbits[i])
+
+
+def _affine_stride(clbits: list):
+    """Stride if the fragment's clbits are contiguous (key = x << c0), else None."""
+    if not clbits:
+        return 0
+    c0 = clbits[0]
+    return (1 << c0) if list(clbits) == list(range(c0, c0 + len(clbits))) else None
+
+
+def knit_operands(virt, frags: list[FragmentState], factored: bool = False) -> KnitOperands:
+    vg = [v.operation for v in virt.vgate_instructions]
+    space = LabelSpace([g.num_instantiations for g in vg], [g.knit_coefficients() for g in vg])
+    clbits = [[] if fs.dropped else list(fs.prog.clbits) for fs in frags]
+    if not factored or not vg:
+        c = space.coefficients()
+        rows, coefs = [], []
+        for i, fs in enumerate(frags):
+            rows.append(space.fragment_rows(fs.touches))
+            coefs.append(c if i == 0 else np.ones_like(c))
+        return KnitOperands(rows, coefs, [None] * len(frags), clbits, space.num_labels)
+    # factored: per gate rank factorisation, fragment transform = kron over touching gates
+    Ts = []
+    for j in range(len(vg)):
+        eps = _endpoints(virt, j)
+        Ts.append(factor_vgate(eps[0], eps[1], vg[j].knit_coefficients()))
+    ranks = [t[0].shape[0] for t in Ts]
+    transforms = []
+    for fs in frags:
+        W = np.ones((1, 1))
+        sides = _fragment_sides(virt, fs)
+        for j in range(len(vg)):
+            if sides[j] is None:
+                # gate not touching: its rank index is free on this fragment (ones row per r)
+                W = np.kron(W, np.ones((ranks[j], 1)))
+            else:
+                W = np.kron(W, Ts[j][sides[j]])
+        transforms.append(W)
+    return KnitOperands([None] * len(frags), [None] * len(frags), transforms, clbits, int(np.prod(ranks)))
+
+
+def _endpoints(virt, j):
+    out = [None, None]
+    for instr in virt.circuit:
+        op = instr.operation
+        if getattr(op, "vgate_idx", None) == j:
+            out[op.qubit_idx] = op
+    return out
+
+
+def _fragment_sides(virt, fs: FragmentState):
+    sides = [None] * len(virt.vgate_instructions)
+    members = set(fs.fragment)
+    for instr in virt.circuit:
+        op = instr.operation
+        if hasattr(op, "vgate_idx") and instr.qubits[0] in members:
+            if sides[op.vgate_idx] is not None:
+                raise NotImplementedError("both sides of a virtual gate in one fragment")
+            sides[op.vgate_idx] = op.qubit_idx
+    return sides
+
+
+def fragment_operands(ctx: Context, ops: KnitOperands, qs: list) -> list:
+    """Contraction-ready operands ``[num_terms, 2^m_f]`` per fragment (coefficients folded)."""
+    T = torch()
+    dev = T.device("cuda", ctx.device)
+    mats = []
+    for i, q in enumerate(qs):
+        q = q.contiguous()
+        if ops.transforms[i] is not None:
+            W = T.from_numpy(np.ascontiguousarray(ops.transforms[i].T)).to(dev)  # [L_f, R]
+            a = T.empty((W.shape[1], q.shape[1]), dtype=T.float64, device=dev)
+            gemm_keyed(ctx, W, q, out=a, strideA=q.shape[1])
+        else:
+            idx_t = T.from_numpy(ops.rows[i]).to(dev)
+            coef_t = T.from_numpy(ops.coefs[i]).to(dev)
+            a = gather_rows(ctx, q, idx_t, coef_t)
+        mats.append(a)
+    return mats
+
+
+def knit_dense(ctx: Context, virt, frags: list[FragmentState], qs: list, out=None,
+               factored: bool = False, num_clbits: int | None = None, row_block=None):
+    """Dense knit on the GPU: returns the float64 distribution over all meas clbits.
+
+    ``row_block=(lo, hi)`` computes only columns ``[lo, hi)`` of the first
+    contraction operand (output-sharded multi-GPU knit); other keys stay untouched.
+    """
+    T = torch()
+    dev = T.device("cuda", ctx.device)
+    N = virt.circuit.num_clbits if num_clbits is None else num_clbits
+    ops = knit_operands(virt, frags, factored)
+    if out is None:
+        out = T.zeros(1 << N, dtype=T.float64, device=dev)
+    mats = fragment_operands(ctx, ops, qs)
+    if not mats:
+        c = T.from_numpy(LabelSpace([g.operation.num_instantiations for g in virt.vgate_instructions],
+                                    [g.operation.knit_coefficients() for g in virt.vgate_instructions]
+                                    ).coefficients()).to(dev)
+        out[0] = c.sum()
+        return out
+    return contract(ctx, mats, ops.clbits, out, row_block)
+
+
+def contract_order(clbits: list) -> list:
+    """Fragment order for the contraction: the one holding the lowest clbit goes last
+    (it becomes the GEMM's N axis, whose 16 consecutive outcomes land on one 128-B run)."""
+    return sorted(range(len(clbits)), key=lambda i: -(min(clbits[i]) if clbits[i] else 1 << 62))
+
+
+def contract(ctx: Context, mats: list, clbits: list, out, row_block=None):
+    T = torch()
+    dev = out.device
+    order = contract_order(clbits)
+    mats = [mats[i] for i in order]
+    cls = [clbits[i] for i in order]
+
+    def key_arg(c, lo=None, hi=None):
+        st = _affine_stride(c)
+        if st is not None and lo is None:
+            return None, st
+        if st is not None:
+            return T.arange(lo, hi, dtype=T.int64, device=dev) * st, 0
+        k = T.from_numpy(deposit_keys(c)).to(dev)
+        return (k if lo is None else k[lo:hi].contiguous()), 0
+
+    if len(mats) == 1:
+        A = mats[0]
+        if row_block is not None:
+            lo, hi = row_block
+            A = A[:, lo:hi].contiguous()
+            kA, sA = key_arg(cls[0], lo, hi)
+        else:
+            kA, sA = key_arg(cls[0])
+        ones = T.ones((A.shape[0], 1), dtype=T.float64, device=dev)
+        return gemm_keyed(ctx, A.contiguous(), ones, keyA=kA, strideA=sA, keyB=None, strideB=0, out=out)
+    A = mats[0]
+    if len(mats) > 2:
+        kA = T.from_numpy(deposit_keys(cls[0])).to(dev)
+        for B, c in zip(mats[1:-1], cls[1:-1]):
+            A = khatri_rao(ctx, A.contiguous(), B.contiguous())
+            kB = T.from_numpy(deposit_keys(c)).to(dev)
+            kA = (kA.view(1, -1) + kB.view(-1, 1)).reshape(-1)  # index i + j*M
+        sA = 0
+        if row_block is not None:
+            lo, hi = row_block
+            A, kA = A[:, lo:hi], kA[lo:hi].contiguous()
+    elif row_block is not None:
+        lo, hi = row_block
+        A = A[:, lo:hi]
+        kA, sA = key_arg(cls[0], lo, hi)
+    else:
+        kA, sA = key_arg(cls[0])
+    B = mats[-1]
+    kB, sB = key_arg(cls[-1])
+    return gemm_keyed(ctx, A.contiguous(), B.contiguous(), keyA=kA, strideA=sA, keyB=kB, strideB=sB, out=out)
+
+
+def knit_quasi_distrs(virt, results: dict, device: int = 0, factored: bool = False):
+    """GPU knit of reference-shaped inputs ``{fragment: [QuasiDistr per label]}``.
+
+    Config bits (``N + j``) are folded with sign ``(-1)^m`` and fragment keys
+    are compressed to the fragment's measured clbits before the dense knit.
+    Fragments absent from ``results`` are treated as the reference does
+    (skipped = contribute a factor 1).
+    """
+    T = torch()
+    ctx = get_context(device)
+    N = virt.circuit.num_clbits
+    circ = virt.circuit
+    cl = clbit_indexer(circ)
+    vg = virt.vgate_instructions
+    frags, qs = [], []
+    for frag, distrs in results.items():
+        fcirc = virt.fragment_circuits[frag]
+        prog = compile_fragment(fcirc, frag, cl)
+        labels = virt.get_instance_labels(frag)
+        if len(distrs) != len(labels):
+            raise ValueError(f"fragment {frag}: {len(distrs)} results for {len(labels)} labels")
+        clbits = prog.clbits
+        width = 1 << len(clbits)
+        q = np.zeros((len(labels), width), dtype=np.float64)
+        pos = {c: i for i, c in enumerate(clbits)}
+        for li, d in enumerate(distrs):
+            for key, val in d.items():
+                data, cfg = key & ((1 << N) - 1), key >> N
+                x = 0
+                b = data
+                while b:
+                    low = b & -b
+                    c = low.bit_length() - 1
+                    if c not in pos:
+                        raise ValueError(f"key {key} sets clbit {c} not measured by fragment")
+                    x |= 1 << pos[c]
+                    b ^= low
+                q[li, x] += (-1.0) ** bin(cfg).count("1") * val
+        touches = [bool(set(v.qubits) & set(frag)) for v in vg]
+        frags.append(FragmentState(frag, labels, prog, None, None, touches))
+        qs.append(T.from_numpy(q).to(T.device("cuda", device)))
+    out = knit_dense(ctx, virt, frags, qs, factored=factored)
+    return out

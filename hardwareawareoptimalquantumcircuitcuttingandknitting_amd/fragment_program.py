@@ -1,0 +1,291 @@
+"""Fragment compiler: fragment circuit + instance labels -> batched sweep program.
+
+Replaces what the reference does per instance in Python + Aer
+(``virtual_circuit.py:183-213`` builds one instance circuit per label and
+``run.py:42`` ships them to ``AerSimulator``): here ONE program per fragment is
+compiled, and the per-instance differences are reduced to a table of 2x2
+"slot" matrices, one per virtual-gate endpoint per job.
+
+Definitions:
+
+* local qubit order: measured data qubits first, ordered by their global
+  ``meas`` clbit (so the fragment output index ``x_f`` is the low ``m`` bits of
+  the state index and maps to global keys by a bit deposit), then the
+  unmeasured qubits (traced out);
+* a *slot* is one :class:`VirtualGateEndpoint`; instantiation ``i`` of its side
+  is a 1-qubit program ``U_post . [P_m] . U_pre`` with at most one config-bit
+  measurement; a measured side yields two *branches* ``m = 0, 1`` with sign
+  ``(-1)^m`` (the reference's ``split`` + subtract, ``virtual_gates.py:105-124,
+  179-194,262-286``);
+* a *job* is one (label, branch combination); its slot matrices fold the fixed
+  1-qubit gates adjacent to the endpoint; its output is ``sign * |amp|^2``
+  traced over unmeasured qubits; jobs of one label are contiguous and sum to
+  the label's signed-folded distribution ``q_f[label]``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import gates as _g
+from .circuit import CompositeInstruction
+from .virtual_gates import VirtualGateEndpoint
+
+P0 = np.array([[1, 0], [0, 0]], dtype=np.complex128)
+P1 = np.array([[0, 0], [0, 1]], dtype=np.complex128)
+I2 = np.eye(2, dtype=np.complex128)
+
+
+class UnsupportedCircuit(ValueError):
+    pass
+
+
+@dataclass
+class HostOp:
+    kind: str  # "u1" | "u2" | "slot"
+    qubits: tuple
+    mat: np.ndarray | None = None
+    slot: int = -1
+
+
+@dataclass
+class SlotSpec:
+    vgate_idx: int
+    side: int
+    qubit: int  # local qubit
+    endpoint: VirtualGateEndpoint
+    pre: np.ndarray = field(default_factory=lambda: I2.copy())
+    post: np.ndarray = field(default_factory=lambda: I2.copy())
+
+
+@dataclass
+class FragmentProgram:
+    n: int
+    m: int
+    clbits: list  # global meas clbit for local output bit i, ascending
+    ops: list
+    slots: list
+    qubit_order: list  # fragment Qubit objects in local order
+
+    @property
+    def num_slots(self) -> int:
+        return len(self.slots)
+
+
+def _op_matrix(op) -> np.ndarray:
+    if hasattr(op, "to_matrix"):
+        try:
+            return np.asarray(op.to_matrix(), dtype=np.complex128)
+        except Exception:  # qiskit ops without a matrix fall back to the table
+            pass
+    return _g.gate_matrix(op.name, getattr(op, "params", ()))
+
+
+def _flatten(instructions, qmap_fn):
+    """Yield (op, local qubit tuple, clbit tuple) with composites inlined."""
+    for instr in instructions:
+        op = instr.operation
+        if isinstance(op, CompositeInstruction):
+            d = op.definition
+            inner_q = [qmap_fn(q) for q in instr.qubits]
+            sub = [(s.operation, tuple(inner_q[d.find_qubit(q)] for q in s.qubits),
+                    tuple(instr.clbits[d.find_clbit(c)] for c in s.clbits)) for s in d]
+            for o, qs, cs in sub:
+                yield o, qs, cs
+        else:
+            yield op, tuple(qmap_fn(q) for q in instr.qubits), tuple(instr.clbits)
+
+
+def compile_fragment(frag_circuit, fragment, clbit_index) -> FragmentProgram:
+    """Compile one fragment circuit (endpoints still in place).
+
+    ``clbit_index(clbit) -> int`` maps a classical bit to its global index in
+    the ``meas``-first clbit order of the cut circuit.
+    """
+    frag_qubits = list(fragment)
+    n = len(frag_qubits)
+    fidx = {q: i for i, q in enumerate(frag_qubits)}
+
+    # -- pass 1: collect raw ops in fragment-qubit indices, find final measurements
+    raw = []
+    measured_at = {}  # frag qubit -> (position in raw, global clbit)
+    for op, qs, cs in _flatten(frag_circuit.data, lambda q: fidx[q]):
+        name = getattr(op, "name", "")
+        if isinstance(op, (VirtualGateEndpoint, BranchMeasure)):
+            raw.append(("slot", qs, op))
+        elif name == "measure":
+            q = qs[0]
+            if q in measured_at:
+                raise UnsupportedCircuit("a qubit is measured twice")
+            measured_at[q] = (len(raw), clbit_index(cs[0]))
+            raw.append(("measure", qs, None))
+        elif name in _g.NON_UNITARY_NOOPS or name == "barrier" or getattr(op, "num_qubits", 1) == 0:
+            continue
+        elif name == "reset":
+            raise UnsupportedCircuit("reset is not supported")
+        else:
+            nq = len(qs)
+            if nq not in (1, 2):
+                raise UnsupportedCircuit(f"{nq}-qubit gate '{name}' is not supported (decompose first)")
+            raw.append(("u1" if nq == 1 else "u2", qs, _op_matrix(op)))
+    for q, (pos, _) in measured_at.items():
+        for kind, qs, _ in raw[pos + 1 :]:
+            if q in qs:
+                raise UnsupportedCircuit("operations after a data measurement are not supported")
+    clb = [c for _, c in measured_at.values()]
+    if len(set(clb)) != len(clb):
+        raise UnsupportedCircuit("two qubits measured into one clbit")
+
+    # -- local order: measured (by clbit) then unmeasured (by fragment index)
+    meas_sorted = sorted(measured_at.items(), key=lambda kv: kv[1][1])
+    order = [q for q, _ in meas_sorted] + [q for q in range(n) if q not in measured_at]
+    loc = {q: i for i, q in enumerate(order)}
+    m = len(meas_sorted)
+    clbits = [c for _, (_, c) in meas_sorted]
+
+    # -- pass 2: fuse 1-qubit runs, build slots
+    ops: list[HostOp] = []
+    slots: list[SlotSpec] = []
+    pending: dict[int, np.ndarray] = {}
+
+    def flush(q):
+        mat = pending.pop(q, None)
+        if mat is not None and not _g.is_identity_up_to_phase(mat):
+            ops.append(HostOp("u1", (q,), mat))
+
+    for kind, qs, payload in raw:
+        lq = tuple(loc[q] for q in qs)
+        if kind == "measure":
+            continue
+        if kind == "u1":
+            q = lq[0]
+            pending[q] = payload @ pending.get(q, I2)
+        elif kind == "u2":
+            for q in lq:
+                flush(q)
+            ops.append(HostOp("u2", lq, payload))
+        else:  # slot
+            q = lq[0]
+            flush(q)
+            ep = payload
+            slots.append(SlotSpec(ep.vgate_idx, ep.qubit_idx, q, ep))
+            ops.append(HostOp("slot", lq, None, len(slots) - 1))
+    for q in list(pending):
+        flush(q)
+
+    # -- pass 3: absorb fixed 1q gates adjacent (per qubit) to a slot into it
+    _absorb_into_slots(ops, slots)
+    return FragmentProgram(n=n, m=m, clbits=clbits, ops=ops, slots=slots,
+                           qubit_order=[frag_qubits[q] for q in order])
+
+
+def _absorb_into_slots(ops: list, slots: list) -> None:
+    dead = set()
+    for i, op in enumerate(ops):
+        if op.kind != "slot":
+            continue
+        q = op.qubits[0]
+        s = slots[op.slot]
+        # previous op on q
+        for j in range(i - 1, -1, -1):
+            if j in dead or q not in ops[j].qubits:
+                continue
+            if ops[j].kind == "u1":
+                s.pre = s.pre @ ops[j].mat  # applied before the slot
+                dead.add(j)
+            break
+        for j in range(i + 1, len(ops)):
+            if j in dead or q not in ops[j].qubits:
+                continue
+            if ops[j].kind == "u1":
+                s.post = ops[j].mat @ s.post  # applied after the slot
+                dead.add(j)
+            break
+    ops[:] = [op for i, op in enumerate(ops) if i not in dead]
+
+
+# ---------------------------------------------------------------------------- jobs
+class BranchMeasure:
+    """Mid-circuit measurement of a plain instance circuit (no sign folding).
+
+    ``vgate_idx`` is the branch index (bit of ``JobTable.branch_bits``),
+    ``clbit`` the global clbit the outcome is written to.
+    """
+
+    name = "branch_measure"
+    num_qubits = 1
+
+    def __init__(self, branch_idx: int, clbit: int):
+        self.vgate_idx = branch_idx
+        self.qubit_idx = 0
+        self.clbit = clbit
+
+
+def side_branches(endpoint, inst_id: int) -> list[tuple[np.ndarray, float]]:
+    """Branches ``(matrix, sign)`` of one endpoint side for instantiation ``inst_id``."""
+    if isinstance(endpoint, BranchMeasure):
+        return [(P0.copy(), 1.0), (P1.copy(), 1.0)]
+    side = endpoint.side_circuit(inst_id)
+    pre, post, measured = I2.copy(), I2.copy(), False
+    for instr in side.data:
+        name = instr.operation.name
+        if name == "measure":
+            if measured:
+                raise UnsupportedCircuit("two config measurements on one side")
+            measured = True
+            continue
+        if name == "barrier":
+            continue
+        mat = _op_matrix(instr.operation)
+        if measured:
+            post = mat @ post
+        else:
+            pre = mat @ pre
+    if not measured:
+        return [(post @ pre, 1.0)]
+    return [(post @ P0 @ pre, 1.0), (post @ P1 @ pre, -1.0)]
+
+
+@dataclass
+class JobTable:
+    slot_mats: np.ndarray  # [n_jobs, n_slots, 2, 2] complex128
+    sign: np.ndarray  # [n_jobs] float64
+    label_offsets: np.ndarray  # [n_labels + 1] int64
+    branch_bits: np.ndarray  # [n_jobs] int64: config-bit outcomes (bit j = vgate j)
+
+    @property
+    def n_jobs(self) -> int:
+        return int(self.sign.shape[0])
+
+
+def build_jobs(prog: FragmentProgram, labels: list) -> JobTable:
+    """Expand labels into branch jobs (labels in the given order, jobs contiguous)."""
+    ns = prog.num_slots
+    cache: dict = {}
+    mats, signs, offs, bits = [], [], [0], []
+    for label in labels:
+        per_slot = []
+        for s in prog.slots:
+            inst = 0 if isinstance(s.endpoint, BranchMeasure) else label[s.vgate_idx]
+            key = (id(s), inst)
+            if key not in cache:
+                cache[key] = [(s.post @ m @ s.pre, sg) for m, sg in side_branches(s.endpoint, inst)]
+            per_slot.append(cache[key])
+        # Cartesian product over slots, last slot fastest
+        combos = [((), 1.0, 0)]
+        for si, br in enumerate(per_slot):
+            vg = prog.slots[si].vgate_idx
+            combos = [
+                (c + (m,), sg * s2, b | ((1 << vg) if (len(br) == 2 and k == 1) else 0))
+                for c, sg, b in combos
+                for k, (m, s2) in enumerate(br)
+            ]
+        for c, sg, b in combos:
+            mats.append(np.stack(c) if ns else np.zeros((0, 2, 2), np.complex128))
+            signs.append(sg)
+            bits.append(b)
+        offs.append(len(signs))
+    slot_mats = np.stack(mats) if mats else np.zeros((0, ns, 2, 2), np.complex128)
+    return JobTable(slot_mats.reshape(len(signs), ns, 2, 2), np.asarray(signs, np.float64),
+                    np.asarray(offs, np.int64), np.asarray(bits, np.int64))

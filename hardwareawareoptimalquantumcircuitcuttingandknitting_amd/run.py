@@ -1,0 +1,99 @@
+"""``run_virtual_circuit``: the knitting hot path, MI355X-native.
+
+Drop-in for ``third_party/qvm/qvm/run.py:23-71``: same name, same arguments,
+same return shape ``(dict[int, float], RunTimeInfo)``. Differences, by design:
+
+* instances are simulated exactly (fp64 statevector, HIP) instead of being
+  sampled with ``shots`` (``run.py:42``); ``shots`` only matters for fragments
+  whose backend was replaced by a foreign (e.g. qiskit-aer) backend, which are
+  run through the reference's own counts path;
+* the knit is one dense fp64 MFMA contraction; ``QuasiDistr``'s ``ACCURACY``
+  truncation is applied once to the final distribution instead of after every
+  intermediate dict operation, then ``nearest_probability_distribution``
+  (``quasi_distr.py:28-43``) as the reference does at ``run.py:71``;
+* ``dense=True`` returns the full distribution as a device tensor (needed for
+  32-bit outputs: 2^32 fp64 = 34.4 GB cannot be a Python dict).
+
+Timing split (``RunTimeInfo``) follows ``run.py:35,60,65-67``: ``run_time``
+covers instance preparation + simulation, ``knit_time`` the contraction.
+"""
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass
+from time import perf_counter
+
+import numpy as np
+
+from . import engine
+from .backend import MI355XBackend
+from .quasi_distr import QuasiDistr
+from .virtual_circuit import VirtualCircuit, generate_instantiations
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class RunTimeInfo:
+    run_time: float
+    knit_time: float
+
+
+def _sync(device: int) -> None:
+    engine.torch().cuda.synchronize(device)
+
+
+def _foreign_fragment(virt: VirtualCircuit, fs: engine.FragmentState, backend, shots: int, device: int):
+    """Reference counts path for a fragment bound to a non-MI355X backend (run.py:36-58)."""
+    T = engine.torch()
+    N = virt.circuit.num_clbits
+    circuits = generate_instantiations(virt.fragment_circuits[fs.fragment], fs.labels)
+    counts = backend.run(circuits, shots=shots).result().get_counts()
+    counts = [counts] if isinstance(counts, dict) else counts
+    pos = {c: i for i, c in enumerate(fs.prog.clbits)}
+    q = np.zeros((len(fs.labels), 1 << len(pos)), dtype=np.float64)
+    for li, c in enumerate(counts):
+        for key, val in QuasiDistr.from_counts(c).items():
+            data, cfg = key & ((1 << N) - 1), key >> N
+            x = 0
+            while data:
+                low = data & -data
+                x |= 1 << pos[low.bit_length() - 1]
+                data ^= low
+            q[li, x] += (-1.0) ** bin(cfg).count("1") * val
+    return T.from_numpy(q).to(T.device("cuda", device))
+
+
+def run_virtual_circuit_dense(virt: VirtualCircuit, shots: int = 20000, *, device: int = 0,
+                              factored: bool = False, out=None):
+    """Sweep + knit; returns ``(dense fp64 tensor [2^N] on device, RunTimeInfo)``."""
+    ctx = engine.get_context(device)
+    log.info("Running virtualizer with %d %s fragments and %d vgates...",
+             len(virt.fragment_circuits),
+             tuple(len(f) for f in virt.fragment_circuits), len(virt.vgate_instructions))
+    now = perf_counter()
+    frags = engine.prepare_fragments(virt, device)
+    qs = []
+    for fs in frags:
+        backend = virt.get_backend(fs.fragment)
+        if isinstance(backend, MI355XBackend):
+            qs.append(engine.sweep_fragment(ctx, fs))
+        else:
+            qs.append(_foreign_fragment(virt, fs, backend, shots, device))
+    _sync(device)
+    run_time = perf_counter() - now
+    now = perf_counter()
+    dense = engine.knit_dense(ctx, virt, frags, qs, out=out, factored=factored)
+    _sync(device)
+    knit_time = perf_counter() - now
+    log.info("Knitted in %.2fs.", knit_time)
+    return dense, RunTimeInfo(run_time, knit_time)
+
+
+def run_virtual_circuit(virt: VirtualCircuit, shots: int = 20000, *, device: int = 0,
+                        dense: bool = False, factored: bool = False):
+    """Reference-compatible entry point (``run.py:23-71``)."""
+    out, info = run_virtual_circuit_dense(virt, shots, device=device, factored=factored)
+    if dense:
+        return out, info
+    return QuasiDistr.from_dense(out).nearest_probability_distribution(), info

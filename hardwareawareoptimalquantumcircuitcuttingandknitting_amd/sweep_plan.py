@@ -1,0 +1,315 @@
+"""Tile/pass/fiber schedule of a fragment program for the HIP sweep kernel.
+
+The kernel (``csrc/qknit.hip``, ``qk_sweep_pass``) processes a *tile* of
+``2^12`` complex128 amplitudes (64 KiB) per 256-thread workgroup in LDS:
+
+* PACKED mode (``n_eff <= 12``): a tile holds ``2^(12-n_eff)`` whole jobs, so a
+  fragment is swept in ONE launch with no statevector traffic to HBM at all;
+* SPLIT mode (``n > 12``): a tile holds 12 of the ``n`` state bits of one job
+  (always including state bits ``0..LOW_BITS-1`` so HBM accesses are
+  contiguous runs); ops are scheduled into *passes*, each of which can only
+  touch its tile bits except through diagonal action (controls, phases), which
+  is evaluated from the fixed non-tile bits.
+
+Inside a pass, ops are cut into *groups* of at most 4 tile positions (the
+*fiber*); each thread loads the 16 amplitudes of its fiber from LDS into
+registers, applies every op of the group in registers, and writes them back
+(one LDS round trip per group instead of per gate).
+
+This module turns a :class:`FragmentProgram` into the flat arrays the C-ABI
+takes (``include/qknit.h``: ``qk_op``, ``qk_group``, ``qk_pass``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .fragment_program import FragmentProgram, HostOp
+
+TILE_BITS = 12
+FIBER_BITS = 4
+LOW_BITS = 5  # state bits always resident in a SPLIT tile (512-B contiguous runs)
+
+# op kinds (must match qknit.h)
+K_U1, K_D1, K_SLOT, K_U2, K_D2, K_CX, K_SWAP, K_SCALE = range(8)
+
+OP_DTYPE = np.dtype([("kind", "<i4"), ("a", "<i4"), ("b", "<i4"), ("e1", "<i4"),
+                     ("e2", "<i4"), ("slot", "<i4"), ("mat", "<i4"), ("pad", "<i4")])
+GROUP_DTYPE = np.dtype([("pos", "<i4", (4,)), ("op_begin", "<i4"), ("op_end", "<i4"),
+                        ("pad", "<i4", (2,))])
+PASS_DTYPE = np.dtype([("tile_mask", "<u8"), ("group_begin", "<i4"), ("group_end", "<i4"),
+                       ("flags", "<i4"), ("traced_local", "<u4")])
+PASS_INIT, PASS_FINAL = 1, 2
+
+
+# ----------------------------------------------------------------------------- analysis
+def _diag_qubits(op: HostOp) -> set:
+    """Qubits on which the op acts diagonally (it commutes with Z there)."""
+    if op.kind == "slot":
+        return set()
+    m = op.mat
+    if op.kind == "u1":
+        return {op.qubits[0]} if _is_diag(m) else set()
+    out = set()
+    # 4x4 little-endian on (q0, q1): index b0 + 2 b1
+    z0 = np.diag([1, -1, 1, -1]).astype(np.complex128)
+    z1 = np.diag([1, 1, -1, -1]).astype(np.complex128)
+    if np.allclose(m @ z0, z0 @ m, atol=1e-15, rtol=0):
+        out.add(op.qubits[0])
+    if np.allclose(m @ z1, z1 @ m, atol=1e-15, rtol=0):
+        out.add(op.qubits[1])
+    return out
+
+
+def _is_diag(m: np.ndarray) -> bool:
+    return bool(np.all(m[~np.eye(m.shape[0], dtype=bool)] == 0))
+
+
+def op_need(op: HostOp) -> set:
+    return set(op.qubits) - _diag_qubits(op)
+
+
+# ----------------------------------------------------------------------------- passes
+@dataclass
+class Pass:
+    tile: list  # sorted state bits resident in the tile (SPLIT); all bits (PACKED)
+    ops: list  # HostOps in order
+
+
+def schedule_passes(prog: FragmentProgram) -> list[Pass]:
+    n = prog.n
+    if n <= TILE_BITS:
+        return [Pass(list(range(n)), list(prog.ops))]
+    traced = set(range(prog.m, n))
+    if len(traced) > TILE_BITS - LOW_BITS:
+        raise NotImplementedError("more traced qubits than a tile can hold")
+    remaining = list(prog.ops)
+    passes: list[Pass] = []
+    while remaining:
+        tile = set(range(LOW_BITS))
+        taken, blocked, rest = [], set(), []
+        for op in remaining:
+            qs = set(op.qubits)
+            need = op_need(op)
+            if qs & blocked:
+                blocked |= qs
+                rest.append(op)
+                continue
+            if need <= tile or len(tile | need) <= TILE_BITS:
+                tile |= need
+                taken.append(op)
+            else:
+                blocked |= qs
+                rest.append(op)
+        if not taken:  # cannot happen: first op always fits (need <= 2 qubits)
+            raise RuntimeError("pass scheduler made no progress")
+        passes.append(Pass(sorted(tile), taken))
+        remaining = rest
+    if not passes:
+        passes.append(Pass(sorted(set(range(LOW_BITS))), []))
+    # final pass must hold every traced qubit; prefer swapping in unused bits
+    last = passes[-1]
+    tile = set(last.tile)
+    used = set(range(LOW_BITS))
+    for op in last.ops:
+        used |= op_need(op)
+    for q in traced - tile:
+        if len(tile) < TILE_BITS:
+            tile.add(q)
+            continue
+        spare = sorted(tile - used - traced)
+        if spare:
+            tile.discard(spare[-1])
+            tile.add(q)
+        else:
+            passes.append(Pass([], []))
+            tile = set(range(LOW_BITS)) | traced
+            break
+    passes[-1].tile = sorted(tile)
+    # fill every tile to exactly TILE_BITS bits (lowest unused first)
+    for p in passes:
+        t = set(p.tile)
+        for q in range(n):
+            if len(t) >= TILE_BITS:
+                break
+            t.add(q)
+        p.tile = sorted(t)
+    return passes
+
+
+# ----------------------------------------------------------------------------- encoding
+@dataclass
+class EncodedProgram:
+    n: int  # fragment qubits
+    n_eff: int  # padded width (>= FIBER_BITS)
+    m: int
+    n_slots: int
+    packed: bool
+    ops: np.ndarray  # OP_DTYPE
+    groups: np.ndarray  # GROUP_DTYPE
+    passes: np.ndarray  # PASS_DTYPE
+    mats: np.ndarray  # float64, interleaved complex
+    n_host_ops: int
+
+    @property
+    def jobs_per_tile(self) -> int:
+        return 1 << (TILE_BITS - self.n_eff) if self.packed else 1
+
+    @property
+    def tiles_per_job(self) -> int:
+        return 1 if self.packed else 1 << (self.n - TILE_BITS)
+
+
+class _Mats:
+    def __init__(self):
+        self.buf: list = []
+
+    def add(self, *mats) -> int:
+        off = len(self.buf)
+        for m in mats:
+            for z in np.asarray(m, dtype=np.complex128).ravel():
+                self.buf.extend((float(z.real), float(z.imag)))
+        return off
+
+
+def _swap_order4(m: np.ndarray) -> np.ndarray:
+    """Re-express a 4x4 (q0,q1) matrix in (q1,q0) order."""
+    p = [0, 2, 1, 3]
+    return m[np.ix_(p, p)]
+
+
+def _is_cx(m: np.ndarray) -> bool:
+    ref = np.array([[1, 0, 0, 0], [0, 0, 0, 1], [0, 0, 1, 0], [0, 1, 0, 0]], dtype=np.complex128)
+    return bool(np.array_equal(m, ref))
+
+
+def _is_swap(m: np.ndarray) -> bool:
+    ref = np.array([[1, 0, 0, 0], [0, 0, 1, 0], [0, 1, 0, 0], [0, 0, 0, 1]], dtype=np.complex128)
+    return bool(np.array_equal(m, ref))
+
+
+def _block(m: np.ndarray, ctrl_pos: int, bit: int) -> np.ndarray:
+    """2x2 block acting on the other qubit when qubit ``ctrl_pos`` (0/1) has value ``bit``."""
+    if ctrl_pos == 0:
+        idx = [bit, bit + 2]  # b0 fixed, b1 varies
+    else:
+        idx = [2 * bit, 2 * bit + 1]
+    return m[np.ix_(idx, idx)]
+
+
+def _emit(op: HostOp, fib: dict, mats: _Mats) -> list:
+    """Encode one host op given the group fiber map (state bit -> fiber index)."""
+    rec = lambda kind, a=-1, b=-1, e1=-1, e2=-1, slot=-1, mat=-1: (kind, a, b, e1, e2, slot, mat, 0)
+    if op.kind == "slot":
+        return [rec(K_SLOT, a=fib[op.qubits[0]], slot=op.slot)]
+    if op.kind == "u1":
+        q = op.qubits[0]
+        m = op.mat
+        if _is_diag(m):
+            d = np.diag(m)
+            if q in fib:
+                return [rec(K_D1, a=fib[q], mat=mats.add(d))]
+            return [rec(K_SCALE, e1=q, mat=mats.add([d[0], d[1], d[0], d[1]]))]
+        return [rec(K_U1, a=fib[q], mat=mats.add(m))]
+    # two-qubit
+    q0, q1 = op.qubits
+    m = op.mat
+    diag = _diag_qubits(op)
+    if _is_diag(m):
+        d = np.diag(m)  # index b0 + 2 b1
+        if q0 in fib and q1 in fib:
+            a, b = fib[q0], fib[q1]
+            if a > b:
+                a, b, d = b, a, d[[0, 2, 1, 3]]
+            return [rec(K_D2, a=a, b=b, mat=mats.add(d))]
+        if q0 in fib:  # q1 external: variants by b1
+            return [rec(K_D1, a=fib[q0], e1=q1, mat=mats.add(d[[0, 1]], d[[2, 3]]))]
+        if q1 in fib:  # q0 external: variants by b0
+            return [rec(K_D1, a=fib[q1], e1=q0, mat=mats.add(d[[0, 2]], d[[1, 3]]))]
+        # both external: scalar selected by (b0, b1) -> index e1bit + 2 e2bit
+        return [rec(K_SCALE, e1=q0, e2=q1, mat=mats.add(d))]
+    if q0 in diag or q1 in diag:
+        c_pos = 0 if q0 in diag else 1
+        ctrl, tgt = (q0, q1) if c_pos == 0 else (q1, q0)
+        if ctrl in fib:
+            a, b = fib[ctrl], fib[tgt]
+            mm = m if c_pos == 0 else _swap_order4(m)  # now ctrl = first
+            if _is_cx(mm):
+                return [rec(K_CX, a=a, b=b)]
+            if a > b:
+                a, b, mm = b, a, _swap_order4(mm)
+            return [rec(K_U2, a=a, b=b, mat=mats.add(mm))]
+        m0, m1 = _block(m, c_pos, 0), _block(m, c_pos, 1)
+        if _is_diag(m0) and _is_diag(m1):
+            return [rec(K_D1, a=fib[tgt], e1=ctrl, mat=mats.add(np.diag(m0), np.diag(m1)))]
+        return [rec(K_U1, a=fib[tgt], e1=ctrl, mat=mats.add(m0, m1))]
+    a, b = fib[q0], fib[q1]
+    if _is_swap(m):
+        return [rec(K_SWAP, a=min(a, b), b=max(a, b))]
+    mm = m
+    if a > b:
+        a, b, mm = b, a, _swap_order4(m)
+    return [rec(K_U2, a=a, b=b, mat=mats.add(mm))]
+
+
+def encode(prog: FragmentProgram) -> EncodedProgram:
+    n = prog.n
+    packed = n <= TILE_BITS
+    n_eff = max(n, FIBER_BITS) if packed else n
+    passes = schedule_passes(prog)
+    mats = _Mats()
+    ops_out, groups_out, passes_out = [], [], []
+    for pi, p in enumerate(passes):
+        tile = list(range(n_eff)) if packed else p.tile
+        local = {q: i for i, q in enumerate(tile)}  # state bit -> local position
+        n_local = n_eff if packed else TILE_BITS
+        g_begin = len(groups_out)
+        # cut the pass into fiber groups
+        cur: list = []
+        cur_need: set = set()
+
+        def close():
+            if not cur:
+                return
+            pos = sorted(local[q] for q in cur_need)
+            for cand in range(n_local):  # pad the fiber to 4 positions
+                if len(pos) >= FIBER_BITS:
+                    break
+                if cand not in pos:
+                    pos.append(cand)
+            pos = sorted(pos)
+            fib = {tile[p_]: i for i, p_ in enumerate(pos)}
+            ob = len(ops_out)
+            for op in cur:
+                ops_out.extend(_emit(op, fib, mats))
+            groups_out.append((pos, ob, len(ops_out), (0, 0)))
+
+        for op in p.ops:
+            need = op_need(op)
+            if len(cur_need | need) > FIBER_BITS:
+                close()
+                cur, cur_need = [], set()
+            cur.append(op)
+            cur_need |= need
+        close()
+        flags = (PASS_INIT if pi == 0 else 0) | (PASS_FINAL if pi == len(passes) - 1 else 0)
+        traced = 0
+        if flags & PASS_FINAL:
+            for q in range(prog.m, n_eff):
+                traced |= 1 << local[q]
+        tile_mask = 0
+        for q in tile:
+            tile_mask |= 1 << q
+        passes_out.append((tile_mask, g_begin, len(groups_out), flags, traced))
+    ops_arr = np.array(ops_out, dtype=OP_DTYPE) if ops_out else np.zeros(0, OP_DTYPE)
+    grp_arr = np.zeros(len(groups_out), GROUP_DTYPE)
+    for i, (pos, ob, oe, _) in enumerate(groups_out):
+        grp_arr[i]["pos"] = pos
+        grp_arr[i]["op_begin"] = ob
+        grp_arr[i]["op_end"] = oe
+    pass_arr = np.array(passes_out, dtype=PASS_DTYPE)
+    mat_arr = np.asarray(mats.buf if mats.buf else [0.0], dtype=np.float64)
+    return EncodedProgram(n=n, n_eff=n_eff, m=prog.m, n_slots=prog.num_slots, packed=packed,
+                          ops=ops_arr, groups=grp_arr, passes=pass_arr, mats=mat_arr,
+                          n_host_ops=len(prog.ops))

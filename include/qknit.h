@@ -1,0 +1,123 @@
+/*
+ * qknit.h — C ABI of the MI355X (gfx950) circuit-knitting engine, libqknit.so.
+ *
+ * Drop-in boundary for the reference's knitting hot path
+ * (thangktran/HardwareAwareOptimalQuantumCircuitCuttingAndKnitting):
+ *
+ *   qk_sweep         replaces the simulator plug  `virt.get_backend(frag).run(instantiations,
+ *                    shots)` + `job.result().get_counts()` + `QuasiDistr.from_counts`
+ *                    (third_party/qvm/qvm/run.py:36-58, quasi_distr.py:12-20): exact
+ *                    per-instance distributions of every cut instantiation of one fragment,
+ *                    batched, one launch per pass.
+ *   qk_reduce_labels folds the config-bit branches of each instance label with their signs
+ *                    (the `split` + subtract of virtual_gates.py:105-124,179-194,262-286).
+ *   qk_gemm_keyed    replaces the merge + per-vgate knit (virtual_circuit.py:50-68,165-171,
+ *                    216-228; quasi_distr.py:55-60): a dense fp64 MFMA contraction over the
+ *                    instance-label axis with the output scattered to global clbit keys.
+ *   qk_khatri_rao    row-wise outer product (3+ fragment knits).
+ *   qk_gather_rows   label gather + coefficient scaling of fragment rows.
+ *
+ * Conventions: every function returns 0 on success and a QK_E* code otherwise (message via
+ * qk_last_error). Sizes are int64_t. All data buffers are DEVICE pointers owned by the caller,
+ * except qk_program.passes (HOST). Complex values are interleaved (re, im) doubles.
+ * One context per (thread, device); a context holds one HIP stream and no other mutable
+ * global state, so distinct contexts may be driven concurrently from different threads.
+ */
+#ifndef QKNIT_H
+#define QKNIT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QK_OK 0
+#define QK_EARG 1     /* invalid argument / shape */
+#define QK_EHIP 2     /* HIP runtime error */
+#define QK_ESTATE 3   /* invalid context state */
+
+#define QK_TILE_BITS 12
+#define QK_FIBER_BITS 4
+
+/* op kinds (sweep_plan.py K_*) */
+enum { QK_U1 = 0, QK_D1 = 1, QK_SLOT = 2, QK_U2 = 3, QK_D2 = 4, QK_CX = 5, QK_SWAP = 6, QK_SCALE = 7 };
+
+typedef struct qk_op {      /* 32 bytes */
+    int32_t kind;
+    int32_t a, b;            /* fiber positions (0..3) */
+    int32_t e1, e2;          /* external state bits selecting a variant (-1: none) */
+    int32_t slot;            /* QK_SLOT: slot index into the job's slot table */
+    int32_t mat;             /* offset (doubles) into qk_program.mats */
+    int32_t pad;
+} qk_op;
+
+typedef struct qk_group {   /* 32 bytes: one fiber (4 tile positions) and its ops */
+    int32_t pos[4];
+    int32_t op_begin, op_end;
+    int32_t pad[2];
+} qk_group;
+
+typedef struct qk_pass {    /* 24 bytes */
+    uint64_t tile_mask;      /* state bits resident in the tile (SPLIT mode) */
+    int32_t group_begin, group_end;
+    int32_t flags;           /* 1: INIT (state starts as |0..0>), 2: FINAL (emit probabilities) */
+    uint32_t traced_local;   /* FINAL: tile positions that are traced out */
+} qk_pass;
+
+typedef struct qk_program {
+    int32_t n;               /* fragment qubits */
+    int32_t n_eff;           /* padded width (PACKED: >= 4) */
+    int32_t m;               /* measured qubits = local qubits 0..m-1 */
+    int32_t n_slots;         /* virtual-gate endpoints in this fragment */
+    int32_t packed;          /* 1: n_eff <= 12, whole jobs per tile */
+    int32_t n_passes;
+    const qk_pass* passes;   /* HOST */
+    const qk_op* ops;        /* DEVICE */
+    const qk_group* groups;  /* DEVICE */
+    const double* mats;      /* DEVICE */
+} qk_program;
+
+typedef struct qk_ctx qk_ctx;
+
+int qk_ctx_create(int device, qk_ctx** out);
+int qk_ctx_destroy(qk_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch's current stream); NULL restores the own stream. */
+int qk_ctx_set_stream(qk_ctx* ctx, void* hip_stream);
+int qk_ctx_synchronize(qk_ctx* ctx);
+const char* qk_last_error(qk_ctx* ctx);
+const char* qk_version(void);
+
+/* Workspace (bytes) qk_sweep needs for n_jobs jobs of prog (0 in PACKED mode). */
+int qk_sweep_workspace_bytes(const qk_program* prog, int64_t n_jobs, int64_t* bytes);
+
+/* Batched exact sweep of one fragment.
+ *   job_slots : [n_jobs][n_slots][2][2] complex (8 doubles per slot)
+ *   job_sign  : [n_jobs]
+ *   pjob      : [n_jobs][2^m] out: sign * P(x), traced over unmeasured qubits */
+int qk_sweep(qk_ctx* ctx, const qk_program* prog, int64_t n_jobs, const double* job_slots,
+             const double* job_sign, void* workspace, int64_t workspace_bytes, double* pjob);
+
+/* q[l][x] = sum_{j in [offsets[l], offsets[l+1])} pjob[j][x]   (offsets: DEVICE, n_labels+1) */
+int qk_reduce_labels(qk_ctx* ctx, int64_t n_labels, const int64_t* offsets, int64_t width,
+                     const double* pjob, double* q);
+
+/* out[keyA[i] + keyB[j]] (=|+=) sum_k A[k*lda + i] * B[k*ldb + j],  i < M, j < N.
+ * A NULL key table means an affine one: keyA[i] = i*strideA, keyB[j] = j*strideB.
+ * beta: 0 overwrite, 1 accumulate. */
+int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A, int64_t lda,
+                  const double* B, int64_t ldb, const int64_t* keyA, int64_t strideA,
+                  const int64_t* keyB, int64_t strideB, double* out, int beta);
+
+/* out[k][i + j*M] = A[k*lda + i] * B[k*ldb + j] */
+int qk_khatri_rao(qk_ctx* ctx, int64_t K, int64_t M, int64_t N, const double* A, int64_t lda,
+                  const double* B, int64_t ldb, double* out);
+
+/* dst[r][x] = coef[r] * src[idx[r]][x]  (width columns, rows R) */
+int qk_gather_rows(qk_ctx* ctx, int64_t R, int64_t width, const int64_t* idx, const double* coef,
+                   const double* src, double* dst);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QKNIT_H */

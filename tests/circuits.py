@@ -1,0 +1,123 @@
+"""Synthetic cut circuits for parity tests (seeded, small).
+
+Each builder returns ``(uncut circuit, cut circuit)`` built with the
+package's circuit IR and cut-spec builder; they exercise every virtual-gate
+type of ``virtual_gates.py`` (CX/CZ/CY/RZZ generic + both degenerate angles/
+CPhase/Move), multi-cut labels, 2 and 3 fragments and traced qubits.
+"""
+import math
+import random
+
+from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.circuit import QuantumCircuit, QuantumRegister
+from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.cutting import CutSpec, cut_circuit
+
+
+def _rand_layer(qc, qubits, rng):
+    for q in qubits:
+        qc.u(rng.uniform(0, math.pi), rng.uniform(-math.pi, math.pi), rng.uniform(-math.pi, math.pi), q)
+
+
+def two_fragment(kind: str, n0: int = 2, n1: int = 2, seed: int = 7, angle: float | None = None,
+                 n_cuts: int = 1):
+    """Random 1q layers + intra-fragment CX, and ``n_cuts`` cut gates of ``kind`` across."""
+    rng = random.Random(seed)
+    n = n0 + n1
+    qr = QuantumRegister(n, "q")
+    qc = QuantumCircuit(qr)
+    left, right = list(range(n0)), list(range(n0, n))
+    cut_idx = []
+    _rand_layer(qc, range(n), rng)
+    for c in range(n_cuts):
+        if n0 > 1:
+            qc.cx(left[0], left[1])
+        if n1 > 1:
+            qc.cx(right[1], right[0])
+        a, b = left[(c + n0 - 1) % n0], right[c % n1]
+        th = rng.uniform(0.2, 2.9) if angle is None else angle
+        cut_idx.append(len(qc.data))
+        if kind == "cx":
+            qc.cx(a, b)
+        elif kind == "cz":
+            qc.cz(a, b)
+        elif kind == "cy":
+            qc.cy(a, b)
+        elif kind == "rzz":
+            qc.rzz(th, a, b)
+        elif kind == "cp":
+            qc.cp(th, a, b)
+        else:
+            raise ValueError(kind)
+        _rand_layer(qc, range(n), rng)
+    qc.measure_all()
+    return qc, cut_circuit(qc, CutSpec([left, right], cut_idx))
+
+
+def wire_cut(n0: int = 2, n1: int = 2, seed: int = 11, extra_gate_cut: bool = False):
+    """Qubit ``n0-1`` moves from fragment 0 to fragment 1 halfway (VirtualMove)."""
+    rng = random.Random(seed)
+    n = n0 + n1
+    qr = QuantumRegister(n, "q")
+    qc = QuantumCircuit(qr)
+    src = n0 - 1
+    _rand_layer(qc, range(n), rng)
+    for i in range(n0 - 1):
+        qc.cx(i, src)
+    _rand_layer(qc, [src], rng)
+    cut_at = len(qc.data)
+    _rand_layer(qc, [src], rng)
+    for j in range(n0, n):
+        qc.cx(src, j)
+    gate_cuts = []
+    if extra_gate_cut and n0 > 1:
+        gate_cuts.append(len(qc.data))
+        qc.cx(0, n0)
+    _rand_layer(qc, range(n), rng)
+    qc.measure_all()
+    spec = CutSpec([list(range(n0)), list(range(n0, n))], gate_cuts, [(cut_at, src, 1)])
+    return qc, cut_circuit(qc, spec)
+
+
+def three_fragment(seed: int = 5, sizes=(2, 2, 2)):
+    rng = random.Random(seed)
+    n = sum(sizes)
+    qr = QuantumRegister(n, "q")
+    qc = QuantumCircuit(qr)
+    b = [0, sizes[0], sizes[0] + sizes[1], n]
+    parts = [list(range(b[i], b[i + 1])) for i in range(3)]
+    _rand_layer(qc, range(n), rng)
+    for p in parts:
+        for i in range(len(p) - 1):
+            qc.cx(p[i], p[i + 1])
+    cuts = [len(qc.data)]
+    qc.cx(parts[0][-1], parts[1][0])
+    _rand_layer(qc, range(n), rng)
+    cuts.append(len(qc.data))
+    qc.cz(parts[1][-1], parts[2][0])
+    _rand_layer(qc, range(n), rng)
+    qc.measure_all()
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.cutting import decompose
+    d = decompose(qc)
+    # locate the cut 2-qubit gates after decomposition (cz -> h cx h)
+    cx_idx = [i for i, ins in enumerate(d) if ins.operation.name == "cx"
+              and len({d.find_qubit(q) for q in ins.qubits} & set(parts[0] + parts[2])) > 0
+              and any(d.find_qubit(q) in parts[1] for q in ins.qubits)]
+    return d, cut_circuit(d, CutSpec(parts, cx_idx))
+
+
+def partial_measure(seed: int = 3):
+    """Two fragments where one qubit is never measured (traced out)."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.circuit import ClassicalRegister
+    rng = random.Random(seed)
+    qr = QuantumRegister(4, "q")
+    cr = ClassicalRegister(3, "c")
+    qc = QuantumCircuit(qr, cr)
+    _rand_layer(qc, range(4), rng)
+    qc.cx(0, 1)
+    cut = [len(qc.data)]
+    qc.cx(1, 2)
+    qc.cx(3, 2)
+    _rand_layer(qc, range(4), rng)
+    qc.measure(0, 0)
+    qc.measure(2, 1)
+    qc.measure(3, 2)
+    return qc, cut_circuit(qc, CutSpec([[0, 1], [2, 3]], cut))
