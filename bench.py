@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark of the knitting hot path on MI355X (BASELINE.json metric).
+
+metric: subcircuit-instances/s + full-knit wall time, syc 32 p=2, 1/2/4/8 GPUs.
+A step = one full run of the hot path for the workload: batched exact sweep of
+every cut instance of every fragment + the dense fp64 knit of the complete
+2^32-entry distribution (inputs = compiled plan, resident on the GPU).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload syc_32_5_p2] [--factored]
+  N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+value = reference-counted instances (sum over fragments of their label lists, run.py:37-39)
+processed per second by the whole job, timed between barriers, max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense FP64 matrix, spec (MI355X_MICROARCH.md has no measured f64 row)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="syc_32_5_p2")
+    ap.add_argument("--factored", action="store_true", help="rank-factored knit (exact, fewer flops)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-labels", type=int, default=12)
+    return ap.parse_args()
+
+
+def cpu_baseline(cut, n_labels_sample: int):
+    """Oracle (numpy) timing on a bounded sample of the same workload, extrapolated."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import dense, qvm
+    from oracle.statevector import simulate
+
+    try:
+        from threadpoolctl import threadpool_info
+
+        threads = max([t.get("num_threads", 1) for t in threadpool_info()] + [1])
+    except Exception:
+        threads = os.cpu_count() or 1
+    view = qvm.CutView(cut)
+    frags = [list(r) for r in view.qregs if len(r)]
+    t0 = time.perf_counter()
+    done = 0
+    per_frag_labels = []
+    for f in frags:
+        labels = view.labels(f)
+        per_frag_labels.append(len(labels))
+        cl = dense.fragment_clbits(view, f)
+        for label in labels[:n_labels_sample]:
+            d = simulate(view.instance_ops(f, label), len(f))
+            dense.fold(d, view.num_clbits, cl)
+            done += 1
+    t_inst = (time.perf_counter() - t0) / max(done, 1)
+    # knit: one GEMM slice of the contraction (same K and N, a block of M rows)
+    L = len(view.global_labels())
+    widths = [1 << len(dense.fragment_clbits(view, f)) for f in frags]
+    M = widths[0]
+    Nw = int(np.prod(widths[1:])) if len(widths) > 1 else 1
+    rows = min(M, 512)
+    rng = np.random.default_rng(0)
+    A = rng.standard_normal((L, rows))
+    B = rng.standard_normal((L, Nw))
+    t1 = time.perf_counter()
+    A.T @ B
+    t_knit = (time.perf_counter() - t1) * (M / rows)
+    total_inst = sum(per_frag_labels)
+    t_total = t_inst * total_inst + t_knit
+    return {
+        "value": total_inst / t_total,
+        "unit": "instances/s",
+        "cores": int(threads),
+        "kind": "port",
+        "sample": (f"oracle numpy: {done} instances exactly simulated (branching statevector, "
+                   f"{t_inst * 1e3:.1f} ms each) + knit GEMM slice {rows}x{Nw}x{L} "
+                   f"(numpy BLAS, {threads} threads), extrapolated to {total_inst} instances and "
+                   f"{M}x{Nw}x{L}: {t_total:.1f} s per full knit"),
+        "full_knit_s": t_total,
+    }
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    name, n, d, p, variant = cutting.BASELINE_CONFIGS[args.workload]
+    circ, cut, desc = cutting.config_cut_circuit(name, n, d, p, variant)
+    virt = VirtualCircuit(cut)
+    torch.cuda.set_device(local)
+    pipe = KnitPipeline(virt, device=local, factored=args.factored, rank=rank, world=world)
+    counts = pipe.instance_counts()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        pipe.step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    pipe.record_events = True
+    pipe.events.clear()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pipe.step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    gemm_ms = sum(s.elapsed_time(e) for s, e in pipe.events) / max(len(pipe.events), 1)
+    M, Nn, K = pipe.gemm_shape()
+    flops = 2.0 * M * Nn * K
+    achieved = flops / (gemm_ms * 1e-3) / 1e12
+    if rank != 0:
+        return
+    ms_per_step = elapsed / args.steps * 1e3
+    value = counts["instances_ref"] * args.steps / elapsed
+    line = {
+        "metric": "subcircuit-instances/s (full-knit wall time = ms_per_step), syc 32 p=2",
+        "value": value,
+        "unit": "instances/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded circuit generators, random.seed(1234))",
+        "config": {
+            "workload": f"{name} {n} {d} p={p}" + (" (forced cuts)" if variant == "forced" else ""),
+            "cuts": desc,
+            "instances_ref": counts["instances_ref"],
+            "branch_jobs": counts["branch_jobs"],
+            "labels": counts["labels"],
+            "knit": "factored" if args.factored else "direct",
+            "output_entries": 1 << pipe.N,
+            "parallelism": f"labels x{world} ({pipe.mode})",
+        },
+        "roofline": {
+            "kernel": "qk_gemm_keyed_kernel (knit contraction)",
+            "bound": "mfma",
+            "achieved": achieved,
+            "peak": FP64_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
+            "traffic": None,
+            "flops_per_launch": flops,
+            "avg_launch_ms": gemm_ms,
+        },
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(cut, args.cpu_sample_labels)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -432,20 +432,42 @@ constexpr int GT = 128;      // workgroup tile (M and N)
 constexpr int GK = 16;       // K chunk
 constexpr int GPAD = 16;     // LDS row padding (doubles): 1152-B rows avoid the 2-way conflict
 
+// Loads this thread's 8 consecutive columns of chunk row `kr` (zero outside [0,K) x [0,cols)).
+__device__ __forceinline__ void gemm_load8(double (&r)[8], const double* __restrict__ X, int64_t ld,
+                                           int64_t kr, int64_t K, int64_t c0, int64_t cols, bool vec) {
+    if (vec && kr < K && c0 + 8 <= cols) {
+        const double2* p = reinterpret_cast<const double2*>(X + kr * ld + c0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const double2 v = p[c];
+            r[2 * c] = v.x;
+            r[2 * c + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) r[c] = (kr < K && c0 + c < cols) ? X[kr * ld + c0 + c] : 0.0;
+    }
+}
+
+// One 128x128 output tile per 256-thread workgroup (2x2 waves of 64x64 = 4x4 MFMA 16x16x4 f64
+// tiles each). K is streamed in 16-row chunks: the next chunk's global loads are issued into
+// registers before the current chunk's MFMAs (software pipeline), LDS is double buffered so a
+// chunk costs one barrier.
 __global__ __launch_bounds__(256) void qk_gemm_keyed_kernel(
     int64_t M, int64_t N, int64_t K, const double* __restrict__ A, int64_t lda,
     const double* __restrict__ B, int64_t ldb, const int64_t* __restrict__ keyA, int64_t strideA,
     const int64_t* __restrict__ keyB, int64_t strideB, double* __restrict__ out, int beta,
-    int tiles_m, int tiles_n) {
-    __shared__ double As[GK][GT + GPAD];
-    __shared__ double Bs[GK][GT + GPAD];
+    int64_t tiles_m, int64_t tiles_n) {
+    __shared__ double As[2][GK][GT + GPAD];
+    __shared__ double Bs[2][GK][GT + GPAD];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
 
-    // XCD-aware mapping: consecutive block ids land on different XCDs (round-robin of 8),
-    // so give each XCD a contiguous run of tiles (shared A/B panels stay in its L2).
-    const int64_t nblk = (int64_t)tiles_m * tiles_n;
-    int64_t bid = blockIdx.x;
+    // XCD-aware mapping: the dispatcher deals consecutive block ids round-robin over the 8 XCDs,
+    // so hand each XCD a contiguous run of tiles (tiles sharing a B panel share its L2).
+    const int64_t nblk = tiles_m * tiles_n;
+    int64_t bid = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    if (bid >= nblk) return;
     if (nblk % 8 == 0) bid = (bid % 8) * (nblk / 8) + bid / 8;
     const int64_t bm = bid % tiles_m, bn = bid / tiles_m;
     const int64_t m0 = bm * GT, n0 = bn * GT;
@@ -458,30 +480,31 @@ __global__ __launch_bounds__(256) void qk_gemm_keyed_kernel(
 
     const int lr = tid >> 4;        // chunk row 0..15
     const int lc = (tid & 15) * 8;  // 8 columns per thread
+    const bool vecA = ((lda & 1) == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+    const bool vecB = ((ldb & 1) == 0) && ((reinterpret_cast<uintptr_t>(B) & 15) == 0);
+    double ra[8], rb[8];
+    gemm_load8(ra, A, lda, lr, K, m0 + lc, M, vecA);
+    gemm_load8(rb, B, ldb, lr, K, n0 + lc, N, vecB);
+    int buf = 0;
     for (int64_t k0 = 0; k0 < K; k0 += GK) {
-        double ra[8], rb[8];
-        const int64_t kr = k0 + lr;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            const int64_t i = m0 + lc + c, j = n0 + lc + c;
-            ra[c] = (kr < K && i < M) ? A[kr * lda + i] : 0.0;
-            rb[c] = (kr < K && j < N) ? B[kr * ldb + j] : 0.0;
+            As[buf][lr][lc + c] = ra[c];
+            Bs[buf][lr][lc + c] = rb[c];
         }
         __syncthreads();
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            As[lr][lc + c] = ra[c];
-            Bs[lr][lc + c] = rb[c];
+        if (k0 + GK < K) {  // prefetch the next chunk while this one is multiplied
+            gemm_load8(ra, A, lda, k0 + GK + lr, K, m0 + lc, M, vecA);
+            gemm_load8(rb, B, ldb, k0 + GK + lr, K, n0 + lc, N, vecB);
         }
-        __syncthreads();
 #pragma unroll
         for (int kk = 0; kk < GK / 4; ++kk) {
             const int kr2 = kk * 4 + (lane >> 4);
             double fa[4], fb[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                fa[t] = As[kr2][wm * 64 + t * 16 + (lane & 15)];
-                fb[t] = Bs[kr2][wn * 64 + t * 16 + (lane & 15)];
+                fa[t] = As[buf][kr2][wm * 64 + t * 16 + (lane & 15)];
+                fb[t] = Bs[buf][kr2][wn * 64 + t * 16 + (lane & 15)];
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -489,18 +512,21 @@ __global__ __launch_bounds__(256) void qk_gemm_keyed_kernel(
                 for (int j = 0; j < 4; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
+        buf ^= 1;
     }
     // epilogue: f64 16x16 C layout: col = lane & 15, row = (lane >> 4) + 4 * r
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int j = 0; j < 4; ++j) {
+        const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
+        if (col >= N) continue;
+        const int64_t kcol = keyB ? keyB[col] : col * strideB;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
+        for (int i = 0; i < 4; ++i) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
-                if (row < M && col < N) {
-                    const int64_t o = (keyA ? keyA[row] : row * strideA) + (keyB ? keyB[col] : col * strideB);
+                if (row < M) {
+                    const int64_t o = (keyA ? keyA[row] : row * strideA) + kcol;
                     const double val = acc[i][j][r];
                     out[o] = beta ? out[o] + val : val;
                 }
@@ -573,7 +599,7 @@ int qk_ctx_destroy(qk_ctx* ctx) {
 
 int qk_ctx_set_stream(qk_ctx* ctx, void* s) {
     if (!ctx) return QK_EARG;
-    ctx->stream = s ? (hipStream_t)s : ctx->own;
+    ctx->stream = (hipStream_t)s;  // NULL = the device's null stream (torch's default stream)
     return QK_OK;
 }
 
@@ -671,10 +697,14 @@ int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A,
     if (!out || (K > 0 && (!A || !B))) return fail(ctx, QK_EARG, "qk_gemm_keyed: null buffer%s");
     if (lda < M || ldb < N) return fail(ctx, QK_EARG, "qk_gemm_keyed: leading dimension too small%s");
     const int64_t tm = (M + GT - 1) / GT, tn = (N + GT - 1) / GT;
-    if (tm * tn > 0x7fffffff) return fail(ctx, QK_EARG, "qk_gemm_keyed: too many tiles%s");
+    const int64_t nblk = tm * tn;
+    // grid.x * blockDim.x must stay below 2^32 work-items: spill tiles into grid.y
+    const int64_t gx = nblk < (1 << 20) ? nblk : (1 << 20);
+    const int64_t gy = (nblk + gx - 1) / gx;
+    if (gy > 65535) return fail(ctx, QK_EARG, "qk_gemm_keyed: too many tiles%s");
     QK_HIP(ctx, hipSetDevice(ctx->device));
-    hipLaunchKernelGGL(qk_gemm_keyed_kernel, dim3((unsigned)(tm * tn)), dim3(256), 0, ctx->stream, M, N, K,
-                       A, lda, B, ldb, keyA, strideA, keyB, strideB, out, beta, (int)tm, (int)tn);
+    hipLaunchKernelGGL(qk_gemm_keyed_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, ctx->stream, M,
+                       N, K, A, lda, B, ldb, keyA, strideA, keyB, strideB, out, beta, tm, tn);
     QK_HIP(ctx, hipGetLastError());
     return QK_OK;
 }

@@ -407,7 +407,13 @@ def contract_order(clbits: list) -> list:
     return sorted(range(len(clbits)), key=lambda i: -(min(clbits[i]) if clbits[i] else 1 << 62))
 
 
-def contract(ctx: Context, mats: list, clbits: list, out, row_block=None):
+def contract(ctx, mats: list, clbits: list, out, row_block=None, gemm=None, kr=None):
+    """Dense contraction of the per-fragment operands into `out` (see knit_dense).
+
+    `gemm(A, B, **kw)` / `kr(A, B)` default to the HIP kernels of `ctx`.
+    """
+    gemm = gemm or (lambda A, B, **kw: gemm_keyed(ctx, A, B, **kw))
+    kr = kr or (lambda A, B: khatri_rao(ctx, A, B))
     T = torch()
     dev = out.device
     order = contract_order(clbits)
@@ -432,12 +438,12 @@ def contract(ctx: Context, mats: list, clbits: list, out, row_block=None):
         else:
             kA, sA = key_arg(cls[0])
         ones = T.ones((A.shape[0], 1), dtype=T.float64, device=dev)
-        return gemm_keyed(ctx, A.contiguous(), ones, keyA=kA, strideA=sA, keyB=None, strideB=0, out=out)
+        return gemm(A.contiguous(), ones, keyA=kA, strideA=sA, keyB=None, strideB=0, out=out)
     A = mats[0]
     if len(mats) > 2:
         kA = T.from_numpy(deposit_keys(cls[0])).to(dev)
         for B, c in zip(mats[1:-1], cls[1:-1]):
-            A = khatri_rao(ctx, A.contiguous(), B.contiguous())
+            A = kr(A.contiguous(), B.contiguous())
             kB = T.from_numpy(deposit_keys(c)).to(dev)
             kA = (kA.view(1, -1) + kB.view(-1, 1)).reshape(-1)  # index i + j*M
         sA = 0
@@ -452,7 +458,7 @@ def contract(ctx: Context, mats: list, clbits: list, out, row_block=None):
         kA, sA = key_arg(cls[0])
     B = mats[-1]
     kB, sB = key_arg(cls[-1])
-    return gemm_keyed(ctx, A.contiguous(), B.contiguous(), keyA=kA, strideA=sA, keyB=kB, strideB=sB, out=out)
+    return gemm(A.contiguous(), B.contiguous(), keyA=kA, strideA=sA, keyB=kB, strideB=sB, out=out)
 
 
 def knit_quasi_distrs(virt, results: dict, device: int = 0, factored: bool = False):

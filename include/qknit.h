@@ -82,7 +82,8 @@ typedef struct qk_ctx qk_ctx;
 
 int qk_ctx_create(int device, qk_ctx** out);
 int qk_ctx_destroy(qk_ctx* ctx);
-/* Use an external hipStream_t (e.g. torch's current stream); NULL restores the own stream. */
+/* Launch on an external hipStream_t (e.g. torch's current stream); NULL selects the null stream.
+ * A new context launches on its own non-blocking stream until this is called. */
 int qk_ctx_set_stream(qk_ctx* ctx, void* hip_stream);
 int qk_ctx_synchronize(qk_ctx* ctx);
 const char* qk_last_error(qk_ctx* ctx);
