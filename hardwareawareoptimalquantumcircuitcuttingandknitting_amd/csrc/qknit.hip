@@ -453,7 +453,7 @@ __device__ __forceinline__ void gemm_load8(double (&r)[8], const double* __restr
 // tiles each). K is streamed in 16-row chunks: the next chunk's global loads are issued into
 // registers before the current chunk's MFMAs (software pipeline), LDS is double buffered so a
 // chunk costs one barrier.
-__global__ __launch_bounds__(256) void qk_gemm_keyed_kernel(
+__global__ __launch_bounds__(256, 2) void qk_gemm_keyed_kernel(
     int64_t M, int64_t N, int64_t K, const double* __restrict__ A, int64_t lda,
     const double* __restrict__ B, int64_t ldb, const int64_t* __restrict__ keyA, int64_t strideA,
     const int64_t* __restrict__ keyB, int64_t strideB, double* __restrict__ out, int beta,

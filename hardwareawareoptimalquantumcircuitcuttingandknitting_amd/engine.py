@@ -234,7 +234,7 @@ class FragmentState:
     dropped: bool = False  # reference skips fragments whose counts cannot be read (run.py:57-58)
 
 
-def prepare_fragments(virt, device: int = 0) -> list[FragmentState]:
+def prepare_fragments(virt, device: int = 0, upload: bool = True) -> list[FragmentState]:
     circ = virt.circuit
     cl = clbit_indexer(circ)
     vg = virt.vgate_instructions
@@ -249,7 +249,7 @@ def prepare_fragments(virt, device: int = 0) -> list[FragmentState]:
         # run.py:49-58 drops a fragment whose get_counts() raises, i.e. when some instance of
         # it measures nothing at all (no data measurement and no config measurement).
         dropped = prog.m == 0 and _some_label_unmeasured(prog, labels)
-        dp = None if dropped else DeviceProgram.upload(prog, device)
+        dp = DeviceProgram.upload(prog, device) if (upload and not dropped) else None
         out.append(FragmentState(frag, labels, prog, dp, jobs, touches, dropped))
     return out
 
