@@ -158,6 +158,78 @@ __device__ __forceinline__ void dispatch_u1(int a, double2 (&v)[PER], const doub
     }
 }
 
+// Real 2x2 [m00 m01; m10 m11]: 4 FMA per amplitude instead of 8.
+template <int A>
+__device__ __forceinline__ void ap_u1r(double2 (&v)[PER], const double* m) {
+    const double m00 = m[0], m01 = m[1], m10 = m[2], m11 = m[3];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if (r & (1 << A)) continue;
+        const double2 a = v[r], b = v[r | (1 << A)];
+        v[r] = make_double2(fma(m00, a.x, m01 * b.x), fma(m00, a.y, m01 * b.y));
+        v[r | (1 << A)] = make_double2(fma(m10, a.x, m11 * b.x), fma(m10, a.y, m11 * b.y));
+    }
+}
+
+// [m00, i p01; i p10, m11] with real m00, p01, p10, m11 (rx-type): 4 FMA per amplitude.
+template <int A>
+__device__ __forceinline__ void ap_u1x(double2 (&v)[PER], const double* m) {
+    const double m00 = m[0], p01 = m[1], p10 = m[2], m11 = m[3];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if (r & (1 << A)) continue;
+        const double2 a = v[r], b = v[r | (1 << A)];
+        v[r] = make_double2(fma(m00, a.x, -p01 * b.y), fma(m00, a.y, p01 * b.x));
+        v[r | (1 << A)] = make_double2(fma(m11, b.x, -p10 * a.y), fma(m11, b.y, p10 * a.x));
+    }
+}
+
+template <int A>
+__device__ __forceinline__ void ap_d1r(double2 (&v)[PER], const double* d) {
+    const double d0 = d[0], d1 = d[1];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const double s = (r & (1 << A)) ? d1 : d0;
+        v[r] = make_double2(s * v[r].x, s * v[r].y);
+    }
+}
+
+template <int A, int B>
+__device__ __forceinline__ void ap_d2r(double2 (&v)[PER], const double* d) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const double s = d[((r >> A) & 1) | (((r >> B) & 1) << 1)];
+        v[r] = make_double2(s * v[r].x, s * v[r].y);
+    }
+}
+
+__device__ __forceinline__ void dispatch_u1r(int a, double2 (&v)[PER], const double* m) {
+    switch (a) {
+        case 0: ap_u1r<0>(v, m); pin(v); break;
+        case 1: ap_u1r<1>(v, m); pin(v); break;
+        case 2: ap_u1r<2>(v, m); pin(v); break;
+        default: ap_u1r<3>(v, m); pin(v); break;
+    }
+}
+
+__device__ __forceinline__ void dispatch_u1x(int a, double2 (&v)[PER], const double* m) {
+    switch (a) {
+        case 0: ap_u1x<0>(v, m); pin(v); break;
+        case 1: ap_u1x<1>(v, m); pin(v); break;
+        case 2: ap_u1x<2>(v, m); pin(v); break;
+        default: ap_u1x<3>(v, m); pin(v); break;
+    }
+}
+
+__device__ __forceinline__ void dispatch_d1r(int a, double2 (&v)[PER], const double* d) {
+    switch (a) {
+        case 0: ap_d1r<0>(v, d); pin(v); break;
+        case 1: ap_d1r<1>(v, d); pin(v); break;
+        case 2: ap_d1r<2>(v, d); pin(v); break;
+        default: ap_d1r<3>(v, d); pin(v); break;
+    }
+}
+
 __device__ __forceinline__ void dispatch_d1(int a, double2 (&v)[PER], const double* d) {
     switch (a) {
         case 0: ap_d1<0>(v, d); pin(v); break;
@@ -191,6 +263,17 @@ __device__ __forceinline__ void dispatch_d2(int a, int b, double2 (&v)[PER], con
         case 3: ap_d2<1, 2>(v, d); pin(v); break;
         case 4: ap_d2<1, 3>(v, d); pin(v); break;
         default: ap_d2<2, 3>(v, d); pin(v); break;
+    }
+}
+
+__device__ __forceinline__ void dispatch_d2r(int a, int b, double2 (&v)[PER], const double* d) {
+    switch (pair_id(a, b)) {
+        case 0: ap_d2r<0, 1>(v, d); pin(v); break;
+        case 1: ap_d2r<0, 2>(v, d); pin(v); break;
+        case 2: ap_d2r<0, 3>(v, d); pin(v); break;
+        case 3: ap_d2r<1, 2>(v, d); pin(v); break;
+        case 4: ap_d2r<1, 3>(v, d); pin(v); break;
+        default: ap_d2r<2, 3>(v, d); pin(v); break;
     }
 }
 
@@ -365,6 +448,16 @@ __global__ __launch_bounds__(NT) void qk_sweep_pass_kernel(SweepArgs a) {
                     const double sr = s[0], si = s[1];
 #pragma unroll
                     for (int r = 0; r < PER; ++r) v[r] = cmul(sr, si, v[r]);
+                } break;
+                case QK_U1R: dispatch_u1r(op.a, v, a.mats + op.mat); break;
+                case QK_U1X: dispatch_u1x(op.a, v, a.mats + op.mat); break;
+                case QK_D1R: dispatch_d1r(op.a, v, a.mats + op.mat + 2 * var); break;
+                case QK_D2R: dispatch_d2r(op.a, op.b, v, a.mats + op.mat); break;
+                case QK_SCALER: {
+                    const double s = a.mats[op.mat + var];
+#pragma unroll
+                    for (int r = 0; r < PER; ++r) v[r] = make_double2(s * v[r].x, s * v[r].y);
+                    pin(v);
                 } break;
                 default: break;
             }

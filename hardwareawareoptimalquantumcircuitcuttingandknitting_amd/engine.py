@@ -24,7 +24,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from .fragment_program import FragmentProgram, JobTable, build_jobs, compile_fragment
+from .fragment_program import FragmentProgram, JobTable, build_jobs, compile_fragment, dedup_labels
 from .knit_plan import LabelSpace, deposit_keys, factor_vgate
 from .sweep_plan import EncodedProgram, encode
 
@@ -232,9 +232,19 @@ class FragmentState:
     jobs: JobTable | None
     touches: list
     dropped: bool = False  # reference skips fragments whose counts cannot be read (run.py:57-58)
+    uidx: np.ndarray | None = None  # label -> row of the swept (deduplicated) instance list
+    unique_labels: list | None = None
+
+    @property
+    def n_rows(self) -> int:
+        """Rows of the swept q_f (unique instances)."""
+        return len(self.unique_labels) if self.unique_labels is not None else len(self.labels)
+
+    def row_of_label(self) -> np.ndarray:
+        return self.uidx if self.uidx is not None else np.arange(len(self.labels), dtype=np.int64)
 
 
-def prepare_fragments(virt, device: int = 0, upload: bool = True) -> list[FragmentState]:
+def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = True) -> list[FragmentState]:
     circ = virt.circuit
     cl = clbit_indexer(circ)
     vg = virt.vgate_instructions
@@ -245,12 +255,16 @@ def prepare_fragments(virt, device: int = 0, upload: bool = True) -> list[Fragme
         prog = compile_fragment(fcirc, frag, cl)
         labels = virt.get_instance_labels(frag)
         touches = [bool(set(v.qubits) & set(frag)) for v in vg]
-        jobs = build_jobs(prog, labels)
+        if dedup:
+            unique, uidx = dedup_labels(prog, labels)
+        else:
+            unique, uidx = list(labels), np.arange(len(labels), dtype=np.int64)
+        jobs = build_jobs(prog, unique)
         # run.py:49-58 drops a fragment whose get_counts() raises, i.e. when some instance of
         # it measures nothing at all (no data measurement and no config measurement).
         dropped = prog.m == 0 and _some_label_unmeasured(prog, labels)
         dp = DeviceProgram.upload(prog, device) if (upload and not dropped) else None
-        out.append(FragmentState(frag, labels, prog, dp, jobs, touches, dropped))
+        out.append(FragmentState(frag, labels, prog, dp, jobs, touches, dropped, uidx, unique))
     return out
 
 
@@ -267,11 +281,12 @@ def sweep_fragment(ctx: Context, fs: FragmentState, label_range=None):
     """Signed-folded per-label distributions ``q_f`` of one fragment on the GPU.
 
     ``label_range=(lo, hi)`` restricts the sweep to fragment labels ``[lo, hi)``
-    (multi-GPU sharding); rows are returned for that range only.
+    (multi-GPU sharding); rows are returned for that range only. Rows are the
+    swept (deduplicated) instances: ``q[fs.row_of_label()]`` is per label.
     """
     T = torch()
     jobs = fs.jobs
-    lo, hi = (0, len(fs.labels)) if label_range is None else label_range
+    lo, hi = (0, fs.n_rows) if label_range is None else label_range
     width = 1 << fs.prog.m
     if fs.dropped:
         return T.ones((hi - lo, 1), dtype=T.float64, device=T.device("cuda", ctx.device))
@@ -315,7 +330,7 @@ def knit_operands(virt, frags: list[FragmentState], factored: bool = False) -> K
         c = space.coefficients()
         rows, coefs = [], []
         for i, fs in enumerate(frags):
-            rows.append(space.fragment_rows(fs.touches))
+            rows.append(fs.row_of_label()[space.fragment_rows(fs.touches)])
             coefs.append(c if i == 0 else np.ones_like(c))
         return KnitOperands(rows, coefs, [None] * len(frags), clbits, space.num_labels)
     # factored: per gate rank factorisation, fragment transform = kron over touching gates
@@ -334,6 +349,10 @@ def knit_operands(virt, frags: list[FragmentState], factored: bool = False) -> K
                 W = np.kron(W, np.ones((ranks[j], 1)))
             else:
                 W = np.kron(W, Ts[j][sides[j]])
+        if fs.uidx is not None:  # fold labels sharing an instance: W' = W P
+            Wu = np.zeros((W.shape[0], fs.n_rows))
+            np.add.at(Wu.T, fs.uidx, W.T)
+            W = Wu
         transforms.append(W)
     return KnitOperands([None] * len(frags), [None] * len(frags), transforms, clbits, int(np.prod(ranks)))
 

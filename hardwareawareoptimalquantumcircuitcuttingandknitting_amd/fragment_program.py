@@ -137,6 +137,8 @@ def compile_fragment(frag_circuit, fragment, clbit_index) -> FragmentProgram:
     if len(set(clb)) != len(clb):
         raise UnsupportedCircuit("two qubits measured into one clbit")
 
+    raw = _recover_cz(raw)
+
     # -- local order: measured (by clbit) then unmeasured (by fragment index)
     meas_sorted = sorted(measured_at.items(), key=lambda kv: kv[1][1])
     order = [q for q, _ in meas_sorted] + [q for q in range(n) if q not in measured_at]
@@ -178,6 +180,46 @@ def compile_fragment(frag_circuit, fragment, clbit_index) -> FragmentProgram:
     _absorb_into_slots(ops, slots)
     return FragmentProgram(n=n, m=m, clbits=clbits, ops=ops, slots=slots,
                            qubit_order=[frag_qubits[q] for q in order])
+
+
+_H = _g.gate_matrix("h")
+_CZ = _g.gate_matrix("cz")
+
+
+def _recover_cz(raw: list) -> list:
+    """Undo the cutter's ``cz -> h . cx . h`` decomposition (``Cutter.py:84``).
+
+    Pattern on target ``t``: ``h(t)``, ``cx(c, t)``, ``h(t)`` with no other
+    operation on ``t`` in between (operations on ``c`` may interleave: they
+    commute with ``h(t)``). The diagonal CZ needs no fiber position in the
+    sweep kernel and costs one sign flip instead of two dense 2x2 products.
+    """
+    nxt = {}  # index -> index of the next op on the same qubit (per qubit)
+    last = {}
+    for i, (kind, qs, _) in enumerate(raw):
+        for q in qs:
+            if q in last:
+                nxt[(last[q], q)] = i
+            last[q] = i
+    dead = set()
+    out = list(raw)
+    for j, (kind, qs, mat) in enumerate(raw):
+        if kind != "u2" or not np.array_equal(mat, _g.gate_matrix("cx")) or j in dead:
+            continue
+        c, t = qs
+        prev = [i for i in range(j) if (i, t) in nxt and nxt[(i, t)] == j]
+        k = nxt.get((j, t))
+        if not prev or k is None:
+            continue
+        i = prev[0]
+        if i in dead or k in dead:
+            continue
+        ki, qi, mi = raw[i]
+        kk, qk, mk = raw[k]
+        if ki == "u1" and kk == "u1" and np.allclose(mi, _H, atol=1e-15) and np.allclose(mk, _H, atol=1e-15):
+            dead.update((i, k))
+            out[j] = ("u2", qs, _CZ.copy())
+    return [op for i, op in enumerate(out) if i not in dead]
 
 
 def _absorb_into_slots(ops: list, slots: list) -> None:
@@ -245,6 +287,43 @@ def side_branches(endpoint, inst_id: int) -> list[tuple[np.ndarray, float]]:
     if not measured:
         return [(post @ pre, 1.0)]
     return [(post @ P0 @ pre, 1.0), (post @ P1 @ pre, -1.0)]
+
+
+def _side_signature(endpoint, inst_id: int) -> tuple:
+    if isinstance(endpoint, BranchMeasure):
+        return ("branch",)
+    side = endpoint.side_circuit(inst_id)
+    return tuple((ins.operation.name, tuple(round(float(p), 15) for p in getattr(ins.operation, "params", ())))
+                 for ins in side.data)
+
+
+def dedup_labels(prog: FragmentProgram, labels: list) -> tuple[list, np.ndarray]:
+    """Merge labels whose instance programs coincide on this fragment.
+
+    Two labels give the same fragment instance when every endpoint of the
+    fragment gets the same side program (e.g. VirtualCX instantiations 2 and 3
+    are both "measure" on the control side, ``virtual_gates.py:163-168``).
+    Returns ``(unique_labels, uidx)`` with ``labels[i]`` simulated as
+    ``unique_labels[uidx[i]]``. The reference simulates every label
+    (``run.py:36-43``); counts of both are reported.
+    """
+    sig_cache: dict = {}
+    seen: dict = {}
+    unique, uidx = [], np.zeros(len(labels), dtype=np.int64)
+    for i, label in enumerate(labels):
+        key = []
+        for s in prog.slots:
+            inst = 0 if isinstance(s.endpoint, BranchMeasure) else label[s.vgate_idx]
+            ck = (id(s), inst)
+            if ck not in sig_cache:
+                sig_cache[ck] = _side_signature(s.endpoint, inst)
+            key.append(sig_cache[ck])
+        key = tuple(key)
+        if key not in seen:
+            seen[key] = len(unique)
+            unique.append(label)
+        uidx[i] = seen[key]
+    return unique, uidx
 
 
 @dataclass

@@ -121,7 +121,7 @@ class KnitPipeline:
             if fs.dropped:
                 self.sweeps.append(None)
                 continue
-            nl = len(fs.labels)
+            nl = fs.n_rows
             if self.mode == "reduce":
                 t0, t1 = self.term_range
                 rows = np.unique(self.ops.rows[i][t0:t1])
@@ -177,7 +177,7 @@ class KnitPipeline:
         for i, fs in enumerate(self.frags):
             sw = self.sweeps[i]
             if sw is None:
-                ones = be.zeros((len(fs.labels), 1), T.float64)
+                ones = be.zeros((fs.n_rows, 1), T.float64)
                 ones += 1.0
                 qs.append(ones)
                 continue
@@ -189,7 +189,7 @@ class KnitPipeline:
                 q = sw["pjob"]
             q = q[: sw["hi"] - sw["lo"]]
             if self.mode == "gather":
-                q = self._all_gather_rows(q, len(fs.labels))
+                q = self._all_gather_rows(q, fs.n_rows)
             qs.append(q)
         return qs
 
@@ -266,6 +266,7 @@ class KnitPipeline:
         """Reference instance count (``run.py:37-39``: sum of per-fragment label lists) and jobs."""
         return {
             "instances_ref": int(sum(len(fs.labels) for fs in self.frags)),
+            "instances_unique": int(sum(fs.n_rows for fs in self.frags)),
             "branch_jobs": int(sum(fs.jobs.n_jobs for fs in self.frags if not fs.dropped)),
             "labels": int(self.ops.num_terms),
         }

@@ -32,7 +32,7 @@ FIBER_BITS = 4
 LOW_BITS = 5  # state bits always resident in a SPLIT tile (512-B contiguous runs)
 
 # op kinds (must match qknit.h)
-K_U1, K_D1, K_SLOT, K_U2, K_D2, K_CX, K_SWAP, K_SCALE = range(8)
+K_U1, K_D1, K_SLOT, K_U2, K_D2, K_CX, K_SWAP, K_SCALE, K_U1R, K_U1X, K_D1R, K_D2R, K_SCALER = range(13)
 
 OP_DTYPE = np.dtype([("kind", "<i4"), ("a", "<i4"), ("b", "<i4"), ("e1", "<i4"),
                      ("e2", "<i4"), ("slot", "<i4"), ("mat", "<i4"), ("pad", "<i4")])
@@ -172,6 +172,11 @@ class _Mats:
                 self.buf.extend((float(z.real), float(z.imag)))
         return off
 
+    def add_real(self, vals) -> int:
+        off = len(self.buf)
+        self.buf.extend(float(v) for v in np.asarray(vals, dtype=np.float64).ravel())
+        return off
+
 
 def _swap_order4(m: np.ndarray) -> np.ndarray:
     """Re-express a 4x4 (q0,q1) matrix in (q1,q0) order."""
@@ -198,6 +203,22 @@ def _block(m: np.ndarray, ctrl_pos: int, bit: int) -> np.ndarray:
     return m[np.ix_(idx, idx)]
 
 
+def _d1(rec, mats: _Mats, a: int, e1: int, variants: list):
+    """Diagonal on fiber position ``a``, variant chosen by external bit ``e1``."""
+    v = [np.asarray(x, dtype=np.complex128) for x in variants]
+    if all(np.all(x.imag == 0) for x in v):
+        return rec(K_D1R, a=a, e1=e1, mat=mats.add_real(np.concatenate([x.real for x in v])))
+    return rec(K_D1, a=a, e1=e1, mat=mats.add(*v))
+
+
+def _scale(rec, mats: _Mats, e1: int, e2: int, vals):
+    """Whole-fiber scalar chosen by external bits (index e1bit + 2*e2bit)."""
+    vals = np.asarray(vals, dtype=np.complex128)
+    if np.all(vals.imag == 0):
+        return rec(K_SCALER, e1=e1, e2=e2, mat=mats.add_real(vals.real))
+    return rec(K_SCALE, e1=e1, e2=e2, mat=mats.add(vals))
+
+
 def _emit(op: HostOp, fib: dict, mats: _Mats) -> list:
     """Encode one host op given the group fiber map (state bit -> fiber index)."""
     rec = lambda kind, a=-1, b=-1, e1=-1, e2=-1, slot=-1, mat=-1: (kind, a, b, e1, e2, slot, mat, 0)
@@ -209,8 +230,15 @@ def _emit(op: HostOp, fib: dict, mats: _Mats) -> list:
         if _is_diag(m):
             d = np.diag(m)
             if q in fib:
+                if np.all(d.imag == 0):
+                    return [rec(K_D1R, a=fib[q], mat=mats.add_real(d.real))]
                 return [rec(K_D1, a=fib[q], mat=mats.add(d))]
-            return [rec(K_SCALE, e1=q, mat=mats.add([d[0], d[1], d[0], d[1]]))]
+            return [_scale(rec, mats, q, -1, [d[0], d[1], d[0], d[1]])]
+        if np.all(m.imag == 0):
+            return [rec(K_U1R, a=fib[q], mat=mats.add_real(m.real.ravel()))]
+        if np.all(np.diag(m).imag == 0) and m[0, 1].real == 0 and m[1, 0].real == 0:
+            return [rec(K_U1X, a=fib[q], mat=mats.add_real([m[0, 0].real, m[0, 1].imag,
+                                                            m[1, 0].imag, m[1, 1].real]))]
         return [rec(K_U1, a=fib[q], mat=mats.add(m))]
     # two-qubit
     q0, q1 = op.qubits
@@ -222,13 +250,15 @@ def _emit(op: HostOp, fib: dict, mats: _Mats) -> list:
             a, b = fib[q0], fib[q1]
             if a > b:
                 a, b, d = b, a, d[[0, 2, 1, 3]]
+            if np.all(d.imag == 0):
+                return [rec(K_D2R, a=a, b=b, mat=mats.add_real(d.real))]
             return [rec(K_D2, a=a, b=b, mat=mats.add(d))]
         if q0 in fib:  # q1 external: variants by b1
-            return [rec(K_D1, a=fib[q0], e1=q1, mat=mats.add(d[[0, 1]], d[[2, 3]]))]
+            return [_d1(rec, mats, fib[q0], q1, [d[[0, 1]], d[[2, 3]]])]
         if q1 in fib:  # q0 external: variants by b0
-            return [rec(K_D1, a=fib[q1], e1=q0, mat=mats.add(d[[0, 2]], d[[1, 3]]))]
+            return [_d1(rec, mats, fib[q1], q0, [d[[0, 2]], d[[1, 3]]])]
         # both external: scalar selected by (b0, b1) -> index e1bit + 2 e2bit
-        return [rec(K_SCALE, e1=q0, e2=q1, mat=mats.add(d))]
+        return [_scale(rec, mats, q0, q1, d)]
     if q0 in diag or q1 in diag:
         c_pos = 0 if q0 in diag else 1
         ctrl, tgt = (q0, q1) if c_pos == 0 else (q1, q0)
@@ -242,7 +272,7 @@ def _emit(op: HostOp, fib: dict, mats: _Mats) -> list:
             return [rec(K_U2, a=a, b=b, mat=mats.add(mm))]
         m0, m1 = _block(m, c_pos, 0), _block(m, c_pos, 1)
         if _is_diag(m0) and _is_diag(m1):
-            return [rec(K_D1, a=fib[tgt], e1=ctrl, mat=mats.add(np.diag(m0), np.diag(m1)))]
+            return [_d1(rec, mats, fib[tgt], ctrl, [np.diag(m0), np.diag(m1)])]
         return [rec(K_U1, a=fib[tgt], e1=ctrl, mat=mats.add(m0, m1))]
     a, b = fib[q0], fib[q1]
     if _is_swap(m):

@@ -40,8 +40,14 @@ extern "C" {
 #define QK_TILE_BITS 12
 #define QK_FIBER_BITS 4
 
-/* op kinds (sweep_plan.py K_*) */
-enum { QK_U1 = 0, QK_D1 = 1, QK_SLOT = 2, QK_U2 = 3, QK_D2 = 4, QK_CX = 5, QK_SWAP = 6, QK_SCALE = 7 };
+/* op kinds (sweep_plan.py K_*). Matrices are interleaved complex unless noted:
+ *   U1 2x2 (8)  D1 diag (4)  U2 4x4 (32)  D2 diag4 (8)  SCALE (2 per variant)
+ *   U1R real 2x2 (4 reals)   U1X [m00, Im m01, Im m10, m11] for real-diagonal /
+ *   imaginary-off-diagonal 2x2 (rx-type, 4 reals)   D1R real diag (2 per variant)
+ *   D2R real diag4 (4)   SCALER real scalar (1 per variant).
+ * Variant index = bit(e1) + 2*bit(e2) of the thread's fixed state bits (-1: bit taken as 0). */
+enum { QK_U1 = 0, QK_D1 = 1, QK_SLOT = 2, QK_U2 = 3, QK_D2 = 4, QK_CX = 5, QK_SWAP = 6, QK_SCALE = 7,
+       QK_U1R = 8, QK_U1X = 9, QK_D1R = 10, QK_D2R = 11, QK_SCALER = 12 };
 
 typedef struct qk_op {      /* 32 bytes */
     int32_t kind;

@@ -57,6 +57,27 @@ def emulate(enc: sp.EncodedProgram, slot_mats: np.ndarray, signs: np.ndarray) ->
                         M = mv[lo]
                         psi[lo] = M[:, 0, 0] * a0 + M[:, 0, 1] * a1
                         psi[hi] = M[:, 1, 0] * a0 + M[:, 1, 1] * a1
+                    elif k in (sp.K_U1R, sp.K_U1X):
+                        q = qb[op["a"]]
+                        r = enc.mats[op["mat"]: op["mat"] + 4]
+                        if k == sp.K_U1R:
+                            m = r.reshape(2, 2).astype(complex)
+                        else:
+                            m = np.array([[r[0], 1j * r[1]], [1j * r[2], r[3]]])
+                        lo = idx[_bits(idx, q) == 0]
+                        hi = lo | (1 << q)
+                        a0, a1 = psi[lo].copy(), psi[hi].copy()
+                        psi[lo] = m[0, 0] * a0 + m[0, 1] * a1
+                        psi[hi] = m[1, 0] * a0 + m[1, 1] * a1
+                    elif k == sp.K_D1R:
+                        q = qb[op["a"]]
+                        psi = psi * enc.mats[op["mat"] + 2 * var + _bits(idx, q)]
+                    elif k == sp.K_SCALER:
+                        psi = psi * enc.mats[op["mat"] + var]
+                    elif k == sp.K_D2R:
+                        qa, qbb = qb[op["a"]], qb[op["b"]]
+                        d = enc.mats[op["mat"]: op["mat"] + 4]
+                        psi = psi * d[_bits(idx, qa) + 2 * _bits(idx, qbb)]
                     elif k == sp.K_D1:
                         q = qb[op["a"]]
                         d = np.stack([_mat(enc.mats, op["mat"] + 4 * v, 2) for v in range(4)

@@ -131,14 +131,15 @@ def test_syc_32_5_schedule_shape():
 
 
 def test_split_mode_emulated_16_qubits():
-    """A 16-qubit SPLIT-mode fragment (3 passes) through the emulator vs the oracle."""
-    _, cut = cutting.config_cut_circuit("syc", 32, 1, 2, "forced")[:2]
+    """A 16-qubit SPLIT-mode fragment (3 passes) of syc 32 5 through the emulator vs the oracle."""
+    _, cut = cutting.config_cut_circuit("syc", 32, 5, 2)[:2]
     virt = VirtualCircuit(cut)
     view = qvm.CutView(cut)
     cl = engine.clbit_indexer(virt.circuit)
     frag, fcirc = next(iter(virt.fragment_circuits.items()))
     prog = compile_fragment(fcirc, frag, cl)
-    labels = virt.get_instance_labels(frag)[:3]
+    all_labels = virt.get_instance_labels(frag)
+    labels = [all_labels[0], all_labels[500], all_labels[1295]]
     jobs = build_jobs(prog, labels)
     enc = sweep_plan.encode(prog)
     assert not enc.packed and len(enc.passes) >= 2
