@@ -306,6 +306,34 @@ __device__ __forceinline__ void dispatch_cx(int c, int t, double2 (&v)[PER]) {
     }
 }
 
+// out = variant 0 of p (N doubles), or variant 1 where `b` (only if the op has that bit, `h`).
+// `h` is wave-uniform, so the second variant's loads stay scalar; `b` is per lane.
+template <int N>
+__device__ __forceinline__ void select_variant(double (&out)[N], const double* p, bool h, bool b) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) out[k] = p[k];
+    if (h) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const double alt = p[N + k];
+            out[k] = b ? alt : out[k];
+        }
+    }
+}
+
+// Variant index b1 + 2*b2 over up to four N-double variants (SCALE/SCALER encoding).
+template <int N>
+__device__ __forceinline__ void select_variant4(double (&out)[N], const double* p, bool h1, bool b1, bool h2,
+                                                bool b2) {
+    select_variant<N>(out, p, h1, b1);
+    if (h2) {
+        double hi[N];
+        select_variant<N>(hi, p + 2 * N, h1, b1);
+#pragma unroll
+        for (int k = 0; k < N; ++k) out[k] = b2 ? hi[k] : out[k];
+    }
+}
+
 struct SweepArgs {
     const qk_op* ops;
     const qk_group* groups;
@@ -316,6 +344,8 @@ struct SweepArgs {
     double* pjob;    // FINAL: [n_jobs][2^m]
     int64_t n_jobs;
     uint64_t tile_mask;
+    uint64_t zero_mask;  // state elements with any of these bits set are known zero (not loaded)
+    int init_sparse;     // SPLIT INIT pass launched on the |0..0>-containing tile of each job only
     int group_begin, group_end;
     int flags;
     uint32_t traced_local;
@@ -337,7 +367,12 @@ __device__ __forceinline__ uint64_t pdep64(uint64_t x, uint64_t mask) {
 // One pass of the batched sweep. PACKED: a tile = 2^(12-n_eff) whole jobs. SPLIT: a tile =
 // 12 state bits (tile_mask) of one job, 2^(n-12) tiles per job.
 template <bool PACKED>
-__global__ __launch_bounds__(NT) void qk_sweep_pass_kernel(SweepArgs a) {
+// The program (ops, groups, mats) comes in as separate __restrict__ read-only pointers so the
+// compiler can prove it uniform and unclobbered: it then uses scalar (K$) loads instead of a
+// vector-memory round trip per op.
+__global__ __launch_bounds__(NT) void qk_sweep_pass_kernel(SweepArgs a, const qk_op* __restrict__ g_ops,
+                                                           const qk_group* __restrict__ g_groups,
+                                                           const double* __restrict__ g_mats) {
     __shared__ double2 lds[TILE];
     const int tid = threadIdx.x;
     const bool init = a.flags & 1;
@@ -350,7 +385,7 @@ __global__ __launch_bounds__(NT) void qk_sweep_pass_kernel(SweepArgs a) {
     if (PACKED) {
         job0 = (int64_t)blockIdx.x << (QK_TILE_BITS - a.n_eff);
     } else {
-        const int64_t tiles_per_job = (int64_t)1 << (a.n - QK_TILE_BITS);
+        const int64_t tiles_per_job = a.init_sparse ? 1 : ((int64_t)1 << (a.n - QK_TILE_BITS));
         job0 = (int64_t)blockIdx.x / tiles_per_job;
         const uint64_t tj = (uint64_t)((int64_t)blockIdx.x % tiles_per_job);
         const uint64_t nmask = (a.n >= 64) ? ~0ull : ((1ull << a.n) - 1);
@@ -372,6 +407,19 @@ __global__ __launch_bounds__(NT) void qk_sweep_pass_kernel(SweepArgs a) {
     const int64_t njobs = a.n_jobs;
     const int64_t stride_job = PACKED ? 0 : ((int64_t)1 << a.n);
 
+    // A SPLIT tile of |0..0> with a non-zero outside part is all zeros and stays zero under the
+    // pass (tile-local unitaries + diagonal action): store zeros, skip the groups.
+    bool zero_tile = false;
+    if (!PACKED && init && tbase != 0) {
+        if (!final_) {
+            double2* dst = a.state + job0 * stride_job;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) dst[local_to_state(tid + NT * i)] = make_double2(0.0, 0.0);
+            return;
+        }
+        zero_tile = true;
+    }
+
     // ---- load or initialise the tile
     if (init) {
         const int nmask = (1 << a.n_eff) - 1;
@@ -383,17 +431,19 @@ __global__ __launch_bounds__(NT) void qk_sweep_pass_kernel(SweepArgs a) {
         }
     } else {
         const double2* src = a.state + job0 * stride_job;
+        const uint64_t zm = a.zero_mask;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int t = tid + NT * i;
-            lds[swz(t)] = src[local_to_state(t)];
+            const uint64_t s = local_to_state(t);
+            lds[swz(t)] = (s & zm) ? make_double2(0.0, 0.0) : src[s];
         }
     }
     __syncthreads();
 
     // ---- fiber groups
-    for (int g = a.group_begin; g < a.group_end; ++g) {
-        const qk_group grp = a.groups[g];
+    for (int g = a.group_begin; !zero_tile && g < a.group_end; ++g) {
+        const qk_group grp = g_groups[g];
         const int p0 = grp.pos[0], p1 = grp.pos[1], p2 = grp.pos[2], p3 = grp.pos[3];
         const int fmask = (1 << p0) | (1 << p1) | (1 << p2) | (1 << p3);
         // base local index: deposit tid into the 8 non-fiber positions
@@ -429,34 +479,51 @@ __global__ __launch_bounds__(NT) void qk_sweep_pass_kernel(SweepArgs a) {
         const int64_t job_c = job < njobs ? job : njobs - 1;  // padded tile slots reuse a valid row
 
         for (int o = grp.op_begin; o < grp.op_end; ++o) {
-            const qk_op op = a.ops[o];
-            int var = 0;
-            if (op.e1 >= 0) var |= (int)((sbase >> op.e1) & 1);
-            if (op.e2 >= 0) var |= (int)((sbase >> op.e2) & 1) << 1;
+            const qk_op op = g_ops[o];
+            // Matrix data is read at uniform addresses (scalar loads); a per-lane variant chosen by
+            // external state bits is then picked with selects, never with per-lane addresses.
+            const double* mp = g_mats + op.mat;
+            const bool h1 = op.e1 >= 0, h2 = op.e2 >= 0;
+            const bool b1 = h1 && ((sbase >> op.e1) & 1);
+            const bool b2 = h2 && ((sbase >> op.e2) & 1);
             switch (op.kind) {
-                case QK_U1: dispatch_u1(op.a, v, a.mats + op.mat + 8 * var); break;
-                case QK_D1: dispatch_d1(op.a, v, a.mats + op.mat + 4 * var); break;
+                case QK_U1: {
+                    double m[8];
+                    select_variant<8>(m, mp, h1, b1);
+                    dispatch_u1(op.a, v, m);
+                } break;
+                case QK_D1: {
+                    double m[4];
+                    select_variant<4>(m, mp, h1, b1);
+                    dispatch_d1(op.a, v, m);
+                } break;
                 case QK_SLOT:
                     dispatch_u1(op.a, v, a.job_slots + (job_c * a.n_slots + op.slot) * 8);
                     break;
-                case QK_U2: dispatch_u2(op.a, op.b, v, a.mats + op.mat); break;
-                case QK_D2: dispatch_d2(op.a, op.b, v, a.mats + op.mat); break;
+                case QK_U2: dispatch_u2(op.a, op.b, v, mp); break;
+                case QK_D2: dispatch_d2(op.a, op.b, v, mp); break;
                 case QK_CX: dispatch_cx(op.a, op.b, v); break;
                 case QK_SWAP: dispatch_swap(op.a, op.b, v); break;
                 case QK_SCALE: {
-                    const double* s = a.mats + op.mat + 2 * var;
-                    const double sr = s[0], si = s[1];
+                    double s[2];
+                    select_variant4<2>(s, mp, h1, b1, h2, b2);
 #pragma unroll
-                    for (int r = 0; r < PER; ++r) v[r] = cmul(sr, si, v[r]);
+                    for (int r = 0; r < PER; ++r) v[r] = cmul(s[0], s[1], v[r]);
+                    pin(v);
                 } break;
-                case QK_U1R: dispatch_u1r(op.a, v, a.mats + op.mat); break;
-                case QK_U1X: dispatch_u1x(op.a, v, a.mats + op.mat); break;
-                case QK_D1R: dispatch_d1r(op.a, v, a.mats + op.mat + 2 * var); break;
-                case QK_D2R: dispatch_d2r(op.a, op.b, v, a.mats + op.mat); break;
+                case QK_U1R: dispatch_u1r(op.a, v, mp); break;
+                case QK_U1X: dispatch_u1x(op.a, v, mp); break;
+                case QK_D1R: {
+                    double m[2];
+                    select_variant<2>(m, mp, h1, b1);
+                    dispatch_d1r(op.a, v, m);
+                } break;
+                case QK_D2R: dispatch_d2r(op.a, op.b, v, mp); break;
                 case QK_SCALER: {
-                    const double s = a.mats[op.mat + var];
+                    double s[1];
+                    select_variant4<1>(s, mp, h1, b1, h2, b2);
 #pragma unroll
-                    for (int r = 0; r < PER; ++r) v[r] = make_double2(s * v[r].x, s * v[r].y);
+                    for (int r = 0; r < PER; ++r) v[r] = make_double2(s[0] * v[r].x, s[0] * v[r].y);
                     pin(v);
                 } break;
                 default: break;
@@ -753,15 +820,23 @@ int qk_sweep(qk_ctx* ctx, const qk_program* p, int64_t n_jobs, const double* job
         a.group_end = ps.group_end;
         a.flags = ps.flags;
         a.traced_local = ps.traced_local;
+        // A SPLIT INIT pass that is not also FINAL only needs the tile holding |0..0> of each job
+        // (every other tile is zero and stays zero); the next pass then treats the elements
+        // outside that tile as known zeros instead of reading them.
+        const uint64_t nmask = (p->n >= 64) ? ~0ull : ((1ull << p->n) - 1);
+        a.init_sparse = (!p->packed && ip == 0 && p->n_passes > 1) ? 1 : 0;
+        a.zero_mask = (!p->packed && ip == 1) ? (nmask & ~p->passes[0].tile_mask) : 0;
         if (p->packed) {
             const int64_t per = (int64_t)1 << (QK_TILE_BITS - p->n_eff);
             const int64_t blocks = (n_jobs + per - 1) / per;
             if (blocks > 0x7fffffff) return fail(ctx, QK_EARG, "qk_sweep: too many jobs%s");
-            hipLaunchKernelGGL(qk_sweep_pass_kernel<true>, dim3((unsigned)blocks), dim3(NT), 0, ctx->stream, a);
+            hipLaunchKernelGGL(qk_sweep_pass_kernel<true>, dim3((unsigned)blocks), dim3(NT), 0, ctx->stream, a,
+                               a.ops, a.groups, a.mats);
         } else {
-            const int64_t blocks = n_jobs << (p->n - QK_TILE_BITS);
+            const int64_t blocks = a.init_sparse ? n_jobs : (n_jobs << (p->n - QK_TILE_BITS));
             if (blocks > 0x7fffffff) return fail(ctx, QK_EARG, "qk_sweep: too many tiles%s");
-            hipLaunchKernelGGL(qk_sweep_pass_kernel<false>, dim3((unsigned)blocks), dim3(NT), 0, ctx->stream, a);
+            hipLaunchKernelGGL(qk_sweep_pass_kernel<false>, dim3((unsigned)blocks), dim3(NT), 0, ctx->stream, a,
+                               a.ops, a.groups, a.mats);
         }
         QK_HIP(ctx, hipGetLastError());
     }
