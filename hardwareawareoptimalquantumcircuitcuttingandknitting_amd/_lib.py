@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libqknit.so")
+LIB_PATH = os.environ.get("QKNIT_LIB") or os.path.join(_HERE, "libqknit.so")
 
 c_i32, c_i64, c_u32, c_u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64
 c_vp, c_dp, c_lp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)
@@ -43,6 +43,10 @@ SIGNATURES = {
                               c_vp, c_i64, c_vp, ctypes.c_int]),
     "qk_khatri_rao": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "qk_gather_rows": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "qk_npd_workspace_bytes": (c_i32, [c_i64, c_i64, ctypes.POINTER(c_i64)]),
+    "qk_threshold_count": (c_i32, [c_vp, c_i64, c_vp, ctypes.c_double, c_vp, c_i64, c_vp]),
+    "qk_npd": (c_i32, [c_vp, c_i64, c_vp, ctypes.c_double, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "qk_hellinger": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp]),
 }
 
 _lock = threading.Lock()

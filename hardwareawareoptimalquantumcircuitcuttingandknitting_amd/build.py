@@ -6,7 +6,8 @@ import shutil
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "qknit.hip")
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("qknit.hip", "qknit_post.hip")]
+DEPS = SRCS + [os.path.join(HERE, "csrc", "internal.h")]
 HEADER = os.path.join(os.path.dirname(HERE), "include", "qknit.h")
 OUT = os.path.join(HERE, "libqknit.so")
 ARCH = os.environ.get("QKNIT_ARCH", "gfx950")
@@ -21,13 +22,13 @@ def hipcc() -> str:
 
 def build_library(force: bool = False, verbose: bool = False) -> str:
     stale = not os.path.exists(OUT) or any(
-        os.path.getmtime(p) > os.path.getmtime(OUT) for p in (SRC, HEADER)
+        os.path.getmtime(p) > os.path.getmtime(OUT) for p in DEPS + [HEADER]
     )
     if not (force or stale):
         return OUT
     tmp = OUT + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-result", SRC, "-o", tmp]
+           "-Wall", "-Wno-unused-result", *SRCS, "-o", tmp]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{res.stderr}")

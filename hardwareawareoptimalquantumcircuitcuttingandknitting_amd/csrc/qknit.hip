@@ -14,14 +14,7 @@
 #include <cstring>
 #include <string>
 
-#include "../../include/qknit.h"
-
-struct qk_ctx {
-    int device;
-    hipStream_t own;
-    hipStream_t stream;
-    std::string err;
-};
+#include "internal.h"
 
 namespace {
 

@@ -480,6 +480,51 @@ def contract(ctx, mats: list, clbits: list, out, row_block=None, gemm=None, kr=N
     return gemm(A.contiguous(), B.contiguous(), keyA=kA, strideA=sA, keyB=kB, strideB=sB, out=out)
 
 
+def nearest_probability_distribution(ctx: Context, dense, accuracy: float):
+    """Reference-shaped result of a dense distribution, computed on the GPU.
+
+    ``QuasiDistr`` truncation (``|v| > accuracy``, ``quasi_distr.py:7-10``) followed by
+    ``nearest_probability_distribution`` (``quasi_distr.py:28-43``): returns
+    ``(keys, values)`` host arrays in ascending value order (the reference dict's order).
+    """
+    T = torch()
+    dense = dense.contiguous().view(-1)
+    n = dense.numel()
+    dev = dense.device
+    ws_small = ctypes.c_int64()
+    ctx.check(ctx.lib.qk_npd_workspace_bytes(n, 0, ctypes.byref(ws_small)), "qk_npd_workspace_bytes")
+    ws = T.empty(max(ws_small.value, 1), dtype=T.uint8, device=dev)
+    cnt = T.zeros(1, dtype=T.int64, device=dev)
+    ctx.check(ctx.lib.qk_threshold_count(ctx.handle, n, dense.data_ptr(), float(accuracy), ws.data_ptr(),
+                                         ws.numel(), cnt.data_ptr()), "qk_threshold_count")
+    count = int(cnt.item())
+    need = ctypes.c_int64()
+    ctx.check(ctx.lib.qk_npd_workspace_bytes(n, count, ctypes.byref(need)), "qk_npd_workspace_bytes")
+    if need.value > ws.numel():
+        ws = T.empty(need.value, dtype=T.uint8, device=dev)
+    keys = T.empty(max(count, 1), dtype=T.int64, device=dev)
+    vals = T.empty(max(count, 1), dtype=T.float64, device=dev)
+    n_out = T.zeros(1, dtype=T.int64, device=dev)
+    ctx.check(ctx.lib.qk_npd(ctx.handle, n, dense.data_ptr(), float(accuracy), count, ws.data_ptr(), ws.numel(),
+                             keys.data_ptr(), vals.data_ptr(), n_out.data_ptr()), "qk_npd")
+    k = int(n_out.item())
+    return keys[:k].cpu().numpy(), vals[:k].cpu().numpy()
+
+
+def hellinger_fidelity(ctx: Context, p, q) -> float:
+    """Hellinger fidelity of two dense distributions (qiskit ``hellinger_fidelity``, as used at
+    ``Utilities.py:222-224``): ``(sum sqrt(p q) / sqrt(sum p sum q))^2`` with negatives clipped."""
+    T = torch()
+    assert p.numel() == q.numel()
+    acc = T.zeros(3, dtype=T.float64, device=p.device)
+    ctx.check(ctx.lib.qk_hellinger(ctx.handle, p.numel(), p.contiguous().data_ptr(), q.contiguous().data_ptr(),
+                                   acc.data_ptr()), "qk_hellinger")
+    s, sp, sq = acc.cpu().numpy().tolist()
+    if sp <= 0 or sq <= 0:
+        return 0.0
+    return float((s / np.sqrt(sp * sq)) ** 2)
+
+
 def knit_quasi_distrs(virt, results: dict, device: int = 0, factored: bool = False):
     """GPU knit of reference-shaped inputs ``{fragment: [QuasiDistr per label]}``.
 

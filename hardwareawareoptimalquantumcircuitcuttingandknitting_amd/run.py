@@ -96,4 +96,8 @@ def run_virtual_circuit(virt: VirtualCircuit, shots: int = 20000, *, device: int
     out, info = run_virtual_circuit_dense(virt, shots, device=device, factored=factored)
     if dense:
         return out, info
-    return QuasiDistr.from_dense(out).nearest_probability_distribution(), info
+    from . import quasi_distr
+
+    keys, vals = engine.nearest_probability_distribution(engine.get_context(device), out,
+                                                         quasi_distr.ACCURACY)
+    return dict(zip(keys.tolist(), vals.tolist())), info

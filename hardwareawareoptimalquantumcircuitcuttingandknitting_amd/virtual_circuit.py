@@ -44,6 +44,10 @@ def _is_barrier(op) -> bool:
 
 class VirtualCircuit:
     def __init__(self, circuit: QuantumCircuit) -> None:
+        from .ingest import adopt_with_map
+
+        # a foreign (qiskit) cut circuit is rebuilt in this IR; its registers stay valid keys
+        circuit, self._frag_alias = adopt_with_map(circuit)
         self._vgate_instrs = [instr for instr in circuit if _is_vgate(instr.operation)]
         self._circuit = self._replace_vgates_with_endpoints(circuit)
         self._frag_circs = {
@@ -54,9 +58,13 @@ class VirtualCircuit:
         default = MI355XBackend()
         self._frag_to_backend = {qreg: default for qreg in self._frag_circs}
 
+    def _frag(self, fragment):
+        """Translate a caller's (possibly foreign) fragment register to the adopted one."""
+        return self._frag_alias.get(fragment, fragment)
+
     # ------------------------------------------------------------------ labels
     def _touches(self, vg_instr, fragment) -> bool:
-        return bool(set(vg_instr.qubits) & set(fragment))
+        return bool(set(vg_instr.qubits) & set(self._frag(fragment)))
 
     def get_instance_labels(self, fragment) -> list[InstanceLabelType]:
         if not self._vgate_instrs:
@@ -95,7 +103,7 @@ class VirtualCircuit:
         """
         from . import engine
 
-        dense = engine.knit_quasi_distrs(self, results)
+        dense = engine.knit_quasi_distrs(self, {self._frag(f): d for f, d in results.items()})
         return QuasiDistr.from_dense(dense)
 
     # ------------------------------------------------------------------ fragments / backends
@@ -113,14 +121,16 @@ class VirtualCircuit:
         return self._circuit
 
     def replace_fragment_circuit(self, fragment, circuit: QuantumCircuit) -> None:
-        self._frag_circs[fragment] = circuit
+        self._frag_circs[self._frag(fragment)] = circuit
 
     def get_backend(self, fragment):
+        fragment = self._frag(fragment)
         if fragment not in self._frag_to_backend:
             raise ValueError("Fragment not found.")
         return self._frag_to_backend[fragment]
 
     def set_backend(self, fragment, backend) -> None:
+        fragment = self._frag(fragment)
         if fragment not in self._frag_to_backend:
             raise ValueError("Fragment not found.")
         self._frag_to_backend[fragment] = backend

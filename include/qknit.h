@@ -124,6 +124,25 @@ int qk_khatri_rao(qk_ctx* ctx, int64_t K, int64_t M, int64_t N, const double* A,
 int qk_gather_rows(qk_ctx* ctx, int64_t R, int64_t width, const int64_t* idx, const double* coef,
                    const double* src, double* dst);
 
+/* ---- post-processing (reference-shaped results; quasi_distr.py:3-43, run.py:71) ---------- */
+
+/* Workspace for qk_threshold_count / qk_npd over n dense values with `count` kept entries. */
+int qk_npd_workspace_bytes(int64_t n, int64_t count, int64_t* bytes);
+
+/* *count_dev (device int64) = #{i : |vals[i]| > acc}  (QuasiDistr truncation, quasi_distr.py:7-10) */
+int qk_threshold_count(qk_ctx* ctx, int64_t n, const double* vals, double acc, void* ws, int64_t ws_bytes,
+                       int64_t* count_dev);
+
+/* Truncate at acc, then nearest_probability_distribution (quasi_distr.py:28-43): writes the kept
+ * (key, value) pairs ascending by value into out_keys/out_vals (capacity count) and their number
+ * into *n_out_dev (device int64). count must be qk_threshold_count's result. */
+int qk_npd(qk_ctx* ctx, int64_t n, const double* vals, double acc, int64_t count, void* ws, int64_t ws_bytes,
+           int64_t* out_keys, double* out_vals, int64_t* n_out_dev);
+
+/* acc3[0] = sum sqrt(max(p,0) max(q,0)), acc3[1] = sum max(p,0), acc3[2] = sum max(q,0) (device).
+ * Hellinger fidelity = (acc3[0] / sqrt(acc3[1] acc3[2]))^2 (Utilities.py:222-224). */
+int qk_hellinger(qk_ctx* ctx, int64_t n, const double* p, const double* q, double* acc3);
+
 #ifdef __cplusplus
 }
 #endif

@@ -154,6 +154,46 @@ def test_run_virtual_circuit_dict_api(T):
     assert info.run_time > 0
 
 
+@pytest.mark.parametrize("seed,n", [(0, 1), (1, 37), (2, 1000), (3, 1 << 16)])
+def test_gpu_npd_matches_oracle(T, seed, n):
+    """GPU truncation + nearest_probability_distribution == quasi_distr.py:7-10,28-43 (oracle)."""
+    from oracle.quasi import QD
+
+    rng = np.random.default_rng(seed)
+    v = rng.standard_normal(n) * np.where(rng.random(n) < 0.3, 1e-6, 1e-2)
+    v[rng.random(n) < 0.2] *= -1.0
+    ctx = engine.get_context(0)
+    keys, vals = engine.nearest_probability_distribution(ctx, T.from_numpy(v).cuda(), 1e-5)
+    ref = QD({i: float(x) for i, x in enumerate(v)}, 1e-5).npd()
+    assert list(keys) == list(ref.keys())  # same entries, same (ascending-value) order
+    np.testing.assert_allclose(vals, list(ref.values()), rtol=0, atol=1e-15)
+
+
+def test_gpu_hellinger_and_compare_original_with_cut(T):
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import fidelity
+
+    rng = np.random.default_rng(5)
+    p, q = rng.random(4096), rng.random(4096)
+    f = fidelity.hellinger_fidelity_dense(T.from_numpy(p).cuda(), T.from_numpy(q).cuda())
+    ref = (np.sum(np.sqrt(p * q)) / np.sqrt(p.sum() * q.sum())) ** 2
+    assert abs(f - ref) <= 1e-13
+    for case in ("cx_3cuts", "three_wide", "move_gate"):
+        circ, cut = CASES[case]()
+        cmp = fidelity.compare_original_with_cut(circ, cut)
+        assert abs(cmp.cut_vs_uncut_fidelity - 1.0) <= 1e-12
+        np.testing.assert_allclose(cmp.uncut.cpu().numpy(), dense.uncut_distribution(circ), atol=TOL, rtol=0)
+
+
+@pytest.mark.parametrize("case", ["cx_3cuts", "move_gate", "three_wide"])
+def test_foreign_cut_circuit_runs(T, case):
+    """A qiskit-shaped cut circuit goes through run_virtual_circuit unchanged (cut-spec ingestion)."""
+    from foreign import to_foreign
+
+    _, cut = CASES[case]()
+    out, _ = run_virtual_circuit_dense(VirtualCircuit(to_foreign(cut)))
+    np.testing.assert_allclose(out.cpu().numpy(), dense.run_dense(cut), atol=TOL, rtol=0)
+
+
 def test_split_mode_fragment_matches_oracle(T):
     """16-qubit fragments (SPLIT mode, multi-pass) of syc 32 5: all 1296 labels swept, 6 checked."""
     _, cut = cutting.config_cut_circuit("syc", 32, 5, 2)[:2]

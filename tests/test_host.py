@@ -110,6 +110,35 @@ def test_knit_operands_match_oracle_dense_knit(case, factored):
                                          for g in virt.vgate_instructions])
 
 
+@pytest.mark.parametrize("case", ["cx_3cuts", "cp", "rzz", "move_gate", "three", "hwe_p3", "partial"])
+def test_foreign_cut_circuit_ingestion(case):
+    """A qiskit-shaped cut circuit (tests/foreign.py) is adopted into the IR with the same
+    fragments, labels, instance programs and knit as the native one."""
+    from foreign import to_foreign
+
+    _, cut = CASES[case]()
+    native = VirtualCircuit(cut)
+    foreign_circ = to_foreign(cut)
+    virt = VirtualCircuit(foreign_circ)
+    assert [len(f) for f in virt.fragment_circuits] == [len(f) for f in native.fragment_circuits]
+    for fr, fn in zip(foreign_circ.qregs, native.fragment_circuits):
+        assert virt.get_instance_labels(fr) == native.get_instance_labels(fn)
+        virt.set_backend(fr, virt.get_backend(fr))  # foreign registers stay valid keys
+    # same instance programs -> same emulated fragment distributions
+    cl_v, cl_n = engine.clbit_indexer(virt.circuit), engine.clbit_indexer(native.circuit)
+    for (f1, c1), (f2, c2) in zip(virt.fragment_circuits.items(), native.fragment_circuits.items()):
+        if not len(f1):
+            continue
+        p1, p2 = compile_fragment(c1, f1, cl_v), compile_fragment(c2, f2, cl_n)
+        j1, j2 = build_jobs(p1, virt.get_instance_labels(f1)), build_jobs(p2, native.get_instance_labels(f2))
+        np.testing.assert_allclose(j1.slot_mats, j2.slot_mats, atol=1e-15, rtol=0)
+        assert len(p1.ops) == len(p2.ops) and p1.clbits == p2.clbits
+        for a, b in zip(p1.ops, p2.ops):
+            assert a.kind == b.kind and a.qubits == b.qubits
+            if a.mat is not None:
+                np.testing.assert_allclose(a.mat, b.mat, atol=1e-15, rtol=0)
+
+
 def test_syc_32_5_schedule_shape():
     _, cut, desc = cutting.config_cut_circuit("syc", 32, 5, 2)
     virt = VirtualCircuit(cut)

@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Time the knit contraction (qk_gemm_keyed) alone on the syc 32 5 operands.
+
+  python tools/gemm_bench.py [--factored] [--reps 5]
+Prints TF/s per launch (HIP events on the launch stream).
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="syc_32_5_p2")
+    ap.add_argument("--factored", action="store_true")
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    name, n, d, p, var = cutting.BASELINE_CONFIGS[args.workload]
+    _, cut, _ = cutting.config_cut_circuit(name, n, d, p, var)
+    pipe = KnitPipeline(VirtualCircuit(cut), factored=args.factored)
+    qs = pipe.sweep()
+    mats = pipe.operands(qs)
+    pipe.out = pipe._alloc_out(mats)
+    M, N, K = pipe.gemm_shape()
+    flops = 2.0 * M * N * K
+    for r in range(args.reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        pipe._contract(mats)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e)
+        print(f"rep {r}: M={M} N={N} K={K} {ms:.3f} ms  {flops / ms / 1e9:.2f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
