@@ -6,7 +6,7 @@ A step = one full run of the hot path for the workload: batched exact sweep of
 every cut instance of every fragment + the dense fp64 knit of the complete
 2^32-entry distribution (inputs = compiled plan, resident on the GPU).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload syc_32_5_p2] [--factored]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload syc_32_5_p2] [--direct]
   N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 value = reference-counted instances (sum over fragments of their label lists, run.py:37-39)
@@ -31,7 +31,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="syc_32_5_p2")
-    ap.add_argument("--factored", action="store_true", help="rank-factored knit (exact, fewer flops)")
+    ap.add_argument("--direct", action="store_true",
+                    help="direct knit over all global labels (K = prod n_inst) instead of the "
+                         "default rank-factored knit (K = 4^cuts; exact, same result)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-labels", type=int, default=12)
     return ap.parse_args()
@@ -92,6 +94,23 @@ def cpu_baseline(cut, n_labels_sample: int):
     }
 
 
+def traffic_per_launch(M, N, K):
+    """HBM bytes per knit-GEMM launch from the committed PMC summary (profiles/*traffic*.json,
+    written by tools/pmc_traffic.py from a rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE pass of this
+    bench), matched on the GEMM shape; None if no summary for this shape exists."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))):
+        try:
+            rec = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if rec.get("gemm_mnk") == [M, N, K]:
+            best = rec
+    return None if best is None else best["hbm_bytes_per_launch"]
+
+
 def main():
     args = parse()
     import torch
@@ -111,7 +130,7 @@ def main():
     circ, cut, desc = cutting.config_cut_circuit(name, n, d, p, variant)
     virt = VirtualCircuit(cut)
     torch.cuda.set_device(local)
-    pipe = KnitPipeline(virt, device=local, factored=args.factored, rank=rank, world=world)
+    pipe = KnitPipeline(virt, device=local, factored=not args.direct, rank=rank, world=world)
     counts = pipe.instance_counts()
 
     def barrier():
@@ -165,9 +184,11 @@ def main():
             "workload": f"{name} {n} {d} p={p}" + (" (forced cuts)" if variant == "forced" else ""),
             "cuts": desc,
             "instances_ref": counts["instances_ref"],
+            "instances_unique": counts["instances_unique"],
             "branch_jobs": counts["branch_jobs"],
             "labels": counts["labels"],
-            "knit": "factored" if args.factored else "direct",
+            "knit": "direct" if args.direct else "factored",
+            "gemm_mnk": [M, Nn, K],
             "output_entries": 1 << pipe.N,
             "parallelism": f"labels x{world} ({pipe.mode})",
         },
@@ -178,7 +199,7 @@ def main():
             "peak": FP64_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
-            "traffic": None,
+            "traffic": traffic_per_launch(M, Nn, K),
             "flops_per_launch": flops,
             "avg_launch_ms": gemm_ms,
         },

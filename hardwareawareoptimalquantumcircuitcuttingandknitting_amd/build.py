@@ -20,19 +20,22 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
-def build_library(force: bool = False, verbose: bool = False) -> str:
-    stale = not os.path.exists(OUT) or any(
-        os.path.getmtime(p) > os.path.getmtime(OUT) for p in DEPS + [HEADER]
+def build_library(force: bool = False, verbose: bool = False, out: str = OUT,
+                  defines: tuple = ()) -> str:
+    """Build ``out`` (default: the in-tree libqknit.so). ``defines`` are extra ``-D`` macros,
+    used only by tools/ to build kernel-tuning variants next to the product library."""
+    stale = not os.path.exists(out) or any(
+        os.path.getmtime(p) > os.path.getmtime(out) for p in DEPS + [HEADER]
     )
     if not (force or stale):
-        return OUT
-    tmp = OUT + ".tmp"
+        return out
+    tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-result", *SRCS, "-o", tmp]
+           "-Wall", "-Wno-unused-result", *[f"-D{d}" for d in defines], *SRCS, "-o", tmp]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{res.stderr}")
     if verbose and res.stderr:
         print(res.stderr)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out

@@ -585,44 +585,113 @@ constexpr int GT = 128;      // workgroup tile (M and N)
 constexpr int GK = 16;       // K chunk
 constexpr int GPAD = 16;     // LDS row padding (doubles): 1152-B rows avoid the 2-way conflict
 
-// Loads this thread's 8 consecutive columns of chunk row `kr` (zero outside [0,K) x [0,cols)).
-__device__ __forceinline__ void gemm_load8(double (&r)[8], const double* __restrict__ X, int64_t ld,
-                                           int64_t kr, int64_t K, int64_t c0, int64_t cols, bool vec) {
-    if (vec && kr < K && c0 + 8 <= cols) {
-        const double2* p = reinterpret_cast<const double2*>(X + kr * ld + c0);
+#ifndef QK_GEMM_GROUP
+#define QK_GEMM_GROUP 8  // tile rows per L2 group (0 = plain column-major tile order)
+#endif
+#ifndef QK_GEMM_NT
+#define QK_GEMM_NT 1     // non-temporal output stores (the 2^N output is written once)
+#endif
+
+typedef double d2_t __attribute__((ext_vector_type(2)));
+
+// Loads this thread's share of chunk rows [k0, k0+GK): rows k0 + (tid>>6) + 4j, columns
+// c0 + 2*(tid&63) + {0,1}. A wave reads one contiguous 1-KiB row segment per j (coalesced) and
+// later writes it to LDS as one contiguous 1-KiB run (conflict-free ds_write_b128). `full` is
+// workgroup-uniform (whole chunk in range, 16-B aligned), so the fast path is branch-free.
+__device__ __forceinline__ void gemm_load(d2_t (&r)[4], const double* __restrict__ X, int64_t ld,
+                                          int64_t k0, int64_t K, int64_t c0, int64_t cols, bool full) {
+    // uniform chunk base and row steps, one per-lane offset
+    const double* p = X + k0 * ld + c0;
+    const int rl = threadIdx.x >> 6, cl = 2 * (threadIdx.x & 63);
+    const int64_t off = (int64_t)rl * ld + cl;
+    if (full) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const double2 v = p[c];
-            r[2 * c] = v.x;
-            r[2 * c + 1] = v.y;
-        }
+        for (int j = 0; j < 4; ++j) r[j] = *reinterpret_cast<const d2_t*>(p + 4 * j * ld + off);
     } else {
+        const int kl = (int)(K - k0 < GK ? K - k0 : GK);
+        const int cc = (int)(cols - c0 < GT ? cols - c0 : GT);
 #pragma unroll
-        for (int c = 0; c < 8; ++c) r[c] = (kr < K && c0 + c < cols) ? X[kr * ld + c0 + c] : 0.0;
+        for (int j = 0; j < 4; ++j) {
+            const double* q = p + 4 * j * ld + off;
+            const bool rv = rl + 4 * j < kl;
+            r[j].x = (rv && cl < cc) ? q[0] : 0.0;
+            r[j].y = (rv && cl + 1 < cc) ? q[1] : 0.0;
+        }
     }
 }
 
-// One 128x128 output tile per 256-thread workgroup (2x2 waves of 64x64 = 4x4 MFMA 16x16x4 f64
-// tiles each). K is streamed in 16-row chunks: the next chunk's global loads are issued into
+__device__ __forceinline__ void gemm_store_out(double* p, double v) {
+#if QK_GEMM_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
+#ifndef QK_GEMM_PERSIST
+#define QK_GEMM_PERSIST 1  // persistent workgroups looping over tiles (stores overlap next tile)
+#endif
+#ifndef QK_GEMM_WG_PER_CU
+#define QK_GEMM_WG_PER_CU 2
+#endif
+
+struct GemmArgs {
+    int64_t M, N, K;
+    const double* __restrict__ A;
+    int64_t lda;
+    const double* __restrict__ B;
+    int64_t ldb;
+    const int64_t* __restrict__ keyA;
+    int64_t strideA;
+    const int64_t* __restrict__ keyB;
+    int64_t strideB;
+    double* __restrict__ out;
+    int beta;
+    int64_t tiles_m, tiles_n;
+};
+
+// Tile sequence index -> (bm, bn): QK_GEMM_GROUP tile rows x all tile columns, row fastest, so
+// the ~64 tiles an XCD holds at once span 8 A panels x 8 B panels that stay in its 4 MiB L2.
+__device__ __forceinline__ void gemm_tile_coords(int64_t seq, int64_t tiles_m, int64_t tiles_n,
+                                                 int64_t& bm, int64_t& bn) {
+#if QK_GEMM_GROUP
+    const int64_t per_group = (int64_t)QK_GEMM_GROUP * tiles_n;
+    const int64_t g = seq / per_group, r = seq - g * per_group;
+    const int64_t first = g * QK_GEMM_GROUP;
+    const int64_t gsize = tiles_m - first < QK_GEMM_GROUP ? tiles_m - first : QK_GEMM_GROUP;
+    bm = first + r % gsize;
+    bn = r / gsize;
+#else
+    bm = seq % tiles_m;
+    bn = seq / tiles_m;
+#endif
+}
+
+// One 128x128 output tile by one 256-thread workgroup (2x2 waves of 64x64 = 4x4 MFMA 16x16x4
+// f64 tiles each). K is streamed in 16-row chunks: the next chunk's global loads are issued into
 // registers before the current chunk's MFMAs (software pipeline), LDS is double buffered so a
-// chunk costs one barrier.
-__global__ __launch_bounds__(256, 2) void qk_gemm_keyed_kernel(
-    int64_t M, int64_t N, int64_t K, const double* __restrict__ A, int64_t lda,
-    const double* __restrict__ B, int64_t ldb, const int64_t* __restrict__ keyA, int64_t strideA,
-    const int64_t* __restrict__ keyB, int64_t strideB, double* __restrict__ out, int beta,
-    int64_t tiles_m, int64_t tiles_n) {
-    __shared__ double As[2][GK][GT + GPAD];
-    __shared__ double Bs[2][GK][GT + GPAD];
+// chunk costs one barrier. `buf` carries the LDS buffer parity across the tiles of a persistent
+// workgroup: the first store of the next tile goes to the buffer the last chunk did not read.
+__device__ __forceinline__ bool gemm_vec(const double* X, int64_t ld, int64_t c0, int64_t cols) {
+    return ((ld & 1) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && c0 + GT <= cols;
+}
+
+// Chunk 0 of tile (bm, bn) into registers.
+__device__ __forceinline__ void gemm_load_first(const GemmArgs& g, int64_t bm, int64_t bn, d2_t (&ra)[4],
+                                                d2_t (&rb)[4]) {
+    gemm_load(ra, g.A, g.lda, 0, g.K, bm * GT, g.M, gemm_vec(g.A, g.lda, bm * GT, g.M) && GK <= g.K);
+    gemm_load(rb, g.B, g.ldb, 0, g.K, bn * GT, g.N, gemm_vec(g.B, g.ldb, bn * GT, g.N) && GK <= g.K);
+}
+
+// ra/rb hold chunk 0 of this tile on entry; during the last chunk the next tile's chunk 0 is
+// prefetched into them (have_next), so a persistent workgroup never waits on a cold first load.
+__device__ __forceinline__ void gemm_tile(const GemmArgs& g, int64_t bm, int64_t bn, bool have_next,
+                                          int64_t nbm, int64_t nbn, d2_t (&ra)[4], d2_t (&rb)[4],
+                                          double (*As)[GK][GT + GPAD], double (*Bs)[GK][GT + GPAD],
+                                          int& buf) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
-
-    // XCD-aware mapping: the dispatcher deals consecutive block ids round-robin over the 8 XCDs,
-    // so hand each XCD a contiguous run of tiles (tiles sharing a B panel share its L2).
-    const int64_t nblk = tiles_m * tiles_n;
-    int64_t bid = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-    if (bid >= nblk) return;
-    if (nblk % 8 == 0) bid = (bid % 8) * (nblk / 8) + bid / 8;
-    const int64_t bm = bid % tiles_m, bn = bid / tiles_m;
+    const int64_t M = g.M, N = g.N, K = g.K;
     const int64_t m0 = bm * GT, n0 = bn * GT;
 
     d4_t acc[4][4];
@@ -631,24 +700,23 @@ __global__ __launch_bounds__(256, 2) void qk_gemm_keyed_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = (d4_t){0.0, 0.0, 0.0, 0.0};
 
-    const int lr = tid >> 4;        // chunk row 0..15
-    const int lc = (tid & 15) * 8;  // 8 columns per thread
-    const bool vecA = ((lda & 1) == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
-    const bool vecB = ((ldb & 1) == 0) && ((reinterpret_cast<uintptr_t>(B) & 15) == 0);
-    double ra[8], rb[8];
-    gemm_load8(ra, A, lda, lr, K, m0 + lc, M, vecA);
-    gemm_load8(rb, B, ldb, lr, K, n0 + lc, N, vecB);
-    int buf = 0;
+    const int lr = tid >> 6;        // first chunk row of this thread (rows lr + 4j)
+    const int lc = 2 * (tid & 63);  // two columns per thread
     for (int64_t k0 = 0; k0 < K; k0 += GK) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            As[buf][lr][lc + c] = ra[c];
-            Bs[buf][lr][lc + c] = rb[c];
+        for (int j = 0; j < 4; ++j) {
+            *reinterpret_cast<d2_t*>(&As[buf][lr + 4 * j][lc]) = ra[j];
+            *reinterpret_cast<d2_t*>(&Bs[buf][lr + 4 * j][lc]) = rb[j];
         }
         __syncthreads();
-        if (k0 + GK < K) {  // prefetch the next chunk while this one is multiplied
-            gemm_load8(ra, A, lda, k0 + GK + lr, K, m0 + lc, M, vecA);
-            gemm_load8(rb, B, ldb, k0 + GK + lr, K, n0 + lc, N, vecB);
+        // prefetch the next chunk (this tile's, else chunk 0 of the next tile) during the MFMAs
+        const bool more = k0 + GK < K;
+        if (more || have_next) {
+            const int64_t pk = more ? k0 + GK : 0;
+            const int64_t pm = more ? m0 : nbm * GT, pn = more ? n0 : nbn * GT;
+            const bool kfull = pk + GK <= K;
+            gemm_load(ra, g.A, g.lda, pk, K, pm, M, gemm_vec(g.A, g.lda, pm, M) && kfull);
+            gemm_load(rb, g.B, g.ldb, pk, K, pn, N, gemm_vec(g.B, g.ldb, pn, N) && kfull);
         }
 #pragma unroll
         for (int kk = 0; kk < GK / 4; ++kk) {
@@ -667,25 +735,75 @@ __global__ __launch_bounds__(256, 2) void qk_gemm_keyed_kernel(
         }
         buf ^= 1;
     }
-    // epilogue: f64 16x16 C layout: col = lane & 15, row = (lane >> 4) + 4 * r
+    // epilogue: f64 16x16 C layout: col = lane & 15, row = (lane >> 4) + 4 * r. Output offsets
+    // are key(row) + key(col) (keys >= 0; -1 marks a row/column outside the matrix).
+    int64_t kcol[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
-        if (col >= N) continue;
-        const int64_t kcol = keyB ? keyB[col] : col * strideB;
+        kcol[j] = col < N ? (g.keyB ? g.keyB[col] : col * g.strideB) : -1;
+    }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4; ++i) {
+        int64_t krow[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
+            krow[r] = row < M ? (g.keyA ? g.keyA[row] : row * g.strideA) : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
-                if (row < M) {
-                    const int64_t o = (keyA ? keyA[row] : row * strideA) + kcol;
-                    const double val = acc[i][j][r];
-                    out[o] = beta ? out[o] + val : val;
-                }
+#ifdef QK_GEMM_NOSTORE  // tuning experiment only: MFMA + operand traffic without the output
+                if (acc[i][j][r] != 1234.5678) continue;
+#endif
+                if (krow[r] < 0 || kcol[j] < 0) continue;
+                double* o = g.out + krow[r] + kcol[j];
+                if (g.beta) *o += acc[i][j][r];
+                else gemm_store_out(o, acc[i][j][r]);
             }
-        }
     }
+}
+
+// XCD-aware schedule: the dispatcher deals consecutive workgroup ids round-robin over the 8
+// XCDs, so each XCD is handed a contiguous eighth of the (grouped) tile sequence. Persistent
+// mode launches QK_GEMM_WG_PER_CU workgroups per CU; each walks its XCD's eighth with stride =
+// the XCD's workgroup count, so one tile's output stores drain while the next tile's loads and
+// MFMAs issue.
+__global__ __launch_bounds__(256, 2) void qk_gemm_keyed_kernel(GemmArgs g) {
+    __shared__ __attribute__((aligned(16))) double As[2][GK][GT + GPAD];
+    __shared__ __attribute__((aligned(16))) double Bs[2][GK][GT + GPAD];
+    const int64_t nblk = g.tiles_m * g.tiles_n;
+    int buf = 0;
+    int64_t bm, bn;
+#if QK_GEMM_PERSIST
+    const int64_t G = gridDim.x;  // multiple of 8 when nblk % 8 == 0 (host)
+    const bool xcd = nblk % 8 == 0 && G % 8 == 0;
+    const int64_t per_xcd = xcd ? nblk / 8 : nblk, stride = xcd ? G / 8 : G;
+    const int64_t base = xcd ? (blockIdx.x % 8) * per_xcd : 0;
+    int64_t li = xcd ? blockIdx.x / 8 : blockIdx.x;
+    if (li >= per_xcd) return;
+    d2_t ra[4], rb[4];
+    gemm_tile_coords(base + li, g.tiles_m, g.tiles_n, bm, bn);
+    gemm_load_first(g, bm, bn, ra, rb);
+    for (; li < per_xcd; li += stride) {
+        const bool have_next = li + stride < per_xcd;
+        int64_t nbm = 0, nbn = 0;
+        if (have_next) gemm_tile_coords(base + li + stride, g.tiles_m, g.tiles_n, nbm, nbn);
+        gemm_tile(g, bm, bn, have_next, nbm, nbn, ra, rb, As, Bs, buf);
+        bm = nbm;
+        bn = nbn;
+    }
+#else
+    int64_t bid = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    if (bid >= nblk) return;
+    if (nblk % 8 == 0) bid = (bid % 8) * (nblk / 8) + bid / 8;
+    gemm_tile_coords(bid, g.tiles_m, g.tiles_n, bm, bn);
+    d2_t ra[4], rb[4];
+    gemm_load_first(g, bm, bn, ra, rb);
+    gemm_tile(g, bm, bn, false, 0, 0, ra, rb, As, Bs, buf);
+#endif
 }
 
 __global__ void qk_khatri_rao_kernel(int64_t K, int64_t M, int64_t N, const double* __restrict__ A,
@@ -859,13 +977,22 @@ int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A,
     if (lda < M || ldb < N) return fail(ctx, QK_EARG, "qk_gemm_keyed: leading dimension too small%s");
     const int64_t tm = (M + GT - 1) / GT, tn = (N + GT - 1) / GT;
     const int64_t nblk = tm * tn;
+    QK_HIP(ctx, hipSetDevice(ctx->device));
+    GemmArgs g{M, N, K, A, lda, B, ldb, keyA, strideA, keyB, strideB, out, beta, tm, tn};
+#if QK_GEMM_PERSIST
+    int cus = 0;
+    QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    int64_t G = (int64_t)cus * QK_GEMM_WG_PER_CU;
+    G = G < 8 ? 8 : G - G % 8;
+    if (G > nblk) G = nblk;
+    hipLaunchKernelGGL(qk_gemm_keyed_kernel, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
+#else
     // grid.x * blockDim.x must stay below 2^32 work-items: spill tiles into grid.y
     const int64_t gx = nblk < (1 << 20) ? nblk : (1 << 20);
     const int64_t gy = (nblk + gx - 1) / gx;
     if (gy > 65535) return fail(ctx, QK_EARG, "qk_gemm_keyed: too many tiles%s");
-    QK_HIP(ctx, hipSetDevice(ctx->device));
-    hipLaunchKernelGGL(qk_gemm_keyed_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, ctx->stream, M,
-                       N, K, A, lda, B, ldb, keyA, strideA, keyB, strideB, out, beta, tm, tn);
+    hipLaunchKernelGGL(qk_gemm_keyed_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, ctx->stream, g);
+#endif
     QK_HIP(ctx, hipGetLastError());
     return QK_OK;
 }

@@ -16,8 +16,28 @@ def main():
     ap.add_argument("--workload", default="syc_32_5_p2")
     ap.add_argument("--factored", action="store_true")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--synthetic", type=int, nargs=3, metavar=("M", "N", "K"),
+                    help="random operands of this shape, output out[i*N + j] (no circuit)")
     args = ap.parse_args()
     import torch
+
+    if args.synthetic:
+        from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import engine
+
+        M, N, K = args.synthetic
+        ctx = engine.get_context(0)
+        A = torch.randn(K, M, dtype=torch.float64, device="cuda")
+        B = torch.randn(K, N, dtype=torch.float64, device="cuda")
+        out = torch.empty(M * N, dtype=torch.float64, device="cuda")
+        for r in range(args.reps):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            engine.gemm_keyed(ctx, A, B, out=out, strideA=N, strideB=1)
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e)
+            print(f"rep {r}: M={M} N={N} K={K} {ms:.3f} ms  {2.0 * M * N * K / ms / 1e9:.2f} TF/s", flush=True)
+        return
 
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
