@@ -654,16 +654,19 @@ struct GemmArgs {
 // the ~64 tiles an XCD holds at once span 8 A panels x 8 B panels that stay in its 4 MiB L2.
 __device__ __forceinline__ void gemm_tile_coords(int64_t seq, int64_t tiles_m, int64_t tiles_n,
                                                  int64_t& bm, int64_t& bn) {
+    // 32-bit arithmetic (host guarantees tiles_m * tiles_n < 2^31): 64-bit division is a long
+    // software sequence
+    const uint32_t q = (uint32_t)seq, tm = (uint32_t)tiles_m, tn = (uint32_t)tiles_n;
 #if QK_GEMM_GROUP
-    const int64_t per_group = (int64_t)QK_GEMM_GROUP * tiles_n;
-    const int64_t g = seq / per_group, r = seq - g * per_group;
-    const int64_t first = g * QK_GEMM_GROUP;
-    const int64_t gsize = tiles_m - first < QK_GEMM_GROUP ? tiles_m - first : QK_GEMM_GROUP;
+    const uint32_t per_group = (uint32_t)QK_GEMM_GROUP * tn;
+    const uint32_t g = q / per_group, r = q - g * per_group;
+    const uint32_t first = g * QK_GEMM_GROUP;
+    const uint32_t gsize = tm - first < (uint32_t)QK_GEMM_GROUP ? tm - first : (uint32_t)QK_GEMM_GROUP;
     bm = first + r % gsize;
     bn = r / gsize;
 #else
-    bm = seq % tiles_m;
-    bn = seq / tiles_m;
+    bm = q % tm;
+    bn = q / tm;
 #endif
 }
 
@@ -978,6 +981,7 @@ int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A,
     const int64_t tm = (M + GT - 1) / GT, tn = (N + GT - 1) / GT;
     const int64_t nblk = tm * tn;
     QK_HIP(ctx, hipSetDevice(ctx->device));
+    if (nblk >= (int64_t(1) << 31)) return fail(ctx, QK_EARG, "qk_gemm_keyed: too many tiles%s");
     GemmArgs g{M, N, K, A, lda, B, ldb, keyA, strideA, keyB, strideB, out, beta, tm, tn};
 #if QK_GEMM_PERSIST
     int cus = 0;

@@ -426,6 +426,30 @@ def contract_order(clbits: list) -> list:
     return sorted(range(len(clbits)), key=lambda i: -(min(clbits[i]) if clbits[i] else 1 << 62))
 
 
+_KEY_CACHE: dict = {}
+
+
+def _device_keys(clbits: tuple, lo, hi, dev):
+    """Output keys of a fragment's outcomes (deposit of x into its clbit positions), rows
+    [lo, hi), as a device tensor. Cached: a pipeline step must not rebuild them on the host."""
+    key = (clbits, lo, hi, str(dev))
+    k = _KEY_CACHE.get(key)
+    if k is None:
+        T = torch()
+        st = _affine_stride(list(clbits))
+        if st is not None:
+            lo_, hi_ = (0, 1 << len(clbits)) if lo is None else (lo, hi)
+            k = T.arange(lo_, hi_, dtype=T.int64, device=dev) * st
+        else:
+            k = T.from_numpy(deposit_keys(list(clbits))).to(dev)
+            if lo is not None:
+                k = k[lo:hi].contiguous()
+        if len(_KEY_CACHE) > 64:
+            _KEY_CACHE.clear()
+        _KEY_CACHE[key] = k
+    return k
+
+
 def contract(ctx, mats: list, clbits: list, out, row_block=None, gemm=None, kr=None):
     """Dense contraction of the per-fragment operands into `out` (see knit_dense).
 
@@ -443,10 +467,7 @@ def contract(ctx, mats: list, clbits: list, out, row_block=None, gemm=None, kr=N
         st = _affine_stride(c)
         if st is not None and lo is None:
             return None, st
-        if st is not None:
-            return T.arange(lo, hi, dtype=T.int64, device=dev) * st, 0
-        k = T.from_numpy(deposit_keys(c)).to(dev)
-        return (k if lo is None else k[lo:hi].contiguous()), 0
+        return _device_keys(tuple(c), lo, hi, dev), 0
 
     if len(mats) == 1:
         A = mats[0]
@@ -460,10 +481,10 @@ def contract(ctx, mats: list, clbits: list, out, row_block=None, gemm=None, kr=N
         return gemm(A.contiguous(), ones, keyA=kA, strideA=sA, keyB=None, strideB=0, out=out)
     A = mats[0]
     if len(mats) > 2:
-        kA = T.from_numpy(deposit_keys(cls[0])).to(dev)
+        kA = _device_keys(tuple(cls[0]), None, None, dev)
         for B, c in zip(mats[1:-1], cls[1:-1]):
             A = kr(A.contiguous(), B.contiguous())
-            kB = T.from_numpy(deposit_keys(c)).to(dev)
+            kB = _device_keys(tuple(c), None, None, dev)
             kA = (kA.view(1, -1) + kB.view(-1, 1)).reshape(-1)  # index i + j*M
         sA = 0
         if row_block is not None:

@@ -195,3 +195,14 @@ def test_label_space_matches_reference_order():
 def test_deposit_keys():
     k = deposit_keys([0, 3, 5])
     assert k.tolist() == [0, 1, 8, 9, 32, 33, 40, 41]
+
+
+def test_device_keys_cache():
+    import torch
+
+    dev = torch.device("cpu")
+    k = engine._device_keys((2, 3, 4), None, None, dev)
+    assert k.tolist() == [x << 2 for x in range(8)]
+    assert engine._device_keys((2, 3, 4), 2, 5, dev).tolist() == [8, 12, 16]
+    assert engine._device_keys((0, 3, 5), None, None, dev).tolist() == deposit_keys([0, 3, 5]).tolist()
+    assert engine._device_keys((0, 3, 5), 1, 3, dev).tolist() == [1, 8]
