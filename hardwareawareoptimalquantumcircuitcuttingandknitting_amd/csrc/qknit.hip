@@ -620,6 +620,32 @@ __device__ __forceinline__ void gemm_load(d2_t (&r)[4], const double* __restrict
     }
 }
 
+#ifndef QK_GEMM_STORE
+#define QK_GEMM_STORE 2  // 0: per-element stores; 1: paired 16-B nt stores; 2: paired 16-B sc1 stores
+#endif
+
+// Swap a 64-bit value with the neighbouring lane (lane ^ 1).
+template <typename T>
+__device__ __forceinline__ T dpp_swap_pair(T v) {
+    static_assert(sizeof(T) == 8, "64-bit values only");
+    int2 w = *reinterpret_cast<int2*>(&v);
+    w.x = __builtin_amdgcn_mov_dpp(w.x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    w.y = __builtin_amdgcn_mov_dpp(w.y, 0xB1, 0xF, 0xF, false);
+    return *reinterpret_cast<T*>(&w);
+}
+
+// 16-B store of two adjacent outputs. sc1 (write-through) stores do not keep the line in the
+// XCD's L2, so the 2^N output stream does not evict the operand panels other tiles re-read.
+__device__ __forceinline__ void gemm_store_pair(double* p, d2_t v) {
+#if QK_GEMM_STORE == 2
+    // s_nop 1: a >8-B store's data VGPRs must not be rewritten in the next cycle (the hazard
+    // recogniser does not see inside inline asm)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+#else
+    __builtin_nontemporal_store(v, reinterpret_cast<d2_t*>(p));
+#endif
+}
+
 __device__ __forceinline__ void gemm_store_out(double* p, double v) {
 #if QK_GEMM_NT
     __builtin_nontemporal_store(v, p);
@@ -746,6 +772,47 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int64_t bm, int64_t
         const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
         kcol[j] = col < N ? (g.keyB ? g.keyB[col] : col * g.strideB) : -1;
     }
+#if QK_GEMM_STORE
+    // Paired 16-B stores: when every even column's right neighbour is the next output element
+    // (key(c+1) = key(c) + 1, e.g. the fragment holding clbit 0 on the N side), lane pairs swap
+    // one value (DPP quad_perm [1,0,3,2]) so each lane writes two adjacent outputs of one row.
+    bool pairable = !g.beta && n0 + GT <= N;
+    if (pairable) {
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t nb = dpp_swap_pair(kcol[j]);
+            ok = ok && ((lane & 1) ? nb + 1 == kcol[j] : kcol[j] + 1 == nb);
+        }
+        pairable = __all(ok);  // wave-uniform
+    }
+    if (pairable) {
+        const bool odd = lane & 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int rp = 0; rp < 4; rp += 2) {
+                // even lane writes row rp, odd lane row rp+1, both at the even column's key
+                const int rr = rp + (odd ? 1 : 0);
+                const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) + 4 * rr;
+                const int64_t krow = row < M ? (g.keyA ? g.keyA[row] : row * g.strideA) : -1;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const double x = odd ? acc[i][j][rp] : acc[i][j][rp + 1];
+                    const double y = dpp_swap_pair(x);
+                    d2_t v;
+                    v.x = odd ? y : acc[i][j][rp];
+                    v.y = odd ? acc[i][j][rp + 1] : y;
+#ifdef QK_GEMM_NOSTORE
+                    if (v.x != 1234.5678) continue;
+#endif
+                    if (krow >= 0) gemm_store_pair(g.out + krow + kcol[j] - (odd ? 1 : 0), v);
+                }
+            }
+        }
+        return;
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         int64_t krow[4];
