@@ -160,6 +160,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     gemm_ms = sum(s.elapsed_time(e) for s, e in pipe.events) / max(len(pipe.events), 1)
+    sweep_ms = sum(s.elapsed_time(e) for s, e in pipe.sweep_events) / max(len(pipe.sweep_events), 1)
+    traffic = pipe.sweep_traffic()
     M, Nn, K = pipe.gemm_shape()
     flops = 2.0 * M * Nn * K
     achieved = flops / (gemm_ms * 1e-3) / 1e12
@@ -185,6 +187,7 @@ def main():
             "cuts": desc,
             "instances_ref": counts["instances_ref"],
             "instances_unique": counts["instances_unique"],
+            "instances_swept": counts["instances_swept"],
             "branch_jobs": counts["branch_jobs"],
             "labels": counts["labels"],
             "knit": "direct" if args.direct else "factored",
@@ -202,6 +205,17 @@ def main():
             "traffic": traffic_per_launch(M, Nn, K),
             "flops_per_launch": flops,
             "avg_launch_ms": gemm_ms,
+        },
+        "sweep": {
+            "kernel": "qk_sweep_pass_kernel + qk_reduce_labels (all fragments, per step, rank 0)",
+            "bound": "fp64 valu (fused passes move far fewer bytes than the per-gate model)",
+            "ms_per_step": sweep_ms,
+            "branch_jobs": counts["branch_jobs"],
+            "hbm_bytes": traffic["hbm"],
+            "hbm_GBs": traffic["hbm"] / (sweep_ms * 1e-3) / 1e9,
+            "hbm_frac": traffic["hbm"] / (sweep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "algorithmic_bytes": traffic["algorithmic"],
+            "algorithmic_GBs": traffic["algorithmic"] / (sweep_ms * 1e-3) / 1e9,
         },
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -24,7 +24,8 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from .fragment_program import FragmentProgram, JobTable, build_jobs, compile_fragment, dedup_labels
+from .fragment_program import (FragmentProgram, JobTable, basis_reduce, build_jobs, compile_fragment,
+                               dedup_labels)
 from .knit_plan import LabelSpace, deposit_keys, factor_vgate
 from .sweep_plan import EncodedProgram, encode
 
@@ -232,19 +233,36 @@ class FragmentState:
     jobs: JobTable | None
     touches: list
     dropped: bool = False  # reference skips fragments whose counts cannot be read (run.py:57-58)
-    uidx: np.ndarray | None = None  # label -> row of the swept (deduplicated) instance list
+    uidx: np.ndarray | None = None  # label -> row of the deduplicated instance list
     unique_labels: list | None = None
+    # basis reduction (factored knit only): the sweep runs `basis_labels`, and unique instance
+    # u is `expand[u] @ q_basis` (fragment_program.basis_reduce)
+    basis_labels: list | None = None
+    expand: np.ndarray | None = None
+
+    @property
+    def swept_labels(self) -> list:
+        if self.basis_labels is not None:
+            return self.basis_labels
+        return self.unique_labels if self.unique_labels is not None else self.labels
 
     @property
     def n_rows(self) -> int:
-        """Rows of the swept q_f (unique instances)."""
-        return len(self.unique_labels) if self.unique_labels is not None else len(self.labels)
+        """Rows of the swept q_f (unique instances, or basis instances)."""
+        return len(self.swept_labels)
 
     def row_of_label(self) -> np.ndarray:
+        if self.expand is not None:
+            raise ValueError("basis-reduced fragment: labels are combinations of swept rows")
         return self.uidx if self.uidx is not None else np.arange(len(self.labels), dtype=np.int64)
 
 
-def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = True) -> list[FragmentState]:
+def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = True,
+                      basis: bool = False) -> list[FragmentState]:
+    """Compile every fragment, dedup its instances and expand them into branch jobs.
+
+    ``basis=True`` (factored knit only) additionally sweeps a spanning set of instances
+    (``basis_reduce``); the knit transform folds the expansion back in."""
     circ = virt.circuit
     cl = clbit_indexer(circ)
     vg = virt.vgate_instructions
@@ -259,12 +277,15 @@ def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = 
             unique, uidx = dedup_labels(prog, labels)
         else:
             unique, uidx = list(labels), np.arange(len(labels), dtype=np.int64)
-        jobs = build_jobs(prog, unique)
+        red = basis_reduce(prog, unique) if (basis and dedup) else None
+        jobs = build_jobs(prog, red.labels if red is not None else unique)
         # run.py:49-58 drops a fragment whose get_counts() raises, i.e. when some instance of
         # it measures nothing at all (no data measurement and no config measurement).
         dropped = prog.m == 0 and _some_label_unmeasured(prog, labels)
         dp = DeviceProgram.upload(prog, device) if (upload and not dropped) else None
-        out.append(FragmentState(frag, labels, prog, dp, jobs, touches, dropped, uidx, unique))
+        out.append(FragmentState(frag, labels, prog, dp, jobs, touches, dropped, uidx, unique,
+                                 red.labels if red is not None else None,
+                                 red.expand if red is not None else None))
     return out
 
 
@@ -327,6 +348,8 @@ def knit_operands(virt, frags: list[FragmentState], factored: bool = False) -> K
     space = LabelSpace([g.num_instantiations for g in vg], [g.knit_coefficients() for g in vg])
     clbits = [[] if fs.dropped else list(fs.prog.clbits) for fs in frags]
     if not factored or not vg:
+        if any(fs.expand is not None for fs in frags):
+            raise ValueError("basis-reduced fragments need the factored knit")
         c = space.coefficients()
         rows, coefs = [], []
         for i, fs in enumerate(frags):
@@ -350,9 +373,11 @@ def knit_operands(virt, frags: list[FragmentState], factored: bool = False) -> K
             else:
                 W = np.kron(W, Ts[j][sides[j]])
         if fs.uidx is not None:  # fold labels sharing an instance: W' = W P
-            Wu = np.zeros((W.shape[0], fs.n_rows))
+            Wu = np.zeros((W.shape[0], len(fs.unique_labels)))
             np.add.at(Wu.T, fs.uidx, W.T)
             W = Wu
+        if fs.expand is not None:  # instances as combinations of the swept basis: W'' = W' E
+            W = W @ fs.expand
         transforms.append(W)
     return KnitOperands([None] * len(frags), [None] * len(frags), transforms, clbits, int(np.prod(ranks)))
 

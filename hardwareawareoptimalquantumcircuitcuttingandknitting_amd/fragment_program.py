@@ -326,6 +326,92 @@ def dedup_labels(prog: FragmentProgram, labels: list) -> tuple[list, np.ndarray]
     return unique, uidx
 
 
+def _superoperator(endpoint, inst_id: int) -> np.ndarray:
+    """Real 32-vector of the side program's signed channel ``rho -> sum_k s_k M_k rho M_k^+``
+    (the map a slot applies to the fragment state, config outcome folded as ``(-1)^m``)."""
+    phi = np.zeros((4, 4), dtype=np.complex128)
+    for mat, sign in side_branches(endpoint, inst_id):
+        phi += sign * np.kron(mat, mat.conj())
+    return np.concatenate([phi.real.ravel(), phi.imag.ravel()])
+
+
+@dataclass
+class BasisReduction:
+    """Instances of a fragment expressed in a smaller spanning set of instances.
+
+    Every fragment output is linear in each slot's signed channel, and a cut's side programs
+    are linearly dependent as channels (VirtualCX/CZ control side: ``rho + Z rho Z == S rho S^+
+    + S^+ rho S``, so the ``z`` program is ``s + sdg - id``). ``q[unique row] = expand @
+    q[basis row]`` exactly; the fragment then sweeps ``labels`` only.
+    """
+
+    labels: list  # one representative label per basis instance (slot programs in product order)
+    expand: np.ndarray  # [n_unique, n_basis] real
+
+
+def basis_reduce(prog: FragmentProgram, unique_labels: list, tol: float = 1e-12) -> BasisReduction | None:
+    """Per slot, keep a maximal linearly independent subset of its side programs (fewest
+    branch jobs first) and write every other program as a combination of it. Returns None
+    when that does not reduce the fragment's branch-job count."""
+    if not prog.slots or not unique_labels:
+        return None
+    per_slot = []  # (representative inst ids of the basis, coefficient map inst -> row of D)
+    for s in prog.slots:
+        if isinstance(s.endpoint, BranchMeasure):
+            per_slot.append(([0], {0: np.ones(1)}))
+            continue
+        insts = list(dict.fromkeys(int(lab[s.vgate_idx]) for lab in unique_labels))
+        sig = {i: _side_signature(s.endpoint, i) for i in insts}
+        reps = list({sig[i]: i for i in reversed(insts)}.values())[::-1]  # first inst per program
+        nbr = {i: len(side_branches(s.endpoint, i)) for i in reps}
+        phis = {i: _superoperator(s.endpoint, i) for i in reps}
+        basis: list[int] = []
+        for i in sorted(reps, key=lambda i: (nbr[i], reps.index(i))):
+            cand = np.stack([phis[b] for b in basis + [i]], axis=1)
+            if np.linalg.matrix_rank(cand, tol=tol) > len(basis):
+                basis.append(i)
+        basis.sort(key=reps.index)
+        Bm = np.stack([phis[b] for b in basis], axis=1)
+        coef = {}
+        for i in insts:
+            c, *_ = np.linalg.lstsq(Bm, phis[i], rcond=None)
+            c[np.abs(c) < tol] = 0.0
+            if np.abs(Bm @ c - phis[i]).max() > 1e-10:
+                raise AssertionError("side program outside the span of the chosen basis")
+            coef[i] = c
+        per_slot.append((basis, coef))
+    nb_cache: dict = {}
+    jobs_now = sum(_label_jobs(prog, lab, nb_cache) for lab in unique_labels)
+    n_basis = int(np.prod([len(b) for b, _ in per_slot]))
+    base = list(unique_labels[0])
+    labels = []
+    for combo in np.ndindex(*[len(b) for b, _ in per_slot]):  # last slot fastest
+        lab = list(base)
+        for s, (basis, _), k in zip(prog.slots, per_slot, combo):
+            if not isinstance(s.endpoint, BranchMeasure):
+                lab[s.vgate_idx] = basis[k]
+        labels.append(tuple(lab))
+    if sum(_label_jobs(prog, lab, nb_cache) for lab in labels) >= jobs_now:
+        return None
+    expand = np.zeros((len(unique_labels), n_basis))
+    for u, lab in enumerate(unique_labels):
+        row = np.ones(1)
+        for s, (_, coef) in zip(prog.slots, per_slot):
+            row = np.kron(row, coef[0 if isinstance(s.endpoint, BranchMeasure) else int(lab[s.vgate_idx])])
+        expand[u] = row
+    return BasisReduction(labels, expand)
+
+
+def _label_jobs(prog: FragmentProgram, label, cache: dict) -> int:
+    n = 1
+    for s in prog.slots:
+        inst = 0 if isinstance(s.endpoint, BranchMeasure) else int(label[s.vgate_idx])
+        if (id(s), inst) not in cache:
+            cache[(id(s), inst)] = len(side_branches(s.endpoint, inst))
+        n *= cache[(id(s), inst)]
+    return n
+
+
 @dataclass
 class JobTable:
     slot_mats: np.ndarray  # [n_jobs, n_slots, 2, 2] complex128

@@ -17,10 +17,13 @@ collective then assembles the reconstruction:
   labels needs, contracts a partial distribution over that slice, and a single
   ``reduce`` (sum) lands the full distribution on rank 0. Chosen when the output
   (``2^N`` fp64) is smaller than the instance tensors (hwe/bv/qft sizes).
-* ``gather`` mode — each rank sweeps its label shard, a single ``all_gather``
-  replicates the signed instance tensors ``q_f`` (1.36 GB for syc 32 5), and each
-  rank computes its own block of output rows (no 34 GB reduction; the result
-  stays row-sharded in ``(x_A, x_B)`` order).
+* ``gather`` mode — each rank sweeps its shard of every fragment's swept
+  instances and computes its own block of output rows (no 34 GB reduction; the
+  result stays row-sharded in ``(x_A, x_B)`` order). The row-side fragment needs
+  only its column block of every instance: one ``all_to_all`` (each rank sends
+  1/world of its shard to each peer); the column-side fragment is
+  ``all_gather``ed (134 MB for syc 32 5 with the basis-reduced sweep). The first
+  exchange overlaps the second fragment's sweep.
 """
 from __future__ import annotations
 
@@ -47,8 +50,8 @@ class HipBackend:
         self.dev = self.T.device("cuda", device)
         self.ctx = engine.get_context(device)
 
-    def prepare_fragments(self, virt):
-        return engine.prepare_fragments(virt, self.device)
+    def prepare_fragments(self, virt, basis: bool = False):
+        return engine.prepare_fragments(virt, self.device, basis=basis)
 
     def upload_jobs(self, jobs: JobTable):
         return engine.jobs_to_device(jobs, self.device)
@@ -95,7 +98,7 @@ class KnitPipeline:
         self.virt = virt
         self.rank, self.world, self.group = rank, world, group
         self.factored = factored
-        self.frags = self.be.prepare_fragments(virt)
+        self.frags = self.be.prepare_fragments(virt, basis=factored)
         self.ops = engine.knit_operands(virt, self.frags, factored)
         self.N = virt.circuit.num_clbits
         q_bytes = sum(len(fs.labels) << fs.prog.m for fs in self.frags) * 8
@@ -108,6 +111,7 @@ class KnitPipeline:
             raise ValueError(f"unknown mode {mode}")
         self.mode = mode
         self.events = []  # (start, end) events around the main contraction GEMM
+        self.sweep_events = []  # (start, end) events around each step's sweep (all fragments)
         self.record_events = False
         self._plan()
 
@@ -138,12 +142,39 @@ class KnitPipeline:
             n_jobs = sub.n_jobs
             width = 1 << fs.prog.m
             need = be.workspace_bytes(fs, n_jobs) if n_jobs else 0
+            # gather mode: a rank's rows live in a zero-padded [per, width] buffer (the unit of
+            # the collectives); the last rank's padding rows stay zero
+            rows = -(-nl // self.world) if self.mode == "gather" else max(hi - lo, 1)
+            alloc = be.zeros if self.mode == "gather" else be.empty
+            branching = n_jobs != hi - lo
             self.sweeps.append(dict(lo=lo, hi=hi, slot=slot_t, sign=sign_t, off=off_t, n_jobs=n_jobs,
-                                    pjob=be.empty((max(n_jobs, 1), width), T.float64),
-                                    q=(be.empty((max(hi - lo, 1), width), T.float64)
-                                       if n_jobs != hi - lo else None),
+                                    pjob=(be.empty((max(n_jobs, 1), width), T.float64) if branching
+                                          else alloc((max(rows, 1), width), T.float64)),
+                                    q=alloc((max(rows, 1), width), T.float64) if branching else None,
                                     ws=be.empty((max(need, 1),), T.uint8)))
         self._plan_knit()
+        if self.mode == "gather":
+            self._plan_exchange()
+
+    def _plan_exchange(self):
+        """Collectives of gather mode. With two fragments the A side (output rows) only needs
+        its column block of every instance row: one all_to_all of 1/world^2 of q_A per rank
+        pair instead of an all_gather; the B side (output columns) is all-gathered. Buffers are
+        allocated once."""
+        be, T, P = self.be, self.T, self.world
+        live = [i for i, fs in enumerate(self.frags) if not fs.dropped]
+        a_side = self.order[0]
+        width_a = 1 << len(self.ops.clbits[a_side])
+        self.split_a = (len(self.order) == 2 and len(live) == 2 and width_a % P == 0)
+        self.xbuf = {}
+        for i in live:
+            per = -(-self.frags[i].n_rows // P)
+            width = 1 << self.frags[i].prog.m
+            if self.split_a and i == a_side:
+                bw = width // P
+                self.xbuf[i] = ("a2a", be.empty((P, per, bw), T.float64), be.empty((P * per, bw), T.float64))
+            else:
+                self.xbuf[i] = ("gather", None, be.empty((P * per, width), T.float64))
 
     def _plan_knit(self):
         be, ops = self.be, self.ops
@@ -171,15 +202,18 @@ class KnitPipeline:
 
     # ------------------------------------------------------------------ step
     def sweep(self) -> list:
-        """Instance sweep of every fragment; returns the per-label ``q_f`` tensors this rank needs."""
+        """Instance sweep of every fragment; returns the ``q_f`` tensors this rank needs (in
+        gather mode: all rows, and only this rank's column block on a split A side)."""
         T, be = self.T, self.be
-        qs = []
-        for i, fs in enumerate(self.frags):
-            sw = self.sweeps[i]
+        qs = [None] * len(self.frags)
+        pending = []
+        # the A side (output rows) first, so its exchange overlaps the other sweeps
+        for i in sorted(range(len(self.frags)), key=lambda i: self.order.index(i)):
+            fs, sw = self.frags[i], self.sweeps[i]
             if sw is None:
                 ones = be.zeros((fs.n_rows, 1), T.float64)
                 ones += 1.0
-                qs.append(ones)
+                qs[i] = ones
                 continue
             if sw["n_jobs"]:
                 be.sweep(fs, sw["slot"], sw["sign"], sw["n_jobs"], sw["pjob"], sw["ws"])
@@ -187,22 +221,29 @@ class KnitPipeline:
                 q = be.reduce_labels(sw["pjob"], sw["off"], sw["hi"] - sw["lo"], sw["q"])
             else:
                 q = sw["pjob"]
-            q = q[: sw["hi"] - sw["lo"]]
             if self.mode == "gather":
-                q = self._all_gather_rows(q, fs.n_rows)
-            qs.append(q)
+                work, qs[i] = self._exchange(i, q)
+                pending.append(work)
+            else:
+                qs[i] = q[: sw["hi"] - sw["lo"]]
+        for work in pending:
+            work.wait()
         return qs
 
-    def _all_gather_rows(self, q, n_rows):
+    def _exchange(self, i, qpad):
+        """Start fragment i's collective on its zero-padded shard ``qpad`` [per, width]."""
         import torch.distributed as dist
 
-        T = self.T
-        per = -(-n_rows // self.world)
-        buf = self.be.zeros((per, q.shape[1]), q.dtype)
-        buf[: q.shape[0]].copy_(q)
-        full = self.be.empty((per * self.world, q.shape[1]), q.dtype)
-        dist.all_gather_into_tensor(full, buf, group=self.group)
-        return full[:n_rows]
+        kind, send, recv = self.xbuf[i]
+        n_rows = self.frags[i].n_rows
+        if kind == "a2a":  # chunk p = this rank's rows, column block p
+            P, per, bw = send.shape
+            send.copy_(qpad[:per].view(per, P, bw).transpose(0, 1))
+            work = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
+        else:
+            per = recv.shape[0] // self.world
+            work = dist.all_gather_into_tensor(recv, qpad[:per], group=self.group, async_op=True)
+        return work, recv[:n_rows]
 
     def operands(self, qs: list) -> list:
         T, be = self.T, self.be
@@ -254,22 +295,61 @@ class KnitPipeline:
             A = self.be.khatri_rao(A.contiguous(), mats[i].contiguous())
         B = mats[order[-1]]
         lo, hi = self.row_block
-        A = A[:, lo:hi].contiguous()
+        if not self.split_a:  # split A side: the exchange delivered only this block
+            A = A[:, lo:hi]
+        A = A.contiguous()
         return self.be.gemm_keyed(A, B.contiguous(), keyA=None, strideA=B.shape[1], keyB=None, strideB=1,
                                   out=self.out)
 
     def step(self):
-        return self.knit(self.sweep())
+        if not self.record_events:
+            return self.knit(self.sweep())
+        start, end = self.be.event(), self.be.event()
+        start.record()
+        qs = self.sweep()
+        end.record()
+        self.sweep_events.append((start, end))
+        return self.knit(qs)
 
     # ------------------------------------------------------------------ accounting
     def instance_counts(self) -> dict:
         """Reference instance count (``run.py:37-39``: sum of per-fragment label lists) and jobs."""
         return {
             "instances_ref": int(sum(len(fs.labels) for fs in self.frags)),
-            "instances_unique": int(sum(fs.n_rows for fs in self.frags)),
+            "instances_unique": int(sum(len(fs.unique_labels) for fs in self.frags)),
+            "instances_swept": int(sum(fs.n_rows for fs in self.frags)),
             "branch_jobs": int(sum(fs.jobs.n_jobs for fs in self.frags if not fs.dropped)),
             "labels": int(self.ops.num_terms),
         }
+
+    def sweep_traffic(self) -> dict:
+        """Modelled bytes of one step's sweep on this rank.
+
+        ``hbm``: what the kernels move: SPLIT programs write the |0..0> tile in the INIT
+        pass, read it back and write the whole state in the next pass, read + write the state
+        in every middle pass, read it and write ``2^m`` fp64 in the FINAL pass; the label
+        reduction reads the jobs' rows and writes the labels'. ``algorithmic``: SURVEY.md §8d,
+        one read + write of the complex128 state per (fused) gate per job."""
+        from . import sweep_plan
+
+        hbm = alg = 0
+        for fs, sw in zip(self.frags, self.sweeps):
+            if sw is None or not sw["n_jobs"]:
+                continue
+            enc = fs.dprog.enc if getattr(fs, "dprog", None) is not None else sweep_plan.encode(fs.prog)
+            J, n, m, P = sw["n_jobs"], enc.n, enc.m, len(enc.passes)
+            S, tile, out = 16 << n, 16 << sweep_plan.TILE_BITS, 8 << m
+            if enc.packed or P == 1:
+                per_job = out
+            elif P == 2:
+                per_job = 2 * tile + out
+            else:
+                per_job = 2 * tile + S + (P - 3) * 2 * S + S + out
+            hbm += J * per_job
+            if sw["q"] is not None:
+                hbm += J * out + (sw["hi"] - sw["lo"]) * out
+            alg += J * len(fs.prog.ops) * 32 * (1 << fs.prog.n)
+        return {"hbm": hbm, "algorithmic": alg}
 
     def gemm_shape(self) -> tuple[int, int, int]:
         """(M, N, K) of the main contraction on this rank."""

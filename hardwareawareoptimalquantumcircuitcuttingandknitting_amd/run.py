@@ -72,7 +72,8 @@ def run_virtual_circuit_dense(virt: VirtualCircuit, shots: int = 20000, *, devic
              len(virt.fragment_circuits),
              tuple(len(f) for f in virt.fragment_circuits), len(virt.vgate_instructions))
     now = perf_counter()
-    frags = engine.prepare_fragments(virt, device)
+    native = all(isinstance(virt.get_backend(f), MI355XBackend) for f in virt.fragment_circuits if len(f))
+    frags = engine.prepare_fragments(virt, device, basis=factored and native)
     qs = []
     for fs in frags:
         backend = virt.get_backend(fs.fragment)

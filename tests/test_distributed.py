@@ -1,8 +1,9 @@
-"""Multi-rank orchestration of KnitPipeline (world_size 2, gloo, CPU backend model).
+"""Multi-rank orchestration of KnitPipeline (world_size 2-4, gloo, CPU backend model).
 
 Checks both collective modes against the oracle's dense knit:
 * reduce: label-sliced sweep + partial contraction + one reduce to rank 0;
-* gather: label-sharded sweep + one all_gather of q_f + output-sharded contraction.
+* gather: sharded sweep + all_to_all (row side) / all_gather (column side) of q_f +
+  output-sharded contraction.
 """
 import os
 import socket
@@ -75,18 +76,21 @@ def _worker(rank, world, port, case, mode, factored, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,mode,factored", [
-    ("cx_3cuts", "reduce", False), ("cx_3cuts", "gather", False), ("cx_3cuts", "gather", True),
-    ("three", "reduce", False), ("three", "gather", True), ("move_gate", "gather", False),
+@pytest.mark.parametrize("case,mode,factored,world", [
+    ("cx_3cuts", "reduce", False, 2), ("cx_3cuts", "gather", False, 2), ("cx_3cuts", "gather", True, 2),
+    ("three", "reduce", False, 2), ("three", "gather", True, 2), ("move_gate", "gather", False, 2),
+    # 4 ranks: all_to_all split of the row side; 3 ranks: uneven shards, padded rows, no split
+    ("cx_3cuts", "gather", True, 4), ("move_gate", "gather", True, 3),
 ])
-def test_two_rank_pipeline_matches_oracle(case, mode, factored):
+def test_multi_rank_pipeline_matches_oracle(case, mode, factored, world):
     sys.path.insert(0, HERE)
     from oracle import dense
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, mode, factored, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, mode, factored, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     got_mode, res = q.get(timeout=240)

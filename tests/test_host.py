@@ -110,6 +110,44 @@ def test_knit_operands_match_oracle_dense_knit(case, factored):
                                          for g in virt.vgate_instructions])
 
 
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_basis_reduced_sweep_knits_to_oracle(case):
+    """Factored knit over a basis-reduced sweep (fragment_program.basis_reduce): the swept
+    basis instances, emulated from their encoded programs, knit to the oracle's dense result."""
+    _, cut = CASES[case]()
+    virt = VirtualCircuit(cut)
+    frags = engine.prepare_fragments(virt, upload=False, basis=True)
+    ops = engine.knit_operands(virt, frags, factored=True)
+    mats = []
+    for i, fs in enumerate(frags):
+        if fs.dropped:
+            mats.append(np.ones((ops.num_terms, 1)))
+            continue
+        q = _fragment_q_via_emulator(virt, fs)
+        assert q.shape[0] == fs.n_rows
+        mats.append(ops.transforms[i] @ q)
+    R = np.zeros(1 << virt.circuit.num_clbits)
+    keys = [ops.key_table(i) for i in range(len(mats))]
+    for t in range(ops.num_terms):
+        vec, key = mats[0][t], keys[0]
+        for m, k in zip(mats[1:], keys[1:]):
+            vec = np.outer(m[t], vec).reshape(-1)
+            key = (k[:, None] + key[None, :]).reshape(-1)
+        np.add.at(R, key, vec)
+    np.testing.assert_allclose(R, dense.run_dense(cut), atol=1e-13, rtol=0)
+
+
+def test_basis_reduction_counts_syc_32_5():
+    """VirtualCX sides span 4 channels with 5 programs (z = s + sdg - id on the control side):
+    syc 32 5 sweeps 4^4 basis instances (625 branch jobs) per fragment instead of 625 (1296)."""
+    _, cut, _ = cutting.config_cut_circuit("syc", 32, 5, 2)
+    virt = VirtualCircuit(cut)
+    for fs in engine.prepare_fragments(virt, upload=False, basis=True):
+        assert len(fs.unique_labels) == 625
+        assert fs.n_rows == 256 and fs.jobs.n_jobs == 625
+        assert fs.expand.shape == (625, 256)
+
+
 @pytest.mark.parametrize("case", ["cx_3cuts", "cp", "rzz", "move_gate", "three", "hwe_p3", "partial"])
 def test_foreign_cut_circuit_ingestion(case):
     """A qiskit-shaped cut circuit (tests/foreign.py) is adopted into the IR with the same
