@@ -696,6 +696,85 @@ __device__ __forceinline__ void gemm_tile_coords(int64_t seq, int64_t tiles_m, i
 #endif
 }
 
+// Epilogue of one 128x128 tile: f64 16x16 C layout: col = lane & 15, row = (lane >> 4) + 4 * r.
+// Output offsets are key(row) + key(col) (keys >= 0; -1 marks a row/column outside the matrix).
+// FULL: the tile lies inside M x N and beta == 0 (the glds kernel's contract): no bounds checks,
+// so the paired path issues exactly 32 stores per wave (its vmcnt accounting relies on that).
+template <bool FULL>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, int64_t m0, int64_t n0, d4_t (&acc)[4][4]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int64_t M = g.M, N = g.N;
+    int64_t kcol[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
+        kcol[j] = (FULL || col < N) ? (g.keyB ? g.keyB[col] : col * g.strideB) : -1;
+    }
+#if QK_GEMM_STORE
+    // Paired 16-B stores: when every even column's right neighbour is the next output element
+    // (key(c+1) = key(c) + 1, e.g. the fragment holding clbit 0 on the N side), lane pairs swap
+    // one value (DPP quad_perm [1,0,3,2]) so each lane writes two adjacent outputs of one row.
+    bool pairable = FULL || (!g.beta && n0 + GT <= N);
+    if (pairable) {
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t nb = dpp_swap_pair(kcol[j]);
+            ok = ok && ((lane & 1) ? nb + 1 == kcol[j] : kcol[j] + 1 == nb);
+        }
+        pairable = __all(ok);  // wave-uniform
+    }
+    if (pairable) {
+        const bool odd = lane & 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int rp = 0; rp < 4; rp += 2) {
+                // even lane writes row rp, odd lane row rp+1, both at the even column's key
+                const int rr = rp + (odd ? 1 : 0);
+                const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) + 4 * rr;
+                const int64_t krow = (FULL || row < M) ? (g.keyA ? g.keyA[row] : row * g.strideA) : -1;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const double x = odd ? acc[i][j][rp] : acc[i][j][rp + 1];
+                    const double y = dpp_swap_pair(x);
+                    d2_t v;
+                    v.x = odd ? y : acc[i][j][rp];
+                    v.y = odd ? acc[i][j][rp + 1] : y;
+#ifdef QK_GEMM_NOSTORE
+                    if (v.x != 1234.5678) continue;
+#endif
+                    if (FULL || krow >= 0) gemm_store_pair(g.out + krow + kcol[j] - (odd ? 1 : 0), v);
+                }
+            }
+        }
+        return;
+    }
+#endif
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        int64_t krow[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
+            krow[r] = row < M ? (g.keyA ? g.keyA[row] : row * g.strideA) : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#ifdef QK_GEMM_NOSTORE  // tuning experiment only: MFMA + operand traffic without the output
+                if (acc[i][j][r] != 1234.5678) continue;
+#endif
+                if (krow[r] < 0 || kcol[j] < 0) continue;
+                double* o = g.out + krow[r] + kcol[j];
+                if (g.beta) *o += acc[i][j][r];
+                else gemm_store_out(o, acc[i][j][r]);
+            }
+    }
+}
+
 // One 128x128 output tile by one 256-thread workgroup (2x2 waves of 64x64 = 4x4 MFMA 16x16x4
 // f64 tiles each). K is streamed in 16-row chunks: the next chunk's global loads are issued into
 // registers before the current chunk's MFMAs (software pipeline), LDS is double buffered so a
@@ -732,15 +811,24 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int64_t bm, int64_t
     const int lr = tid >> 6;        // first chunk row of this thread (rows lr + 4j)
     const int lc = 2 * (tid & 63);  // two columns per thread
     for (int64_t k0 = 0; k0 < K; k0 += GK) {
+#ifdef QK_GEMM_NOLDSW  // tuning experiment only: LDS written and synchronised once per tile
+        if (k0 == 0)
+#endif
+        {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             *reinterpret_cast<d2_t*>(&As[buf][lr + 4 * j][lc]) = ra[j];
             *reinterpret_cast<d2_t*>(&Bs[buf][lr + 4 * j][lc]) = rb[j];
         }
         __syncthreads();
+        }
         // prefetch the next chunk (this tile's, else chunk 0 of the next tile) during the MFMAs
         const bool more = k0 + GK < K;
+#ifdef QK_GEMM_NOLOAD  // tuning experiment only: no operand loads after a tile's first chunk
+        if (!more && have_next) {
+#else
         if (more || have_next) {
+#endif
             const int64_t pk = more ? k0 + GK : 0;
             const int64_t pm = more ? m0 : nbm * GT, pn = more ? n0 : nbn * GT;
             const bool kfull = pk + GK <= K;
@@ -764,76 +852,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int64_t bm, int64_t
         }
         buf ^= 1;
     }
-    // epilogue: f64 16x16 C layout: col = lane & 15, row = (lane >> 4) + 4 * r. Output offsets
-    // are key(row) + key(col) (keys >= 0; -1 marks a row/column outside the matrix).
-    int64_t kcol[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
-        kcol[j] = col < N ? (g.keyB ? g.keyB[col] : col * g.strideB) : -1;
-    }
-#if QK_GEMM_STORE
-    // Paired 16-B stores: when every even column's right neighbour is the next output element
-    // (key(c+1) = key(c) + 1, e.g. the fragment holding clbit 0 on the N side), lane pairs swap
-    // one value (DPP quad_perm [1,0,3,2]) so each lane writes two adjacent outputs of one row.
-    bool pairable = !g.beta && n0 + GT <= N;
-    if (pairable) {
-        bool ok = true;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int64_t nb = dpp_swap_pair(kcol[j]);
-            ok = ok && ((lane & 1) ? nb + 1 == kcol[j] : kcol[j] + 1 == nb);
-        }
-        pairable = __all(ok);  // wave-uniform
-    }
-    if (pairable) {
-        const bool odd = lane & 1;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int rp = 0; rp < 4; rp += 2) {
-                // even lane writes row rp, odd lane row rp+1, both at the even column's key
-                const int rr = rp + (odd ? 1 : 0);
-                const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) + 4 * rr;
-                const int64_t krow = row < M ? (g.keyA ? g.keyA[row] : row * g.strideA) : -1;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const double x = odd ? acc[i][j][rp] : acc[i][j][rp + 1];
-                    const double y = dpp_swap_pair(x);
-                    d2_t v;
-                    v.x = odd ? y : acc[i][j][rp];
-                    v.y = odd ? acc[i][j][rp + 1] : y;
-#ifdef QK_GEMM_NOSTORE
-                    if (v.x != 1234.5678) continue;
-#endif
-                    if (krow >= 0) gemm_store_pair(g.out + krow + kcol[j] - (odd ? 1 : 0), v);
-                }
-            }
-        }
-        return;
-    }
-#endif
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        int64_t krow[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t row = m0 + wm * 64 + i * 16 + (lane >> 4) + 4 * r;
-            krow[r] = row < M ? (g.keyA ? g.keyA[row] : row * g.strideA) : -1;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-#ifdef QK_GEMM_NOSTORE  // tuning experiment only: MFMA + operand traffic without the output
-                if (acc[i][j][r] != 1234.5678) continue;
-#endif
-                if (krow[r] < 0 || kcol[j] < 0) continue;
-                double* o = g.out + krow[r] + kcol[j];
-                if (g.beta) *o += acc[i][j][r];
-                else gemm_store_out(o, acc[i][j][r]);
-            }
-    }
+    gemm_epilogue<false>(g, m0, n0, acc);
 }
 
 // XCD-aware schedule: the dispatcher deals consecutive workgroup ids round-robin over the 8
@@ -874,6 +893,165 @@ __global__ __launch_bounds__(256, 2) void qk_gemm_keyed_kernel(GemmArgs g) {
     gemm_load_first(g, bm, bn, ra, rb);
     gemm_tile(g, bm, bn, false, 0, 0, ra, rb, As, Bs, buf);
 #endif
+}
+
+// ------------------------------------------------------------------------------------------
+// knit contraction, LDS-DMA pipeline (full tiles: M, N multiples of 128, K of 8, beta = 0)
+// ------------------------------------------------------------------------------------------
+// Every operand row goes global -> LDS directly (global_load_lds_dwordx4: one 1-KiB
+// wave-instruction per 128-double row, SGPR row address + the lane's 16-B offset, no staging
+// VGPRs, no ds_write), into a ring of G2S stages of G2K k-rows. One raw barrier per stage, the
+// waits are counted (vmcnt(N), see gemm_ring_wait), and the MFMA fragments are double-buffered in
+// registers so only a stage's first LDS read is exposed. Measured on syc 32 5's 65536^2 x 256
+// contraction (tools/gemm_bench.py, random operands): the stage depth is the lever (G2K 4 / 8 / 16
+// = 48 / 58-61 / 65 TF/s; more stages in flight at G2K = 8 change nothing), and G2K = 16 with two
+// stages is what fits 2 workgroups per CU (73.7 KiB LDS each); the register-staged kernel above
+// reaches 60.4 TF/s on the same shape.
+#ifndef QK_GEMM_GLDS
+#define QK_GEMM_GLDS 1  // full-tile contractions take the LDS-DMA pipeline
+#endif
+#ifndef QK_G2K
+#define QK_G2K 16
+#endif
+#ifndef QK_G2S
+#define QK_G2S 2
+#endif
+#ifndef QK_GEMM_PRIO
+#define QK_GEMM_PRIO 0  // raise wave priority around each k-step's MFMAs
+#endif
+constexpr int G2K = QK_G2K;  // k-rows per stage (multiple of 4)
+constexpr int G2S = QK_G2S;  // stages in the ring (2 x 36.9 KiB per workgroup, 2 workgroups per CU)
+constexpr int G2L = G2K / 2;  // glds per wave per stage (G2K/4 rows of A and of B)
+
+struct GemmRing {
+    double a[G2K][GT + GPAD];
+    double b[G2K][GT + GPAD];
+};
+
+__device__ __forceinline__ void glds16(const double* src, double* lds_row) {
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                     reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                         reinterpret_cast<uintptr_t>(lds_row)),
+                                     16, 0, 0);
+}
+
+// Wait until at most n of this wave's vector-memory operations are outstanding (n > 63 waits
+// for 63: waiting for more is always safe).
+__device__ __forceinline__ void gemm_ring_wait(int n) {
+#define QK_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+#define QK_VMW8(k) QK_VMW(k) QK_VMW(k + 1) QK_VMW(k + 2) QK_VMW(k + 3) QK_VMW(k + 4) QK_VMW(k + 5) QK_VMW(k + 6) QK_VMW(k + 7)
+    switch (n < 63 ? n : 63) {
+        QK_VMW8(0) QK_VMW8(8) QK_VMW8(16) QK_VMW8(24) QK_VMW8(32) QK_VMW8(40) QK_VMW8(48)
+        QK_VMW(56) QK_VMW(57) QK_VMW(58) QK_VMW(59) QK_VMW(60) QK_VMW(61) QK_VMW(62) QK_VMW(63)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#undef QK_VMW8
+#undef QK_VMW
+}
+
+__global__ __launch_bounds__(256, 2) void qk_gemm_glds_kernel(GemmArgs g) {
+    __shared__ __attribute__((aligned(16))) GemmRing ring[G2S];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int64_t nblk = g.tiles_m * g.tiles_n;
+    const int64_t G = gridDim.x;
+    const bool xcd = nblk % 8 == 0 && G % 8 == 0;
+    const int64_t per_xcd = xcd ? nblk / 8 : nblk, stride = xcd ? G / 8 : G;
+    const int64_t base = xcd ? (blockIdx.x % 8) * per_xcd : 0;
+    const int64_t li0 = xcd ? blockIdx.x / 8 : blockIdx.x;
+    if (li0 >= per_xcd) return;
+    const int nct = (int)(g.K / G2K);                                  // stages per tile
+    const int ntile = (int)((per_xcd - li0 + stride - 1) / stride);  // tiles of this workgroup
+    const int total = ntile * nct;
+
+    // issue side: the (tile, stage) the next glds batch belongs to
+    int it = 0, ic = 0, issued = 0;
+    int64_t ibm, ibn;
+    gemm_tile_coords(base + li0, g.tiles_m, g.tiles_n, ibm, ibn);
+    // this wave's two rows of the A and of the B stage, 16 B per lane
+    // row addresses are wave-uniform (SGPR base + the lane's 16-B offset): no per-lane 64-bit
+    // address arithmetic per load
+    const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+    auto issue = [&]() {
+        if (issued >= total) return;
+        GemmRing& r = ring[issued % G2S];
+        const int64_t k0 = (int64_t)ic * G2K;
+#pragma unroll
+        for (int q = 0; q < G2K / 4; ++q) {
+            const int row = wave_s * (G2K / 4) + q;
+            const double* pa = g.A + (k0 + row) * g.lda + ibm * GT;
+            const double* pb = g.B + (k0 + row) * g.ldb + ibn * GT;
+            glds16(pa + 2 * lane, &r.a[row][0]);
+            glds16(pb + 2 * lane, &r.b[row][0]);
+        }
+        ++issued;
+        if (++ic == nct) {
+            ic = 0;
+            ++it;
+            if (it < ntile) gemm_tile_coords(base + li0 + (int64_t)it * stride, g.tiles_m, g.tiles_n, ibm, ibn);
+        }
+    };
+    for (int s = 0; s < G2S - 1; ++s) issue();
+
+    d4_t acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (d4_t){0.0, 0.0, 0.0, 0.0};
+    int64_t bm, bn;
+    gemm_tile_coords(base + li0, g.tiles_m, g.tiles_n, bm, bn);
+    int t = 0, c = 0;
+    for (int gc = 0; gc < total; ++gc) {
+        // VMEM operations this wave issued after stage gc's batch: the later batches in flight
+        // (G2L each) and the 32 stores of every tile epilogue issued after it (tiles ending at
+        // gc-3..gc-1, all of which followed batch gc)
+        int after = G2L * ((total - 1 - gc) < (G2S - 2) ? (total - 1 - gc) : (G2S - 2));
+#pragma unroll
+        for (int d = 1; d < G2S; ++d)
+            if (gc - d >= 0 && (gc - d + 1) % nct == 0) after += 32;
+        gemm_ring_wait(after);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // stage gc landed for all waves; stage gc-1 fully read
+        const GemmRing& r = ring[gc % G2S];
+        // fragments double-buffered in registers: k-step kk+1's LDS reads are in flight during
+        // k-step kk's MFMAs
+        double fa[2][4], fb[2][4];
+        auto frags = [&](int kk) {
+            const int kr = kk * 4 + (lane >> 4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                fa[kk & 1][q] = r.a[kr][wm * 64 + q * 16 + (lane & 15)];
+                fb[kk & 1][q] = r.b[kr][wn * 64 + q * 16 + (lane & 15)];
+            }
+        };
+        frags(0);  // first fragments in flight while the refill of stage gc-1 is issued
+        issue();
+#pragma unroll
+        for (int kk = 0; kk < G2K / 4; ++kk) {
+            if (kk + 1 < G2K / 4) frags(kk + 1);
+#if QK_GEMM_PRIO
+            __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[kk & 1][i], fb[kk & 1][j], acc[i][j], 0,
+                                                                     0, 0);
+#if QK_GEMM_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
+        }
+        if (++c == nct) {
+            gemm_epilogue<true>(g, bm * GT, bn * GT, acc);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = (d4_t){0.0, 0.0, 0.0, 0.0};
+            c = 0;
+            if (++t < ntile) gemm_tile_coords(base + li0 + (int64_t)t * stride, g.tiles_m, g.tiles_n, bm, bn);
+        }
+    }
 }
 
 __global__ void qk_khatri_rao_kernel(int64_t K, int64_t M, int64_t N, const double* __restrict__ A,
@@ -1050,6 +1228,18 @@ int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A,
     QK_HIP(ctx, hipSetDevice(ctx->device));
     if (nblk >= (int64_t(1) << 31)) return fail(ctx, QK_EARG, "qk_gemm_keyed: too many tiles%s");
     GemmArgs g{M, N, K, A, lda, B, ldb, keyA, strideA, keyB, strideB, out, beta, tm, tn};
+    const bool aligned16 = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) == 0 &&
+                           (lda % 2) == 0 && (ldb % 2) == 0;
+    if (QK_GEMM_GLDS && !beta && M % GT == 0 && N % GT == 0 && K % G2K == 0 && K > 0 && aligned16) {
+        int cus = 0;
+        QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        int64_t G = (int64_t)cus * 2;
+        G = G < 8 ? 8 : G - G % 8;
+        if (G > nblk) G = nblk;
+        hipLaunchKernelGGL(qk_gemm_glds_kernel, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
+        QK_HIP(ctx, hipGetLastError());
+        return QK_OK;
+    }
 #if QK_GEMM_PERSIST
     int cus = 0;
     QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));

@@ -47,6 +47,32 @@ def test_gemm_keyed_matches_numpy(T):
         np.testing.assert_allclose(out2.cpu().numpy().reshape(N, M), ref.T + 1, atol=1e-12 * max(1, K), rtol=0)
 
 
+@pytest.mark.parametrize("K,M,N,keyed", [
+    (16, 128, 128, False), (16, 4096, 4096, False), (32, 4096, 4096, True), (272, 4096, 2048, False),
+    (48, 8192, 1024, True), (256, 1024, 8192, False), (8, 4096, 4096, True),  # K % 16: register kernel
+])
+def test_gemm_keyed_full_tile_pipeline_matches_torch(T, K, M, N, keyed):
+    """Full-tile shapes take the LDS-DMA ring kernel (qk_gemm_glds_kernel): one or several tiles
+    per workgroup, stage rings that wrap across tile ends (K = 16: an epilogue every stage), the
+    paired-store and (transposing keys) the per-element epilogue, against torch's fp64 GEMM."""
+    ctx = engine.get_context(0)
+    g = T.Generator(device="cuda").manual_seed(K + M + N)
+    A = T.randn(K, M, dtype=T.float64, device="cuda", generator=g)
+    B = T.randn(K, N, dtype=T.float64, device="cuda", generator=g)
+    ref = A.T @ B
+    out = T.full((M * N,), float("nan"), dtype=T.float64, device="cuda")
+    if keyed:  # out[j * M + i]: column keys step by M, so no paired stores
+        engine.gemm_keyed(ctx, A, B, keyA=T.arange(M, dtype=T.int64, device="cuda"),
+                          keyB=T.arange(N, dtype=T.int64, device="cuda") * M, out=out)
+        got = out.view(N, M).T
+    else:
+        engine.gemm_keyed(ctx, A, B, out=out, strideA=N)
+        got = out.view(M, N)
+    T.cuda.synchronize()
+    err = float((got - ref).abs().max())
+    assert err <= 1e-12 * K, err
+
+
 def test_khatri_rao_and_gather(T):
     ctx = engine.get_context(0)
     rng = np.random.default_rng(1)
