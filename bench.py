@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense FP64 matrix, spec (MI355X_MICROARCH.md has no measured f64 row)
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X dense FP64 vector (v_fma_f64), spec
 HBM_PEAK_GBS = 8000.0
 
 
@@ -196,7 +197,7 @@ def main():
             "parallelism": f"labels x{world} ({pipe.mode})",
         },
         "roofline": {
-            "kernel": "qk_gemm_keyed_kernel (knit contraction)",
+            "kernel": "qk_gemm_glds_kernel (knit contraction, LDS-DMA ring)",
             "bound": "mfma",
             "achieved": achieved,
             "peak": FP64_MFMA_PEAK_TFLOPS,
@@ -208,7 +209,7 @@ def main():
         },
         "sweep": {
             "kernel": "qk_sweep_pass_kernel + qk_reduce_labels (all fragments, per step, rank 0)",
-            "bound": "fp64 valu (fused passes move far fewer bytes than the per-gate model)",
+            "bound": "latency (issue-bound: 9% of fp64 VALU, 21% of HBM; fused passes move far fewer bytes than the per-gate model)",
             "ms_per_step": sweep_ms,
             "branch_jobs": counts["branch_jobs"],
             "hbm_bytes": traffic["hbm"],
@@ -216,6 +217,9 @@ def main():
             "hbm_frac": traffic["hbm"] / (sweep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "algorithmic_bytes": traffic["algorithmic"],
             "algorithmic_GBs": traffic["algorithmic"] / (sweep_ms * 1e-3) / 1e9,
+            "fp64_flops": traffic["flops"],
+            "fp64_TFs": traffic["flops"] / (sweep_ms * 1e-3) / 1e12,
+            "fp64_valu_frac": traffic["flops"] / (sweep_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
         },
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -41,6 +41,30 @@ def _shard(n: int, rank: int, world: int) -> tuple[int, int]:
     return lo, min(n, lo + per)
 
 
+# fp64 flops per amplitude the sweep kernel spends on one op of each kind (qk_op.kind order,
+# csrc/qknit.hip ap_* helpers: a complex multiply-add is 1 mul + 3 fma per component)
+_OP_FLOPS = (14, 6, 14, 30, 6, 0, 0, 6, 6, 6, 2, 2, 2)
+
+
+def _sweep_flops_per_job(enc) -> int:
+    """fp64 flops one job of an encoded program costs: every op of a pass over the amplitudes
+    the pass touches (the sparse INIT pass of a multi-pass SPLIT program only the |0..0> tile),
+    plus |z|^2 (4 flops) per amplitude in the FINAL pass."""
+    from . import sweep_plan
+
+    n_amp = 1 << (enc.n_eff if enc.packed else enc.n)
+    total = 0
+    P = len(enc.passes)
+    for ip in range(P):
+        ps = enc.passes[ip]
+        amps = (1 << sweep_plan.TILE_BITS) if (not enc.packed and ip == 0 and P > 1) else n_amp
+        for gi in range(int(ps["group_begin"]), int(ps["group_end"])):
+            gr = enc.groups[gi]
+            for oi in range(int(gr["op_begin"]), int(gr["op_end"])):
+                total += _OP_FLOPS[int(enc.ops[oi]["kind"])] * amps
+    return total + 4 * n_amp
+
+
 class HipBackend:
     """Device work of the pipeline on one GPU through the C ABI."""
 
@@ -329,10 +353,11 @@ class KnitPipeline:
         pass, read it back and write the whole state in the next pass, read + write the state
         in every middle pass, read it and write ``2^m`` fp64 in the FINAL pass; the label
         reduction reads the jobs' rows and writes the labels'. ``algorithmic``: SURVEY.md §8d,
-        one read + write of the complex128 state per (fused) gate per job."""
+        one read + write of the complex128 state per (fused) gate per job. ``flops``: fp64
+        arithmetic the kernel executes (``_sweep_flops_per_job``)."""
         from . import sweep_plan
 
-        hbm = alg = 0
+        hbm = alg = flops = 0
         for fs, sw in zip(self.frags, self.sweeps):
             if sw is None or not sw["n_jobs"]:
                 continue
@@ -349,7 +374,8 @@ class KnitPipeline:
             if sw["q"] is not None:
                 hbm += J * out + (sw["hi"] - sw["lo"]) * out
             alg += J * len(fs.prog.ops) * 32 * (1 << fs.prog.n)
-        return {"hbm": hbm, "algorithmic": alg}
+            flops += J * _sweep_flops_per_job(enc)
+        return {"hbm": hbm, "algorithmic": alg, "flops": flops}
 
     def gemm_shape(self) -> tuple[int, int, int]:
         """(M, N, K) of the main contraction on this rank."""
