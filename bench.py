@@ -208,8 +208,10 @@ def main():
             "avg_launch_ms": gemm_ms,
         },
         "sweep": {
-            "kernel": "qk_sweep_pass_kernel + qk_reduce_labels (all fragments, per step, rank 0)",
-            "bound": "latency (issue-bound: 9% of fp64 VALU, 21% of HBM; fused passes move far fewer bytes than the per-gate model)",
+            "kernel": "per-program sweep kernels (sweep_codegen + hiprtc) + qk_reduce_labels "
+                      "(all fragments, per step, this rank)",
+            "bound": "hbm (modelled bytes below; fused passes move far fewer than the per-gate "
+                     "algorithmic model)",
             "ms_per_step": sweep_ms,
             "branch_jobs": counts["branch_jobs"],
             "hbm_bytes": traffic["hbm"],

@@ -38,6 +38,11 @@ SIGNATURES = {
     "qk_last_error": (ctypes.c_char_p, [c_vp]),
     "qk_sweep_workspace_bytes": (c_i32, [ctypes.POINTER(QkProgram), c_i64, ctypes.POINTER(c_i64)]),
     "qk_sweep": (c_i32, [c_vp, ctypes.POINTER(QkProgram), c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "qk_module_compile": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                  ctypes.POINTER(c_vp)]),
+    "qk_module_destroy": (c_i32, [c_vp]),
+    "qk_sweep_compiled": (c_i32, [c_vp, c_vp, ctypes.POINTER(QkProgram), c_i64, c_vp, c_vp, c_vp, c_i64,
+                                  c_vp]),
     "qk_reduce_labels": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "qk_gemm_keyed": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                               c_vp, c_i64, c_vp, ctypes.c_int]),

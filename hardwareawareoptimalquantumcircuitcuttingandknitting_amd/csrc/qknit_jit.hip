@@ -1,0 +1,120 @@
+// qknit_jit.hip — per-program sweep kernels compiled at run time (hiprtc, gfx950).
+//
+// The interpreter kernel (qk_sweep_pass_kernel) reads every op descriptor and matrix at run
+// time and dispatches on it; on syc 32 5 it spends most of its issue slots on that and on
+// index arithmetic (PMC: 12% of VALU instructions are f64 FMAs, 49% of wave time waiting).
+// sweep_codegen.py instead emits one kernel per pass with the tile layout, fiber positions,
+// op sequence and gate matrices as constants (the same ops, from sweep_ops.h); this file
+// compiles such source with hiprtc, loads the code object, and launches its passes with
+// qk_sweep's grid and argument contract.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+struct qk_module {
+    hipModule_t mod = nullptr;
+    std::vector<hipFunction_t> fns;
+};
+
+namespace {
+
+int jfail(qk_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qk_module_compile(qk_ctx* ctx, const char* source, const char* const* names, int n_names,
+                      qk_module** out) {
+    if (!ctx || !source || !names || n_names < 1 || !out) return QK_EARG;
+    *out = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return jfail(ctx, QK_EHIP, "qk_module_compile: hipSetDevice");
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, source, "qk_sweep_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+        return jfail(ctx, QK_EHIP, "qk_module_compile: hiprtcCreateProgram failed");
+    for (int i = 0; i < n_names; ++i) hiprtcAddNameExpression(prog, names[i]);
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    if (rc != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n, '\0');
+        if (n) hiprtcGetProgramLog(prog, &log[0]);
+        hiprtcDestroyProgram(&prog);
+        return jfail(ctx, QK_EARG, "qk_module_compile: " + std::string(hiprtcGetErrorString(rc)) + "\n" + log);
+    }
+    size_t code_size = 0;
+    hiprtcGetCodeSize(prog, &code_size);
+    std::vector<char> code(code_size);
+    hiprtcGetCode(prog, code.data());
+    hiprtcDestroyProgram(&prog);
+    qk_module* m = new qk_module();
+    if (hipModuleLoadData(&m->mod, code.data()) != hipSuccess) {
+        delete m;
+        return jfail(ctx, QK_EHIP, "qk_module_compile: hipModuleLoadData failed");
+    }
+    for (int i = 0; i < n_names; ++i) {
+        hipFunction_t f;
+        if (hipModuleGetFunction(&f, m->mod, names[i]) != hipSuccess) {
+            hipModuleUnload(m->mod);
+            delete m;
+            return jfail(ctx, QK_EARG, std::string("qk_module_compile: no kernel ") + names[i]);
+        }
+        m->fns.push_back(f);
+    }
+    *out = m;
+    return QK_OK;
+}
+
+int qk_module_destroy(qk_module* m) {
+    if (!m) return QK_EARG;
+    if (m->mod) (void)hipModuleUnload(m->mod);
+    delete m;
+    return QK_OK;
+}
+
+int qk_sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* p, int64_t n_jobs,
+                      const double* job_slots, const double* job_sign, void* workspace,
+                      int64_t workspace_bytes, double* pjob) {
+    if (!ctx) return QK_EARG;
+    if (!module || !p || !p->passes || p->n_passes < 1) return jfail(ctx, QK_EARG, "qk_sweep_compiled: empty program");
+    if ((int)module->fns.size() != p->n_passes)
+        return jfail(ctx, QK_EARG, "qk_sweep_compiled: module does not hold one kernel per pass");
+    if (n_jobs <= 0) return QK_OK;
+    if (p->packed || p->n <= QK_TILE_BITS || p->n > 40)
+        return jfail(ctx, QK_EARG, "qk_sweep_compiled: SPLIT programs only");
+    if (!job_sign || !pjob || (p->n_slots > 0 && !job_slots))
+        return jfail(ctx, QK_EARG, "qk_sweep_compiled: null buffer");
+    const int64_t need = n_jobs * ((int64_t)1 << p->n) * (int64_t)(2 * sizeof(double));
+    if (!workspace || workspace_bytes < need) return jfail(ctx, QK_EARG, "qk_sweep_compiled: workspace too small");
+    if (hipSetDevice(ctx->device) != hipSuccess) return jfail(ctx, QK_EHIP, "qk_sweep_compiled: hipSetDevice");
+    for (int ip = 0; ip < p->n_passes; ++ip) {
+        const bool sparse_init = ip == 0 && p->n_passes > 1;  // qk_sweep: INIT tile of each job only
+        const int64_t blocks = sparse_init ? n_jobs : (n_jobs << (p->n - QK_TILE_BITS));
+        if (blocks > 0x7fffffff) return jfail(ctx, QK_EARG, "qk_sweep_compiled: too many tiles");
+        struct {
+            const double* slots;
+            const double* sign;
+            void* state;
+            double* pjob;
+            int64_t n_jobs;
+        } args{job_slots, job_sign, workspace, pjob, n_jobs};
+        size_t size = sizeof(args);
+        void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+                       HIP_LAUNCH_PARAM_END};
+        const hipError_t e = hipModuleLaunchKernel(module->fns[ip], (unsigned)blocks, 1, 1, 256, 1, 1, 0,
+                                                   ctx->stream, nullptr, cfg);
+        if (e != hipSuccess) return jfail(ctx, QK_EHIP, std::string("qk_sweep_compiled: ") + hipGetErrorString(e));
+    }
+    return QK_OK;
+}
+
+}  // extern "C"

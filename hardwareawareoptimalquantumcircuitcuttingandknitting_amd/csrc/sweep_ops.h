@@ -1,0 +1,157 @@
+// sweep_ops.h — per-fiber amplitude updates of the batched sweep (shared by the interpreter
+// kernel in qknit.hip and the per-program kernels sweep_codegen.py generates for hiprtc).
+// A thread holds a fiber of PER = 16 amplitudes (4 tile positions) in registers; fiber bit A of
+// the register index r is the op's qubit.
+#ifndef QKNIT_SWEEP_OPS_H
+#define QKNIT_SWEEP_OPS_H
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+#endif
+
+namespace qk_sweep_ops {
+
+constexpr int PER = 16;
+
+__device__ __forceinline__ double2 cmul(double ar, double ai, double2 b) {
+    return make_double2(fma(ar, b.x, -ai * b.y), fma(ar, b.y, ai * b.x));
+}
+// m0 * a + m1 * b with m given as (re, im) pairs
+__device__ __forceinline__ double2 cmac2(const double* m, double2 a, double2 b) {
+    double re = m[0] * a.x;
+    re = fma(-m[1], a.y, re);
+    re = fma(m[2], b.x, re);
+    re = fma(-m[3], b.y, re);
+    double im = m[0] * a.y;
+    im = fma(m[1], a.x, im);
+    im = fma(m[2], b.y, im);
+    im = fma(m[3], b.x, im);
+    return make_double2(re, im);
+}
+
+// LDS swizzle: XOR the low nibble with the two higher nibbles (bank spread for strided fibers)
+__device__ __forceinline__ int swz(int t) { return t ^ (((t >> 4) ^ (t >> 8)) & 15); }
+
+template <int A>
+__device__ __forceinline__ void ap_u1(double2 (&v)[PER], const double* m) {
+    double mm[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mm[i] = m[i];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if (r & (1 << A)) continue;
+        const double2 a = v[r], b = v[r | (1 << A)];
+        v[r] = cmac2(mm, a, b);
+        v[r | (1 << A)] = cmac2(mm + 4, a, b);
+    }
+}
+
+template <int A>
+__device__ __forceinline__ void ap_d1(double2 (&v)[PER], const double* d) {
+    const double d0r = d[0], d0i = d[1], d1r = d[2], d1i = d[3];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) v[r] = (r & (1 << A)) ? cmul(d1r, d1i, v[r]) : cmul(d0r, d0i, v[r]);
+}
+
+template <int A, int B>
+__device__ __forceinline__ void ap_u2(double2 (&v)[PER], const double* m) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if (r & ((1 << A) | (1 << B))) continue;
+        const int i0 = r, i1 = r | (1 << A), i2 = r | (1 << B), i3 = r | (1 << A) | (1 << B);
+        const double2 x0 = v[i0], x1 = v[i1], x2 = v[i2], x3 = v[i3];
+        double2 y[4];
+#pragma unroll
+        for (int row = 0; row < 4; ++row) {
+            const double* mr = m + row * 8;
+            double2 s = cmac2(mr, x0, x1);
+            const double2 t = cmac2(mr + 4, x2, x3);
+            y[row] = make_double2(s.x + t.x, s.y + t.y);
+        }
+        v[i0] = y[0];
+        v[i1] = y[1];
+        v[i2] = y[2];
+        v[i3] = y[3];
+    }
+}
+
+template <int A, int B>
+__device__ __forceinline__ void ap_d2(double2 (&v)[PER], const double* d) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const int k = ((r >> A) & 1) | (((r >> B) & 1) << 1);
+        v[r] = cmul(d[2 * k], d[2 * k + 1], v[r]);
+    }
+}
+
+template <int C, int T>
+__device__ __forceinline__ void ap_cx(double2 (&v)[PER]) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if (!(r & (1 << C)) || (r & (1 << T))) continue;
+        const double2 t = v[r];
+        v[r] = v[r | (1 << T)];
+        v[r | (1 << T)] = t;
+    }
+}
+
+template <int A, int B>
+__device__ __forceinline__ void ap_swap(double2 (&v)[PER]) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if ((r & (1 << A)) && !(r & (1 << B))) {
+            const int o = (r ^ (1 << A)) | (1 << B);
+            const double2 t = v[r];
+            v[r] = v[o];
+            v[o] = t;
+        }
+    }
+}
+
+// Real 2x2 [m00 m01; m10 m11]: 4 FMA per amplitude instead of 8.
+template <int A>
+__device__ __forceinline__ void ap_u1r(double2 (&v)[PER], const double* m) {
+    const double m00 = m[0], m01 = m[1], m10 = m[2], m11 = m[3];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if (r & (1 << A)) continue;
+        const double2 a = v[r], b = v[r | (1 << A)];
+        v[r] = make_double2(fma(m00, a.x, m01 * b.x), fma(m00, a.y, m01 * b.y));
+        v[r | (1 << A)] = make_double2(fma(m10, a.x, m11 * b.x), fma(m10, a.y, m11 * b.y));
+    }
+}
+
+// [m00, i p01; i p10, m11] with real m00, p01, p10, m11 (rx-type): 4 FMA per amplitude.
+template <int A>
+__device__ __forceinline__ void ap_u1x(double2 (&v)[PER], const double* m) {
+    const double m00 = m[0], p01 = m[1], p10 = m[2], m11 = m[3];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if (r & (1 << A)) continue;
+        const double2 a = v[r], b = v[r | (1 << A)];
+        v[r] = make_double2(fma(m00, a.x, -p01 * b.y), fma(m00, a.y, p01 * b.x));
+        v[r | (1 << A)] = make_double2(fma(m11, b.x, -p10 * a.y), fma(m11, b.y, p10 * a.x));
+    }
+}
+
+template <int A>
+__device__ __forceinline__ void ap_d1r(double2 (&v)[PER], const double* d) {
+    const double d0 = d[0], d1 = d[1];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const double s = (r & (1 << A)) ? d1 : d0;
+        v[r] = make_double2(s * v[r].x, s * v[r].y);
+    }
+}
+
+template <int A, int B>
+__device__ __forceinline__ void ap_d2r(double2 (&v)[PER], const double* d) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const double s = d[((r >> A) & 1) | (((r >> B) & 1) << 1)];
+        v[r] = make_double2(s * v[r].x, s * v[r].y);
+    }
+}
+
+}  // namespace qk_sweep_ops
+
+#endif  // QKNIT_SWEEP_OPS_H

@@ -18,6 +18,7 @@ Pipeline of one virtual-circuit run (``run.py:23-71`` in the reference):
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from dataclasses import dataclass, field
 
@@ -102,6 +103,7 @@ class DeviceProgram:
     mats: object
     passes: object  # ctypes array (host)
     struct: _lib.QkProgram = field(default=None)
+    module: object = None  # qk_module* of the per-program kernels (SPLIT programs), or None
 
     @staticmethod
     def upload(prog: FragmentProgram, device) -> "DeviceProgram":
@@ -130,7 +132,32 @@ class DeviceProgram:
         st = _lib.QkProgram(enc.n, enc.n_eff, enc.m, enc.n_slots, int(enc.packed), len(np_pass),
                             ctypes.cast(passes, ctypes.POINTER(_lib.QkPass)),
                             ops.data_ptr(), groups.data_ptr(), mats.data_ptr())
-        return DeviceProgram(prog, enc, ops, groups, mats, passes, st)
+        module = compiled_module(device, enc) if not enc.packed else None
+        return DeviceProgram(prog, enc, ops, groups, mats, passes, st, module)
+
+
+_MODULES: dict = {}
+_modules_lock = threading.Lock()
+
+
+def compiled_module(device: int, enc):
+    """Per-program sweep kernels of a SPLIT program (sweep_codegen.generate), compiled once per
+    (device, program) with hiprtc. QKNIT_SWEEP_JIT=0 selects the interpreter kernel instead."""
+    if os.environ.get("QKNIT_SWEEP_JIT", "1") == "0":
+        return None
+    from . import sweep_codegen
+
+    src, names = sweep_codegen.generate(enc)
+    key = (device, names[0])
+    with _modules_lock:
+        if key not in _MODULES:
+            ctx = get_context(device)
+            arr = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
+            h = ctypes.c_void_p()
+            ctx.check(ctx.lib.qk_module_compile(ctx.handle, src.encode(), arr, len(names), ctypes.byref(h)),
+                      "qk_module_compile")
+            _MODULES[key] = h
+        return _MODULES[key]
 
 
 def jobs_to_device(jobs: JobTable, device):
@@ -156,9 +183,14 @@ def sweep_jobs(ctx: Context, dprog: DeviceProgram, slot_t, sign_t, n_jobs: int, 
               "qk_sweep_workspace_bytes")
     if need.value and (workspace is None or workspace.numel() < need.value):
         workspace = T.empty(need.value, dtype=T.uint8, device=dev)
-    ctx.check(ctx.lib.qk_sweep(ctx.handle, ctypes.byref(dprog.struct), n_jobs, slot_t.data_ptr(),
-                               sign_t.data_ptr(), _ptr(workspace) if need.value else None,
-                               need.value, pjob.data_ptr()), "qk_sweep")
+    if dprog.module is not None:
+        ctx.check(ctx.lib.qk_sweep_compiled(ctx.handle, dprog.module, ctypes.byref(dprog.struct), n_jobs,
+                                            slot_t.data_ptr(), sign_t.data_ptr(), _ptr(workspace),
+                                            need.value, pjob.data_ptr()), "qk_sweep_compiled")
+    else:
+        ctx.check(ctx.lib.qk_sweep(ctx.handle, ctypes.byref(dprog.struct), n_jobs, slot_t.data_ptr(),
+                                   sign_t.data_ptr(), _ptr(workspace) if need.value else None,
+                                   need.value, pjob.data_ptr()), "qk_sweep")
     return pjob, workspace
 
 

@@ -1,0 +1,274 @@
+"""Per-program sweep kernels: HIP source specialised to one encoded fragment program.
+
+The interpreter kernel (``csrc/qknit.hip``, ``qk_sweep_pass_kernel``) executes an encoded
+program (``sweep_plan.encode``) by loading every op descriptor and matrix at run time and
+dispatching on its kind and fiber positions. For SPLIT programs (``n > 12``: the syc
+fragments) that dispatch and the generic index arithmetic dominate: on syc 32 5 only 12% of
+its VALU instructions are f64 FMAs and waves wait 49% of their time.
+
+:func:`generate` emits, for each pass of a SPLIT program, one ``extern "C"`` kernel with the
+same semantics as the interpreter on that pass — sparse INIT tile, known-zero state bits,
+fiber groups, the FINAL trace over unmeasured qubits — but with the tile layout, the bit
+deposits, the fiber positions, the op sequence and every gate matrix as compile-time
+constants (hex float literals: exact). The per-op arithmetic is the interpreter's own
+(``csrc/sweep_ops.h``, inlined into the source), so results agree with it. The source is
+compiled at plan time with hiprtc (``qk_module_compile``) and run by ``qk_sweep_compiled``.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+
+from . import sweep_plan as sp
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+OPS_HEADER = os.path.join(_HERE, "csrc", "sweep_ops.h")
+NT = 256
+PER = 16
+
+
+def _lit(x: float) -> str:
+    x = float(x)
+    return x.hex() if x != 0.0 else ("-0.0" if str(x).startswith("-") else "0.0")
+
+
+def _deposit(src: str, src_bits: list, dst_bits: list) -> str:
+    """Expression moving bit src_bits[i] of ``src`` to bit dst_bits[i] (runs merged)."""
+    terms = []
+    i = 0
+    while i < len(src_bits):
+        j = i
+        while (j + 1 < len(src_bits) and src_bits[j + 1] == src_bits[j] + 1
+               and dst_bits[j + 1] == dst_bits[j] + 1):
+            j += 1
+        width = j - i + 1
+        mask = (1 << width) - 1
+        sb, db = src_bits[i], dst_bits[i]
+        terms.append(f"((({src}) >> {sb}) & 0x{mask:x}ull) << {db}")
+        i = j + 1
+    return "(" + " | ".join(terms) + ")" if terms else "0ull"
+
+
+def _bits(mask: int) -> list:
+    return [b for b in range(64) if (mask >> b) & 1]
+
+
+def _swz(t: int) -> int:
+    return t ^ (((t >> 4) ^ (t >> 8)) & 15)
+
+
+class _Emitter:
+    def __init__(self):
+        self.lines: list[str] = []
+
+    def __call__(self, s: str = "", ind: int = 1) -> None:
+        self.lines.append("    " * ind + s)
+
+
+def _variant(vals: list, ebits: list) -> list:
+    """select_variant4 semantics: vals holds up to 4 variants of length N; ebits = [b1 expr or
+    None, b2 expr or None]. Returns per-element C expressions."""
+    b1, b2 = ebits
+    nvar = 1 + (b1 is not None) + 2 * (b2 is not None)
+    del nvar
+    N = len(vals[0])
+
+    def pick(lo_v, hi_v, cond):
+        return [f"({cond} ? {_lit(h)} : {_lit(l)})" if h != l else _lit(l) for l, h in zip(lo_v, hi_v)]
+
+    low = pick(vals[0], vals[1], b1) if b1 is not None else [_lit(x) for x in vals[0]]
+    if b2 is None:
+        return low
+    high = pick(vals[2], vals[3], b1) if b1 is not None else [_lit(x) for x in vals[2]]
+    return [f"({b2} ? {h} : {l})" if h != l else l for l, h in zip(low, high)][:N]
+
+
+def _emit_op(e: _Emitter, op, mats, ext, n_slots: int) -> None:
+    kind, a, b, e1, e2, slot, mat = (int(op["kind"]), int(op["a"]), int(op["b"]), int(op["e1"]),
+                                     int(op["e2"]), int(op["slot"]), int(op["mat"]))
+    b1 = ext(e1) if e1 >= 0 else None
+    b2 = ext(e2) if e2 >= 0 else None
+
+    def arr(n, off=0):
+        return [float(x) for x in mats[mat + off: mat + off + n]]
+
+    def const_arr(name, exprs):
+        e(f"const double {name}[{len(exprs)}] = {{{', '.join(exprs)}}};", 2)
+
+    e("{", 1)
+    if kind == sp.K_U1:
+        vals = [arr(8), arr(8, 8)] if b1 is not None else [arr(8)]
+        const_arr("m", _variant(vals, [b1, None]))
+        e(f"ap_u1<{a}>(v, m);", 2)
+    elif kind == sp.K_D1:
+        vals = [arr(4), arr(4, 4)] if b1 is not None else [arr(4)]
+        const_arr("d", _variant(vals, [b1, None]))
+        e(f"ap_d1<{a}>(v, d);", 2)
+    elif kind == sp.K_SLOT:
+        e(f"ap_u1<{a}>(v, job_slots + (job * {n_slots} + {slot}) * 8);", 2)
+    elif kind == sp.K_U2:
+        const_arr("m", [_lit(x) for x in arr(32)])
+        e(f"ap_u2<{a}, {b}>(v, m);", 2)
+    elif kind == sp.K_D2:
+        const_arr("d", [_lit(x) for x in arr(8)])
+        e(f"ap_d2<{a}, {b}>(v, d);", 2)
+    elif kind == sp.K_CX:
+        e(f"ap_cx<{a}, {b}>(v);", 2)
+    elif kind == sp.K_SWAP:
+        e(f"ap_swap<{a}, {b}>(v);", 2)
+    elif kind in (sp.K_SCALE, sp.K_SCALER):
+        N = 2 if kind == sp.K_SCALE else 1
+        nv = 4 if b2 is not None else 2 if b1 is not None else 1
+        # select_variant4 reads p[0:2N) for the b1 pair and p[2N:4N) when h2
+        vals = [arr(N, k * N) for k in range(4)] if b2 is not None else [arr(N, k * N) for k in range(2)]
+        if b1 is None:  # variant pair collapses to its first entry
+            vals = [vals[0], vals[0]] + ([vals[2], vals[2]] if b2 is not None else [])
+        del nv
+        s = _variant(vals, [b1, b2])
+        if kind == sp.K_SCALE:
+            e(f"const double sr = {s[0]}, si = {s[1]};", 2)
+            e("#pragma unroll", 0)
+            e(f"for (int r = 0; r < {PER}; ++r) v[r] = cmul(sr, si, v[r]);", 2)
+        else:
+            e(f"const double sr = {s[0]};", 2)
+            e("#pragma unroll", 0)
+            e(f"for (int r = 0; r < {PER}; ++r) v[r] = make_double2(sr * v[r].x, sr * v[r].y);", 2)
+    elif kind == sp.K_U1R:
+        const_arr("m", [_lit(x) for x in arr(4)])
+        e(f"ap_u1r<{a}>(v, m);", 2)
+    elif kind == sp.K_U1X:
+        const_arr("m", [_lit(x) for x in arr(4)])
+        e(f"ap_u1x<{a}>(v, m);", 2)
+    elif kind == sp.K_D1R:
+        vals = [arr(2), arr(2, 2)] if b1 is not None else [arr(2)]
+        const_arr("d", _variant(vals, [b1, None]))
+        e(f"ap_d1r<{a}>(v, d);", 2)
+    elif kind == sp.K_D2R:
+        const_arr("d", [_lit(x) for x in arr(4)])
+        e(f"ap_d2r<{a}, {b}>(v, d);", 2)
+    else:
+        raise ValueError(f"unknown op kind {kind}")
+    e("}", 1)
+
+
+def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str) -> list:
+    n, m = enc.n, enc.m
+    P = len(enc.passes)
+    ps = enc.passes[ip]
+    flags = int(ps["flags"])
+    init, final = bool(flags & sp.PASS_INIT), bool(flags & sp.PASS_FINAL)
+    tile_mask = int(ps["tile_mask"])
+    bitpos = _bits(tile_mask)
+    assert len(bitpos) == sp.TILE_BITS
+    nmask = (1 << n) - 1
+    outside = _bits(nmask & ~tile_mask)
+    init_sparse = ip == 0 and P > 1
+    zero_mask = (nmask & ~int(enc.passes[0]["tile_mask"])) if ip == 1 else 0
+    tpj_log = 0 if init_sparse else n - sp.TILE_BITS
+    traced = int(ps["traced_local"])
+    mmask = (1 << m) - 1
+    hi = [sum(((i >> k) & 1) << bitpos[8 + k] for k in range(4)) for i in range(PER)]
+
+    e = _Emitter()
+    e(f'extern "C" __global__ __launch_bounds__({NT}) void {name}(', 0)
+    e("const double* __restrict__ job_slots, const double* __restrict__ job_sign,", 2)
+    e("double2* __restrict__ state, double* __restrict__ pjob, long long n_jobs) {", 2)
+    e("using namespace qk_sweep_ops;")
+    e("__shared__ double2 lds[4096];")
+    e("const unsigned tid = threadIdx.x;")
+    e(f"const long long job = (long long)(blockIdx.x >> {tpj_log});")
+    if tpj_log:
+        e(f"const unsigned long long tj = blockIdx.x & {(1 << tpj_log) - 1}u;")
+        e(f"const unsigned long long tbase = {_deposit('tj', list(range(len(outside))), outside)};")
+    else:
+        e("const unsigned long long tbase = 0ull;")
+    e(f"const unsigned long long lo = {_deposit('(unsigned long long)tid', list(range(8)), bitpos[:8])};")
+    e(f"double2* st = state + job * {1 << n}ll;")
+    e("(void)n_jobs; (void)job_slots; (void)st; (void)lo;")
+    zero_tile = init and not init_sparse and tpj_log > 0
+    if init:
+        e("lds[swz(tid)] = make_double2((tid == 0 && tbase == 0ull) ? 1.0 : 0.0, 0.0);")
+        for i in range(1, PER):
+            e(f"lds[swz(tid + {NT * i})] = make_double2(0.0, 0.0);")
+    else:
+        for i in range(PER):
+            s = f"(tbase | lo | 0x{hi[i]:x}ull)"
+            if zero_mask:
+                e(f"{{ const unsigned long long s = {s}; lds[swz(tid + {NT * i})] = "
+                  f"(s & 0x{zero_mask:x}ull) ? make_double2(0.0, 0.0) : st[s]; }}")
+            else:
+                e(f"lds[swz(tid + {NT * i})] = st[{s}];")
+    e("__syncthreads();")
+    if zero_tile:
+        if not final:
+            raise ValueError("SPLIT INIT pass that is not FINAL must be sparse")
+        e("if (tbase == 0ull) {")
+    for gi in range(int(ps["group_begin"]), int(ps["group_end"])):
+        gr = enc.groups[gi]
+        pos = [int(x) for x in gr["pos"]]
+        nonfib = [p for p in range(sp.TILE_BITS) if p not in pos]
+        e("{")
+        e(f"const unsigned base = {_deposit('tid', list(range(8)), nonfib)};", 2)
+        cst = [sum(((r >> k) & 1) << pos[k] for k in range(4)) for r in range(PER)]
+        e("double2 v[16];", 2)
+        for r in range(PER):
+            e(f"v[{r}] = lds[swz(base | {cst[r]}u)];", 2)
+
+        def ext(ebit, nonfib=nonfib):
+            if ebit in bitpos:
+                j = bitpos.index(ebit)
+                if j not in nonfib:  # a fiber position: the base has it cleared
+                    return "false"
+                return f"((tid >> {nonfib.index(j)}) & 1u)"
+            return f"((tbase >> {ebit}) & 1ull)"
+
+        for oi in range(int(gr["op_begin"]), int(gr["op_end"])):
+            _emit_op(e, enc.ops[oi], enc.mats, ext, enc.n_slots)
+        for r in range(PER):
+            e(f"lds[swz(base | {cst[r]}u)] = v[{r}];", 2)
+        e("__syncthreads();", 2)
+        e("}")
+    if zero_tile:
+        e("}")
+    if final:
+        subs = []
+        sub = 0
+        while True:
+            subs.append(sub)
+            sub = (sub - traced) & traced
+            if sub == 0:
+                break
+        e(f"const double sgn = job_sign[job];")
+        for i in range(PER):
+            if (NT * i) & traced:
+                continue
+            cond = traced & (NT - 1)
+            e(f"if (!(tid & {cond}u)) {{" if cond else "{")
+            e("double acc = 0.0;", 2)
+            for sb in subs:
+                e(f"{{ const double2 z = lds[swz((tid + {NT * i}) | {sb}u)]; "
+                  f"acc = fma(z.x, z.x, fma(z.y, z.y, acc)); }}", 2)
+            e(f"const unsigned long long x = (tbase | lo | 0x{hi[i]:x}ull) & 0x{mmask:x}ull;", 2)
+            e(f"pjob[(job << {m}) + (long long)x] = sgn * acc;", 2)
+            e("}")
+    else:
+        for i in range(PER):
+            e(f"st[tbase | lo | 0x{hi[i]:x}ull] = lds[swz(tid + {NT * i})];")
+    e("}", 0)
+    return e.lines
+
+
+def generate(enc: sp.EncodedProgram) -> tuple[str, list]:
+    """HIP source (sweep_ops.h inlined) and kernel names, one kernel per pass."""
+    if enc.packed:
+        raise ValueError("per-program kernels are generated for SPLIT programs (n > 12) only")
+    body = []
+    names = []
+    key = hashlib.sha1(enc.ops.tobytes() + enc.groups.tobytes() + enc.passes.tobytes()
+                       + enc.mats.tobytes() + bytes([enc.n, enc.m, enc.n_slots])).hexdigest()[:12]
+    for ip in range(len(enc.passes)):
+        name = f"qk_sweep_{key}_p{ip}"
+        names.append(name)
+        body += _pass_kernel(enc, ip, name) + [""]
+    src = open(OPS_HEADER).read() + "\n" + "\n".join(body) + "\n"
+    return src, names

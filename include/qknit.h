@@ -105,6 +105,22 @@ int qk_sweep_workspace_bytes(const qk_program* prog, int64_t n_jobs, int64_t* by
 int qk_sweep(qk_ctx* ctx, const qk_program* prog, int64_t n_jobs, const double* job_slots,
              const double* job_sign, void* workspace, int64_t workspace_bytes, double* pjob);
 
+/* ---- per-program sweep kernels (run-time compiled; qknit_jit.hip, sweep_codegen.py) --------
+ * Same contract as qk_sweep for SPLIT programs (n > 12), but the passes run as kernels
+ * specialised to one fragment program (tile layout, fibers, ops and matrices as constants). */
+typedef struct qk_module qk_module;
+
+/* Compile HIP source with hiprtc for gfx950 and load it; names: its extern "C" kernels. */
+int qk_module_compile(qk_ctx* ctx, const char* source, const char* const* names, int n_names,
+                      qk_module** out);
+int qk_module_destroy(qk_module* module);
+
+/* qk_sweep with pass i launched as module kernel i (kernel args: job_slots, job_sign, state,
+ * pjob, n_jobs), same grid (sparse INIT pass: one tile per job). */
+int qk_sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* prog, int64_t n_jobs,
+                      const double* job_slots, const double* job_sign, void* workspace,
+                      int64_t workspace_bytes, double* pjob);
+
 /* q[l][x] = sum_{j in [offsets[l], offsets[l+1])} pjob[j][x]   (offsets: DEVICE, n_labels+1) */
 int qk_reduce_labels(qk_ctx* ctx, int64_t n_labels, const int64_t* offsets, int64_t width,
                      const double* pjob, double* q);

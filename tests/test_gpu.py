@@ -237,6 +237,24 @@ def test_split_mode_fragment_matches_oracle(T):
             np.testing.assert_allclose(q[li], ref, atol=TOL, rtol=0)
 
 
+def test_compiled_sweep_matches_interpreter(T):
+    """Per-program kernels (sweep_codegen + hiprtc, qk_sweep_compiled) == the interpreter kernel
+    (qk_sweep) on every branch job of both syc 32 5 fragments (basis-reduced: 625 jobs each)."""
+    import dataclasses
+
+    _, cut = cutting.config_cut_circuit("syc", 32, 5, 2)[:2]
+    virt = VirtualCircuit(cut)
+    ctx = engine.get_context(0)
+    for fs in engine.prepare_fragments(virt, 0, basis=True):
+        assert fs.dprog.module is not None, "SPLIT programs run as compiled kernels"
+        slot_t, sign_t, _ = engine.jobs_to_device(fs.jobs, 0)
+        jit, _ = engine.sweep_jobs(ctx, fs.dprog, slot_t, sign_t, fs.jobs.n_jobs)
+        interp, _ = engine.sweep_jobs(ctx, dataclasses.replace(fs.dprog, module=None), slot_t, sign_t,
+                                      fs.jobs.n_jobs)
+        T.cuda.synchronize()
+        assert float((jit - interp).abs().max()) <= 1e-13
+
+
 def _uncut_dense_gpu(circ):
     """Exact uncut distribution on the GPU: the whole circuit as one 0-cut fragment."""
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.circuit import QuantumCircuit, QuantumRegister

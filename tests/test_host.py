@@ -244,3 +244,25 @@ def test_device_keys_cache():
     assert engine._device_keys((2, 3, 4), 2, 5, dev).tolist() == [8, 12, 16]
     assert engine._device_keys((0, 3, 5), None, None, dev).tolist() == deposit_keys([0, 3, 5]).tolist()
     assert engine._device_keys((0, 3, 5), 1, 3, dev).tolist() == [1, 8]
+
+
+def test_generated_sweep_kernels_compile_for_gfx950(tmp_path):
+    """sweep_codegen emits one kernel per pass of a SPLIT program; the source (sweep_ops.h
+    inlined) compiles for gfx950 with hipcc here (on the GPU the same text goes to hiprtc)."""
+    import shutil
+    import subprocess
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import sweep_codegen
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    _, cut, _ = cutting.config_cut_circuit("syc", 32, 5, 2)
+    virt = VirtualCircuit(cut)
+    for fs in engine.prepare_fragments(virt, upload=False, basis=True)[:1]:
+        enc = sweep_plan.encode(fs.prog)
+        src, names = sweep_codegen.generate(enc)
+        assert len(names) == len(enc.passes)
+        f = tmp_path / "k.hip"
+        f.write_text(src)
+        r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-c",
+                            str(f), "-o", str(tmp_path / "k.o")], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr[-2000:]

@@ -25,7 +25,7 @@ def main():
     _, cut, _ = cutting.config_cut_circuit(name, n, d, p, var)
     virt = VirtualCircuit(cut)
     ctx = engine.get_context(0)
-    frags = engine.prepare_fragments(virt, 0, dedup=not args.no_dedup)
+    frags = engine.prepare_fragments(virt, 0, dedup=not args.no_dedup, basis=not args.no_dedup)
     tabs = []
     for fs in frags:
         slot_t, sign_t, off_t = engine.jobs_to_device(fs.jobs, 0)
