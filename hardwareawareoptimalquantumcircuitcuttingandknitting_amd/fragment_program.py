@@ -423,6 +423,19 @@ class JobTable:
     def n_jobs(self) -> int:
         return int(self.sign.shape[0])
 
+    def label_jobs(self) -> np.ndarray:
+        """Branch jobs per label."""
+        return np.diff(self.label_offsets)
+
+    def take(self, rows) -> "JobTable":
+        """The jobs of labels ``rows`` (any order), labels renumbered 0..len(rows)-1."""
+        rows = np.asarray(rows, dtype=np.int64)
+        offs = self.label_offsets
+        idx = (np.concatenate([np.arange(offs[r], offs[r + 1]) for r in rows]) if rows.size
+               else np.zeros(0, np.int64))
+        new_offs = np.concatenate([[0], np.cumsum(offs[rows + 1] - offs[rows])]).astype(np.int64)
+        return JobTable(self.slot_mats[idx], self.sign[idx], new_offs, self.branch_bits[idx])
+
 
 def build_jobs(prog: FragmentProgram, labels: list) -> JobTable:
     """Expand labels into branch jobs (labels in the given order, jobs contiguous)."""

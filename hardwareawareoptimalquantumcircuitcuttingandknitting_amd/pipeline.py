@@ -41,6 +41,18 @@ def _shard(n: int, rank: int, world: int) -> tuple[int, int]:
     return lo, min(n, lo + per)
 
 
+def _deal_rows(jobs_per_row: np.ndarray, world: int) -> list:
+    """Swept rows per rank, balanced by branch jobs: rows in descending job count dealt
+    round-robin, reversing direction every round (at most ceil(n / world) rows per rank).
+    Contiguous shards would give the rank holding a measured side program twice the jobs."""
+    order = sorted(range(len(jobs_per_row)), key=lambda r: (-int(jobs_per_row[r]), r))
+    out = [[] for _ in range(world)]
+    for k, r in enumerate(order):
+        rnd, pos = divmod(k, world)
+        out[pos if rnd % 2 == 0 else world - 1 - pos].append(r)
+    return [sorted(x) for x in out]
+
+
 # fp64 flops per amplitude the sweep kernel spends on one op of each kind (qk_op.kind order,
 # csrc/qknit.hip ap_* helpers: a complex multiply-add is 1 mul + 3 fma per component)
 _OP_FLOPS = (14, 6, 14, 30, 6, 0, 0, 6, 6, 6, 2, 2, 2)
@@ -145,33 +157,41 @@ class KnitPipeline:
         self.sweeps = []  # per fragment: device job tables and buffers, or None (dropped)
         L = self.ops.num_terms
         self.term_range = _shard(L, self.rank, self.world) if self.mode == "reduce" else (0, L)
+        self.place = {}  # gather mode: fragment -> position of each swept row in the gathered rows
         for i, fs in enumerate(self.frags):
             if fs.dropped:
                 self.sweeps.append(None)
                 continue
             nl = fs.n_rows
-            if self.mode == "reduce":
-                t0, t1 = self.term_range
-                rows = np.unique(self.ops.rows[i][t0:t1])
-                lo, hi = (int(rows.min()), int(rows.max()) + 1) if rows.size else (0, 0)
-            elif self.mode == "gather":
-                lo, hi = _shard(nl, self.rank, self.world)
-            else:
-                lo, hi = 0, nl
             jobs = fs.jobs
-            j0, j1 = int(jobs.label_offsets[lo]), int(jobs.label_offsets[hi])
-            sub = JobTable(jobs.slot_mats[j0:j1], jobs.sign[j0:j1], jobs.label_offsets[lo:hi + 1] - j0,
-                           jobs.branch_bits[j0:j1])
+            lo = 0
+            if self.mode == "gather":
+                per = -(-nl // self.world)
+                dealt = _deal_rows(jobs.label_jobs(), self.world)
+                place = np.zeros(nl, dtype=np.int64)
+                for r, rows_r in enumerate(dealt):
+                    place[rows_r] = r * per + np.arange(len(rows_r))
+                self.place[i] = place
+                sub = jobs.take(dealt[self.rank])
+            else:
+                if self.mode == "reduce":
+                    t0, t1 = self.term_range
+                    rows = np.unique(self.ops.rows[i][t0:t1])
+                    lo, hi = (int(rows.min()), int(rows.max()) + 1) if rows.size else (0, 0)
+                else:
+                    lo, hi = 0, nl
+                sub = jobs.take(np.arange(lo, hi))
+            n_local = len(sub.label_offsets) - 1
             slot_t, sign_t, off_t = be.upload_jobs(sub)
             n_jobs = sub.n_jobs
             width = 1 << fs.prog.m
             need = be.workspace_bytes(fs, n_jobs) if n_jobs else 0
             # gather mode: a rank's rows live in a zero-padded [per, width] buffer (the unit of
-            # the collectives); the last rank's padding rows stay zero
-            rows = -(-nl // self.world) if self.mode == "gather" else max(hi - lo, 1)
+            # the collectives); padding rows stay zero
+            rows = -(-nl // self.world) if self.mode == "gather" else max(n_local, 1)
             alloc = be.zeros if self.mode == "gather" else be.empty
-            branching = n_jobs != hi - lo
-            self.sweeps.append(dict(lo=lo, hi=hi, slot=slot_t, sign=sign_t, off=off_t, n_jobs=n_jobs,
+            branching = n_jobs != n_local
+            self.sweeps.append(dict(lo=lo, n_local=n_local, slot=slot_t, sign=sign_t, off=off_t, n_jobs=n_jobs,
                                     pjob=(be.empty((max(n_jobs, 1), width), T.float64) if branching
                                           else alloc((max(rows, 1), width), T.float64)),
                                     q=alloc((max(rows, 1), width), T.float64) if branching else None,
@@ -205,15 +225,25 @@ class KnitPipeline:
         self.gather_idx, self.gather_coef, self.transforms = [], [], []
         t0, t1 = self.term_range
         for i, fs in enumerate(self.frags):
+            place = self.place.get(i)
             if ops.transforms[i] is not None:
-                self.transforms.append(be.to_device(ops.transforms[i].T))
+                Wt = ops.transforms[i].T  # [swept rows, terms]
+                if place is not None:  # rows as the collectives deliver them (rank-major, padded)
+                    Wg = np.zeros((self.world * -(-fs.n_rows // self.world), Wt.shape[1]))
+                    Wg[place] = Wt
+                    Wt = Wg
+                self.transforms.append(be.to_device(Wt))
                 self.gather_idx.append(None)
                 self.gather_coef.append(None)
             else:
                 self.transforms.append(None)
                 sw = self.sweeps[i]
-                base = sw["lo"] if (sw is not None and self.mode == "reduce") else 0
-                self.gather_idx.append(be.to_device(ops.rows[i][t0:t1] - base))
+                rows = ops.rows[i][t0:t1]
+                if place is not None:
+                    rows = place[rows]
+                elif sw is not None and self.mode == "reduce":
+                    rows = rows - sw["lo"]
+                self.gather_idx.append(be.to_device(rows))
                 self.gather_coef.append(be.to_device(ops.coefs[i][t0:t1]))
         self.order = engine.contract_order(ops.clbits)
         self.row_block = None
@@ -242,14 +272,14 @@ class KnitPipeline:
             if sw["n_jobs"]:
                 be.sweep(fs, sw["slot"], sw["sign"], sw["n_jobs"], sw["pjob"], sw["ws"])
             if sw["q"] is not None:
-                q = be.reduce_labels(sw["pjob"], sw["off"], sw["hi"] - sw["lo"], sw["q"])
+                q = be.reduce_labels(sw["pjob"], sw["off"], sw["n_local"], sw["q"])
             else:
                 q = sw["pjob"]
             if self.mode == "gather":
                 work, qs[i] = self._exchange(i, q)
                 pending.append(work)
             else:
-                qs[i] = q[: sw["hi"] - sw["lo"]]
+                qs[i] = q[: sw["n_local"]]
         for work in pending:
             work.wait()
         return qs
@@ -259,7 +289,6 @@ class KnitPipeline:
         import torch.distributed as dist
 
         kind, send, recv = self.xbuf[i]
-        n_rows = self.frags[i].n_rows
         if kind == "a2a":  # chunk p = this rank's rows, column block p
             P, per, bw = send.shape
             send.copy_(qpad[:per].view(per, P, bw).transpose(0, 1))
@@ -267,7 +296,8 @@ class KnitPipeline:
         else:
             per = recv.shape[0] // self.world
             work = dist.all_gather_into_tensor(recv, qpad[:per], group=self.group, async_op=True)
-        return work, recv[:n_rows]
+        # rows arrive rank-major (self.place); the transforms / gather indices are laid out so
+        return work, recv
 
     def operands(self, qs: list) -> list:
         T, be = self.T, self.be
@@ -372,7 +402,7 @@ class KnitPipeline:
                 per_job = 2 * tile + S + (P - 3) * 2 * S + S + out
             hbm += J * per_job
             if sw["q"] is not None:
-                hbm += J * out + (sw["hi"] - sw["lo"]) * out
+                hbm += J * out + sw["n_local"] * out
             alg += J * len(fs.prog.ops) * 32 * (1 << fs.prog.n)
             flops += J * _sweep_flops_per_job(enc)
         return {"hbm": hbm, "algorithmic": alg, "flops": flops}

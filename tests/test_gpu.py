@@ -292,3 +292,40 @@ def test_syc_32_full_knit_equals_uncut(T, depth, variant, factored):
     assert err <= TOL
     del unc, knit
     T.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("factored", [False, True])
+def test_gather_mode_through_rccl_single_rank(T, factored):
+    """The multi-GPU gather path (job-dealt rows, all_to_all of the row side, all_gather of the
+    column side, output-row block contraction) on the HIP backend with a real RCCL
+    process group of world size 1 (the only size one GPU allows; 2-4 ranks run under gloo in
+    test_distributed.py)."""
+    import socket
+
+    import torch.distributed as dist
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.knit_plan import deposit_keys
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=T.device("cuda", 0))
+    try:
+        for name in ("cx_3cuts", "three_wide", "move_gate", "hwe_16_1_p3"):
+            _, cut = CASES[name]()
+            pipe = KnitPipeline(VirtualCircuit(cut), factored=factored, rank=0, world=1, mode="gather")
+            res = pipe.step().cpu().numpy()
+            cls = pipe.ops.clbits
+            kA = deposit_keys(cls[pipe.order[0]])
+            for i in pipe.order[1:-1]:
+                kA = (kA[None, :] + deposit_keys(cls[i])[:, None]).reshape(-1)
+            kB = deposit_keys(cls[pipe.order[-1]])
+            lo, hi = pipe.row_block
+            full = np.zeros(1 << pipe.N)
+            full[(kA[lo:hi, None] + kB[None, :]).reshape(-1)] = res[: (hi - lo) * kB.size]
+            np.testing.assert_allclose(full, dense.run_dense(cut), atol=TOL, rtol=0)
+    finally:
+        dist.destroy_process_group()

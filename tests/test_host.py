@@ -266,3 +266,19 @@ def test_generated_sweep_kernels_compile_for_gfx950(tmp_path):
         r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-c",
                             str(f), "-o", str(tmp_path / "k.o")], capture_output=True, text=True)
         assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_gather_mode_rows_dealt_by_jobs():
+    """Multi-GPU gather mode deals swept rows to ranks by branch-job count: on syc 32 5 every
+    rank of 2/4/8 gets the same number of jobs (contiguous shards would differ up to 2x)."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import _deal_rows
+
+    _, cut, _ = cutting.config_cut_circuit("syc", 32, 5, 2)
+    fs = engine.prepare_fragments(VirtualCircuit(cut), upload=False, basis=True)[0]
+    jobs = fs.jobs.label_jobs()
+    for world in (2, 4, 8):
+        dealt = _deal_rows(jobs, world)
+        assert sorted(r for rows in dealt for r in rows) == list(range(len(jobs)))
+        assert max(len(r) for r in dealt) <= -(-len(jobs) // world)
+        per_rank = [int(jobs[r].sum()) for r in dealt]
+        assert max(per_rank) - min(per_rank) <= int(jobs.max())
