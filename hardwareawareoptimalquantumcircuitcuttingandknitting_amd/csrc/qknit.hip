@@ -483,7 +483,8 @@ __device__ __forceinline__ void gemm_load(d2_t (&r)[4], const double* __restrict
 }
 
 #ifndef QK_GEMM_STORE
-#define QK_GEMM_STORE 2  // 0: per-element stores; 1: paired 16-B nt stores; 2: paired 16-B sc1 stores
+#define QK_GEMM_STORE 1  // 0: per-element stores; 1: paired 16-B nt stores; 2: paired 16-B sc1 stores
+// (LDS-DMA kernel, syc 32 5 contraction: nt 66.1 TF/s, sc1 65.4)
 #endif
 
 // Swap a 64-bit value with the neighbouring lane (lane ^ 1).
@@ -834,6 +835,7 @@ __global__ __launch_bounds__(256, 2) void qk_gemm_glds_kernel(GemmArgs g) {
     // row addresses are wave-uniform (SGPR base + the lane's 16-B offset): no per-lane 64-bit
     // address arithmetic per load
     const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+    const int src_off = 2 * lane;
     auto issue = [&]() {
         if (issued >= total) return;
         GemmRing& r = ring[issued % G2S];
@@ -843,8 +845,8 @@ __global__ __launch_bounds__(256, 2) void qk_gemm_glds_kernel(GemmArgs g) {
             const int row = wave_s * (G2K / 4) + q;
             const double* pa = g.A + (k0 + row) * g.lda + ibm * GT;
             const double* pb = g.B + (k0 + row) * g.ldb + ibn * GT;
-            glds16(pa + 2 * lane, &r.a[row][0]);
-            glds16(pb + 2 * lane, &r.b[row][0]);
+            glds16(pa + src_off, &r.a[row][0]);
+            glds16(pb + src_off, &r.b[row][0]);
         }
         ++issued;
         if (++ic == nct) {
