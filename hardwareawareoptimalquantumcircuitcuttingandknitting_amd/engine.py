@@ -106,7 +106,7 @@ class DeviceProgram:
     module: object = None  # qk_module* of the per-program kernels (SPLIT programs), or None
 
     @staticmethod
-    def upload(prog: FragmentProgram, device) -> "DeviceProgram":
+    def upload(prog: FragmentProgram, device, jit: bool = True) -> "DeviceProgram":
         T = torch()
         enc = encode(prog)
         dev = T.device("cuda", device)
@@ -132,7 +132,7 @@ class DeviceProgram:
         st = _lib.QkProgram(enc.n, enc.n_eff, enc.m, enc.n_slots, int(enc.packed), len(np_pass),
                             ctypes.cast(passes, ctypes.POINTER(_lib.QkPass)),
                             ops.data_ptr(), groups.data_ptr(), mats.data_ptr())
-        module = compiled_module(device, enc) if not enc.packed else None
+        module = compiled_module(device, enc) if (jit and not enc.packed) else None
         return DeviceProgram(prog, enc, ops, groups, mats, passes, st, module)
 
 
@@ -314,11 +314,17 @@ def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = 
         # run.py:49-58 drops a fragment whose get_counts() raises, i.e. when some instance of
         # it measures nothing at all (no data measurement and no config measurement).
         dropped = prog.m == 0 and _some_label_unmeasured(prog, labels)
-        dp = DeviceProgram.upload(prog, device) if (upload and not dropped) else None
+        dp = DeviceProgram.upload(prog, device, jit=_worth_compiling(prog, jobs)) if (upload and not dropped) else None
         out.append(FragmentState(frag, labels, prog, dp, jobs, touches, dropped, uidx, unique,
                                  red.labels if red is not None else None,
                                  red.expand if red is not None else None))
     return out
+
+
+def _worth_compiling(prog: FragmentProgram, jobs: JobTable) -> bool:
+    """Per-program kernels pay their hiprtc compile (about 1 s per 100 ops) only on real work:
+    >= 2^24 amplitudes per sweep, and at most 400 ops (qft 16: 586 ops, 20 s, one instance)."""
+    return (jobs.n_jobs << prog.n) >= (1 << 24) and len(prog.ops) <= 400
 
 
 def _some_label_unmeasured(prog: FragmentProgram, labels: list) -> bool:

@@ -273,7 +273,7 @@ def _chunked_max_abs_diff(a, b, chunk=1 << 28):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("depth,variant,factored", [(1, "forced", False), (5, "ref", True)])
+@pytest.mark.parametrize("depth,variant,factored", [(1, "forced", False), (1, "ref", True), (5, "ref", True)])
 def test_syc_32_full_knit_equals_uncut(T, depth, variant, factored):
     """Full size (2^32 outputs): knit of the cut syc 32 circuit == uncut 32-qubit sweep.
 
@@ -329,3 +329,12 @@ def test_gather_mode_through_rccl_single_rank(T, factored):
             np.testing.assert_allclose(full, dense.run_dense(cut), atol=TOL, rtol=0)
     finally:
         dist.destroy_process_group()
+
+
+def test_qft_16_1_p3_config_matches_oracle(T):
+    """BASELINE config qft 16 1 p=3: the cutter keeps all 16 lines in one fragment (0 cuts, two
+    empty fragments); 586 fused ops on one instance (interpreter kernel)."""
+    name, n, d, p, var = cutting.BASELINE_CONFIGS["qft_16_1_p3"]
+    _, cut, _ = cutting.config_cut_circuit(name, n, d, p, var)
+    out, _ = run_virtual_circuit_dense(VirtualCircuit(cut))
+    np.testing.assert_allclose(out.cpu().numpy(), dense.run_dense(cut), atol=TOL, rtol=0)
