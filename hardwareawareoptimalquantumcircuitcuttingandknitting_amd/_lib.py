@@ -52,6 +52,9 @@ SIGNATURES = {
     "qk_threshold_count": (c_i32, [c_vp, c_i64, c_vp, ctypes.c_double, c_vp, c_i64, c_vp]),
     "qk_npd": (c_i32, [c_vp, c_i64, c_vp, ctypes.c_double, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "qk_hellinger": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "qk_sample_cdf": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "qk_sample_counts": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_u64, c_vp]),
+    "qk_fold_counts": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, ctypes.c_double, c_vp]),
 }
 
 _lock = threading.Lock()

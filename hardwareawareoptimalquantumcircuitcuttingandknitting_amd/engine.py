@@ -18,6 +18,7 @@ Pipeline of one virtual-circuit run (``run.py:23-71`` in the reference):
 from __future__ import annotations
 
 import ctypes
+import dataclasses
 import os
 import threading
 from dataclasses import dataclass, field
@@ -202,6 +203,68 @@ def reduce_labels(ctx: Context, pjob, off_t, n_labels: int, q=None):
     ctx.check(ctx.lib.qk_reduce_labels(ctx.handle, n_labels, off_t.data_ptr(), width,
                                        pjob.data_ptr(), q.data_ptr()), "qk_reduce_labels")
     return q
+
+
+# ----------------------------------------------------------------------------- shot sampling
+_SEED_STRIDE = 0x632BE59BD9B4E019  # per-fragment stream offset (mirrored by oracle/sampling.py)
+_U64 = (1 << 64) - 1
+
+
+def fragment_seed(seed: int, index: int) -> int:
+    """Sampling stream seed of the index-th non-empty fragment (``fragment_circuits`` order)."""
+    return (int(seed) + index * _SEED_STRIDE) & _U64
+
+
+def sample_fragment(ctx: Context, fs: "FragmentState", shots: int, seed: int, accuracy: float):
+    """Shot-sampled per-label distributions ``q_f [len(fs.labels), 2^m]`` on the GPU.
+
+    The reference samples every instance circuit ``shots`` times and keeps frequencies above
+    ``ACCURACY`` (``run.py:42,56``, ``quasi_distr.py:12-20``). Here every reference label
+    draws its own ``shots`` (labels sharing an instance are not merged, as in the reference)
+    from the exact per-branch distribution of its swept instance (``qk_sweep``): per instance
+    CDF (``qk_sample_cdf``), inverse-CDF draws over (config branch, outcome) with a
+    counter-based stream (``qk_sample_counts``), frequencies truncated at ``accuracy`` and
+    sign-folded over the config bits (``qk_fold_counts``). Rows follow ``fs.labels``; knit
+    the result with :func:`label_rows` ``(fs)``.
+    """
+    T = torch()
+    dev = T.device("cuda", ctx.device)
+    L = len(fs.labels)
+    if shots <= 0:
+        raise ValueError("shots must be positive")
+    if fs.dropped:
+        return T.ones((L, 1), dtype=T.float64, device=dev)
+    if fs.expand is not None:
+        raise ValueError("basis-reduced fragments cannot be sampled (prepare with basis=False)")
+    jobs = fs.jobs
+    width = 1 << fs.prog.m
+    slot_t, sign_t, off_t = jobs_to_device(jobs, ctx.device)
+    pjob, _ = sweep_jobs(ctx, fs.dprog, slot_t, sign_t, jobs.n_jobs)
+    cdf = T.empty_like(pjob)
+    n_seg = len(jobs.label_offsets) - 1
+    ctx.check(ctx.lib.qk_sample_cdf(ctx.handle, n_seg, off_t.data_ptr(), width, pjob.data_ptr(),
+                                    cdf.data_ptr()), "qk_sample_cdf")
+    seg = np.ascontiguousarray(fs.row_of_label(), dtype=np.int64)
+    offs = jobs.label_offsets
+    row_off = np.zeros(L + 1, dtype=np.int64)
+    np.cumsum((offs[1:] - offs[:-1])[seg], out=row_off[1:])
+    rows = np.concatenate([np.arange(offs[s], offs[s + 1]) for s in seg])
+    seg_t = T.from_numpy(seg).to(dev)
+    row_off_t = T.from_numpy(row_off).to(dev)
+    row_sign_t = T.from_numpy(np.ascontiguousarray(jobs.sign[rows])).to(dev)
+    counts = T.zeros((int(row_off[-1]), width), dtype=T.int32, device=dev)
+    ctx.check(ctx.lib.qk_sample_counts(ctx.handle, L, 0, seg_t.data_ptr(), off_t.data_ptr(), row_off_t.data_ptr(),
+                                       width, cdf.data_ptr(), int(shots), int(seed) & _U64, counts.data_ptr()),
+              "qk_sample_counts")
+    q = T.empty((L, width), dtype=T.float64, device=dev)
+    ctx.check(ctx.lib.qk_fold_counts(ctx.handle, L, row_off_t.data_ptr(), width, row_sign_t.data_ptr(),
+                                     counts.data_ptr(), int(shots), float(accuracy), q.data_ptr()), "qk_fold_counts")
+    return q
+
+
+def label_rows(fs: "FragmentState") -> "FragmentState":
+    """``fs`` with one row per reference label: the layout of sampled and foreign-backend q_f."""
+    return dataclasses.replace(fs, uidx=None, unique_labels=None)
 
 
 # ----------------------------------------------------------------------------- GEMM helpers

@@ -3,10 +3,13 @@
 Drop-in for ``third_party/qvm/qvm/run.py:23-71``: same name, same arguments,
 same return shape ``(dict[int, float], RunTimeInfo)``. Differences, by design:
 
-* instances are simulated exactly (fp64 statevector, HIP) instead of being
-  sampled with ``shots`` (``run.py:42``); ``shots`` only matters for fragments
-  whose backend was replaced by a foreign (e.g. qiskit-aer) backend, which are
-  run through the reference's own counts path;
+* by default instances are simulated exactly (fp64 statevector, HIP) instead of
+  being sampled with ``shots`` (``run.py:42``); ``sample=True`` draws ``shots``
+  outcomes per instance label from the exact distributions on the GPU
+  (``engine.sample_fragment``: counter-based stream, ``seed``) and applies
+  ``from_counts``' truncation, as the reference's Aer path does; fragments whose
+  backend was replaced by a foreign (e.g. qiskit-aer) backend are run through the
+  reference's own counts path;
 * the knit is one dense fp64 MFMA contraction; ``QuasiDistr``'s ``ACCURACY``
   truncation is applied once to the final distribution instead of after every
   intermediate dict operation, then ``nearest_probability_distribution``
@@ -26,6 +29,7 @@ from time import perf_counter
 import numpy as np
 
 from . import engine
+from . import quasi_distr as _qd
 from .backend import MI355XBackend
 from .quasi_distr import QuasiDistr
 from .virtual_circuit import VirtualCircuit, generate_instantiations
@@ -65,22 +69,27 @@ def _foreign_fragment(virt: VirtualCircuit, fs: engine.FragmentState, backend, s
 
 
 def run_virtual_circuit_dense(virt: VirtualCircuit, shots: int = 20000, *, device: int = 0,
-                              factored: bool = False, out=None):
-    """Sweep + knit; returns ``(dense fp64 tensor [2^N] on device, RunTimeInfo)``."""
+                              factored: bool = False, out=None, sample: bool = False, seed: int = 0):
+    """Sweep (or shot-sample, ``sample=True``) + knit; returns ``(dense fp64 tensor [2^N] on
+    device, RunTimeInfo)``."""
     ctx = engine.get_context(device)
     log.info("Running virtualizer with %d %s fragments and %d vgates...",
              len(virt.fragment_circuits),
              tuple(len(f) for f in virt.fragment_circuits), len(virt.vgate_instructions))
     now = perf_counter()
     native = all(isinstance(virt.get_backend(f), MI355XBackend) for f in virt.fragment_circuits if len(f))
-    frags = engine.prepare_fragments(virt, device, basis=factored and native)
+    frags = engine.prepare_fragments(virt, device, basis=factored and native and not sample)
     qs = []
-    for fs in frags:
+    for i, fs in enumerate(frags):
         backend = virt.get_backend(fs.fragment)
-        if isinstance(backend, MI355XBackend):
+        if isinstance(backend, MI355XBackend) and not sample:
             qs.append(engine.sweep_fragment(ctx, fs))
+            continue
+        if isinstance(backend, MI355XBackend):
+            qs.append(engine.sample_fragment(ctx, fs, shots, engine.fragment_seed(seed, i), _qd.ACCURACY))
         else:
             qs.append(_foreign_fragment(virt, fs, backend, shots, device))
+        frags[i] = engine.label_rows(fs)  # one q row per reference label
     _sync(device)
     run_time = perf_counter() - now
     now = perf_counter()
@@ -92,9 +101,10 @@ def run_virtual_circuit_dense(virt: VirtualCircuit, shots: int = 20000, *, devic
 
 
 def run_virtual_circuit(virt: VirtualCircuit, shots: int = 20000, *, device: int = 0,
-                        dense: bool = False, factored: bool = False):
+                        dense: bool = False, factored: bool = False, sample: bool = False, seed: int = 0):
     """Reference-compatible entry point (``run.py:23-71``)."""
-    out, info = run_virtual_circuit_dense(virt, shots, device=device, factored=factored)
+    out, info = run_virtual_circuit_dense(virt, shots, device=device, factored=factored, sample=sample,
+                                          seed=seed)
     if dense:
         return out, info
     from . import quasi_distr

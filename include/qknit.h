@@ -155,6 +155,28 @@ int qk_threshold_count(qk_ctx* ctx, int64_t n, const double* vals, double acc, v
 int qk_npd(qk_ctx* ctx, int64_t n, const double* vals, double acc, int64_t count, void* ws, int64_t ws_bytes,
            int64_t* out_keys, double* out_vals, int64_t* n_out_dev);
 
+/* ---- shot sampling (qknit_sample.hip; run.py:42 `backend.run(instantiations, shots)` +
+ * quasi_distr.py:12-20 `from_counts`) ----------------------------------------------------------
+ * An instance s owns the pjob rows [seg_off[s], seg_off[s+1]) (its branch jobs, width values each);
+ * its outcome distribution over (row, x) is |pjob|. Reference label l samples instance
+ * label_seg[l] `shots` times and owns the count rows [label_row_off[l], label_row_off[l+1]). */
+
+/* cdf[i] = inclusive prefix sum of |pjob| within each instance (same layout as pjob). */
+int qk_sample_cdf(qk_ctx* ctx, int64_t n_seg, const int64_t* seg_off, int64_t width, const double* pjob,
+                  double* cdf);
+
+/* counts[label_row_off[l]*width + i] += #{draws s < shots : i = first index with cdf > u * total},
+ * u = u(seed, label_base + l, s) a counter-based SplitMix64 stream: results do not depend on
+ * scheduling or on how labels are split over calls. counts must be zeroed by the caller. */
+int qk_sample_counts(qk_ctx* ctx, int64_t n_labels, int64_t label_base, const int64_t* label_seg,
+                     const int64_t* seg_off, const int64_t* label_row_off, int64_t width, const double* cdf,
+                     int64_t shots, uint64_t seed, unsigned int* counts);
+
+/* q[l][x] = sum_r row_sign[r] * f_r(x) over the label's count rows, f = counts / shots, keeping only
+ * f > acc (from_counts truncation at ACCURACY): the config-bit sign fold of the knit. */
+int qk_fold_counts(qk_ctx* ctx, int64_t n_labels, const int64_t* label_row_off, int64_t width,
+                   const double* row_sign, const unsigned int* counts, int64_t shots, double acc, double* q);
+
 /* acc3[0] = sum sqrt(max(p,0) max(q,0)), acc3[1] = sum max(p,0), acc3[2] = sum max(q,0) (device).
  * Hellinger fidelity = (acc3[0] / sqrt(acc3[1] acc3[2]))^2 (Utilities.py:222-224). */
 int qk_hellinger(qk_ctx* ctx, int64_t n, const double* p, const double* q, double* acc3);

@@ -338,3 +338,105 @@ def test_qft_16_1_p3_config_matches_oracle(T):
     _, cut, _ = cutting.config_cut_circuit(name, n, d, p, var)
     out, _ = run_virtual_circuit_dense(VirtualCircuit(cut))
     np.testing.assert_allclose(out.cpu().numpy(), dense.run_dense(cut), atol=TOL, rtol=0)
+
+
+SAMPLE_CASES = ["cx", "rzz", "cx_3cuts", "move", "move_gate", "three", "partial", "bv_5_1_p2", "hwe_16_1_p2"]
+
+
+@pytest.mark.parametrize("case", SAMPLE_CASES)
+def test_sampled_fragments_match_oracle_draw_for_draw(T, case):
+    """qk_sweep + qk_sample_cdf/counts + qk_fold_counts == oracle/sampling.py (the same SplitMix64
+    stream and inverse-CDF draw over the exact instance distribution, from_counts truncation at
+    1e-5, signed fold) for every reference label: exact equality of the sampled q (a draw landing
+    within an ulp of a CDF step could differ; none does on these seeded cases)."""
+    from oracle import sampling
+
+    _, cut = CASES[case]()
+    virt = VirtualCircuit(cut)
+    view = qvm.CutView(cut)
+    ctx = engine.get_context(0)
+    shots, seed, acc = 3000, 17, 1e-5
+    for i, fs in enumerate(engine.prepare_fragments(virt, 0)):
+        q = engine.sample_fragment(ctx, fs, shots, engine.fragment_seed(seed, i), acc).cpu().numpy()
+        if fs.dropped:
+            continue
+        ref = np.stack([r[1] for r in sampling.sampled_fragment(view, list(fs.fragment), i, shots, seed, acc)])
+        np.testing.assert_array_equal(q, ref)
+
+
+@pytest.mark.parametrize("case", ["cx", "move_gate", "three", "cx_3cuts"])
+@pytest.mark.parametrize("factored", [False, True])
+def test_sampled_run_matches_oracle_knit(T, case, factored):
+    """run_virtual_circuit_dense(sample=True) == dense knit of the oracle's sampled fragments."""
+    import hardwareawareoptimalquantumcircuitcuttingandknitting_amd.quasi_distr as pqd
+    from oracle import sampling
+
+    _, cut = CASES[case]()
+    out, _ = run_virtual_circuit_dense(VirtualCircuit(cut), shots=4000, sample=True, seed=3, factored=factored)
+    view = qvm.CutView(cut)
+    qs, cls = {}, {}
+    for i, f in enumerate([list(r) for r in view.qregs if len(r)]):
+        if qvm.instance_distributions(view, f) is None:  # dropped fragment (run.py:49-58)
+            continue
+        qs[tuple(f)] = np.stack([q for _, q in sampling.sampled_fragment(view, f, i, 4000, 3, pqd.ACCURACY)])
+        cls[tuple(f)] = dense.fragment_clbits(view, f)
+    np.testing.assert_allclose(out.cpu().numpy(), dense.dense_knit(view, qs, cls), atol=TOL, rtol=0)
+
+
+def test_sample_counts_split_over_calls_and_oracle(T):
+    """Raw C ABI: counts do not depend on how labels are split over calls (label_base), every
+    label draws exactly `shots`, and each label's counts equal the oracle's draws."""
+    from oracle import sampling
+
+    ctx = engine.get_context(0)
+    rng = np.random.default_rng(0)
+    W, shots, seed = 64, 5000, 99
+    seg_off = np.array([0, 1, 3, 4], dtype=np.int64)  # instance 1 has two branch rows
+    p = rng.random((4, W)) * np.array([[1.0], [1.0], [-1.0], [1.0]])
+    label_seg = np.array([0, 1, 2, 1, 0], dtype=np.int64)
+    per = np.diff(seg_off)[label_seg]
+    row_off = np.concatenate([[0], np.cumsum(per)]).astype(np.int64)
+    d = lambda a: T.from_numpy(np.ascontiguousarray(a)).cuda()
+    pj, so, ls, ro = d(p), d(seg_off), d(label_seg), d(row_off)
+    cdf = T.empty_like(pj)
+    ctx.check(ctx.lib.qk_sample_cdf(ctx.handle, 3, so.data_ptr(), W, pj.data_ptr(), cdf.data_ptr()), "cdf")
+    full = T.zeros((int(row_off[-1]), W), dtype=T.int32, device="cuda")
+    ctx.check(ctx.lib.qk_sample_counts(ctx.handle, 5, 0, ls.data_ptr(), so.data_ptr(), ro.data_ptr(), W,
+                                       cdf.data_ptr(), shots, seed, full.data_ptr()), "counts")
+    split = T.zeros_like(full)
+    ro2 = d(row_off[2:] - row_off[2])
+    ctx.check(ctx.lib.qk_sample_counts(ctx.handle, 2, 0, ls.data_ptr(), so.data_ptr(), ro.data_ptr(), W,
+                                       cdf.data_ptr(), shots, seed, split.data_ptr()), "counts a")
+    ctx.check(ctx.lib.qk_sample_counts(ctx.handle, 3, 2, ls[2:].data_ptr(), so.data_ptr(), ro2.data_ptr(), W,
+                                       cdf.data_ptr(), shots, seed, split[int(row_off[2]):].data_ptr()), "counts b")
+    full_h, split_h = full.cpu().numpy(), split.cpu().numpy()
+    np.testing.assert_array_equal(full_h, split_h)
+    for l, s in enumerate(label_seg):
+        c = full_h[row_off[l]:row_off[l + 1]].reshape(-1)
+        assert c.sum() == shots
+        ref = sampling.sample_counts(p[seg_off[s]:seg_off[s + 1]].reshape(-1), seed, l, shots)
+        np.testing.assert_array_equal(c, ref)
+
+
+def test_foreign_backend_fragment_rows_per_label(T):
+    """A fragment bound to a non-MI355X backend goes through the reference counts path
+    (run.py:36-58) with one q row per reference label, also where labels share an instance."""
+    import hardwareawareoptimalquantumcircuitcuttingandknitting_amd.quasi_distr as pqd
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.backend import MI355XBackend
+
+    class Foreign:  # duck-typed BackendV2 (exact probabilities as counts)
+        def run(self, circuits, shots=None):
+            return MI355XBackend().run(circuits, shots)
+
+    old, pqd.ACCURACY = pqd.ACCURACY, 0.0
+    try:
+        for case in ("cx", "cx_3cuts", "move_gate"):
+            for factored in (False, True):
+                _, cut = CASES[case]()
+                virt = VirtualCircuit(cut)
+                frags = [f for f in virt.fragment_circuits if len(f)]
+                virt.set_backend(frags[0], Foreign())
+                out, _ = run_virtual_circuit_dense(virt, shots=1000, factored=factored)
+                np.testing.assert_allclose(out.cpu().numpy(), dense.run_dense(cut), atol=1e-10, rtol=0)
+    finally:
+        pqd.ACCURACY = old
