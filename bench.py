@@ -36,6 +36,8 @@ def parse():
                     help="direct knit over all global labels (K = prod n_inst) instead of the "
                          "default rank-factored knit (K = 4^cuts; exact, same result)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="skip the syc 32 1 sweep-only measurement (north_star_sweep)")
     ap.add_argument("--cpu-sample-labels", type=int, default=12)
     return ap.parse_args()
 
@@ -93,6 +95,51 @@ def cpu_baseline(cut, n_labels_sample: int):
                    f"{M}x{Nw}x{L}: {t_total:.1f} s per full knit"),
         "full_knit_s": t_total,
     }
+
+
+def north_star_sweep(steps: int) -> dict:
+    """BASELINE.json north-star target: the batched statevector sweep for syc 32 1 at p=2 on one
+    MI355X against the HBM roofline. Per variant (the reference cut: 0 cuts, 2 instances; the
+    forced 4-cut variant: the full 4^k instance batch) the sweep of every fragment is timed alone
+    with HIP events on the launch stream; ``roofline_frac`` = SURVEY.md §8d algorithmic bytes (one
+    read + write of the complex128 state per fused op per branch job) / time / 8 TB/s, and
+    ``hbm_frac`` the same for the bytes the kernels actually move (modelled)."""
+    import torch
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    out = {}
+    for key in ("syc_32_1_p2", "syc_32_1_p2_forced"):
+        name, n, d, p, var = cutting.BASELINE_CONFIGS[key]
+        _, cut, desc = cutting.config_cut_circuit(name, n, d, p, var)
+        pipe = KnitPipeline(VirtualCircuit(cut), factored=(var == "forced"))
+        for _ in range(2):
+            pipe.sweep()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(steps):
+            pipe.sweep()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / steps
+        tr = pipe.sweep_traffic()
+        counts = pipe.instance_counts()
+        out[key] = {
+            "workload": f"{name} {n} {d} p={p}" + (" (forced cuts)" if var == "forced" else ""),
+            "cuts": desc,
+            "instances_ref": counts["instances_ref"],
+            "branch_jobs": counts["branch_jobs"],
+            "ms_per_sweep": ms,
+            "algorithmic_bytes": tr["algorithmic"],
+            "roofline_frac": tr["algorithmic"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "hbm_bytes": tr["hbm"],
+            "hbm_frac": tr["hbm"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        }
+        del pipe
+        torch.cuda.empty_cache()
+    return out
 
 
 def traffic_per_launch(M, N, K):
@@ -208,8 +255,8 @@ def main():
             "avg_launch_ms": gemm_ms,
         },
         "sweep": {
-            "kernel": "per-program sweep kernels (sweep_codegen + hiprtc) + qk_reduce_labels "
-                      "(all fragments, per step, this rank)",
+            "kernel": "per-program sweep kernels (sweep_codegen + hiprtc; FINAL pass sums each label's "
+                      "branch jobs) (all fragments, per step, this rank)",
             "bound": "hbm (modelled bytes below; fused passes move far fewer than the per-gate "
                      "algorithmic model)",
             "ms_per_step": sweep_ms,
@@ -224,6 +271,8 @@ def main():
             "fp64_valu_frac": traffic["flops"] / (sweep_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
         },
     }
+    if world == 1 and not args.no_north_star:
+        line["north_star_sweep"] = north_star_sweep(args.steps)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(cut, args.cpu_sample_labels)
     print(json.dumps(line), flush=True)

@@ -81,9 +81,15 @@ int qk_module_destroy(qk_module* m) {
     return QK_OK;
 }
 
-int qk_sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* p, int64_t n_jobs,
-                      const double* job_slots, const double* job_sign, void* workspace,
-                      int64_t workspace_bytes, double* pjob) {
+}  // extern "C"
+
+namespace {
+
+// Passes of a compiled program; with label_off the FINAL pass runs one workgroup per (label, tile)
+// and sums the label's branch jobs (signed) before its single store.
+int sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* p, int64_t n_jobs,
+                   const double* job_slots, const double* job_sign, void* workspace, int64_t workspace_bytes,
+                   double* pjob, int64_t n_labels, const int64_t* label_off) {
     if (!ctx) return QK_EARG;
     if (!module || !p || !p->passes || p->n_passes < 1) return jfail(ctx, QK_EARG, "qk_sweep_compiled: empty program");
     if ((int)module->fns.size() != p->n_passes)
@@ -98,7 +104,9 @@ int qk_sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* p,
     if (hipSetDevice(ctx->device) != hipSuccess) return jfail(ctx, QK_EHIP, "qk_sweep_compiled: hipSetDevice");
     for (int ip = 0; ip < p->n_passes; ++ip) {
         const bool sparse_init = ip == 0 && p->n_passes > 1;  // qk_sweep: INIT tile of each job only
-        const int64_t blocks = sparse_init ? n_jobs : (n_jobs << (p->n - QK_TILE_BITS));
+        const bool fin = ip == p->n_passes - 1;
+        const int64_t units = (fin && label_off) ? n_labels : n_jobs;
+        const int64_t blocks = sparse_init ? n_jobs : (units << (p->n - QK_TILE_BITS));
         if (blocks > 0x7fffffff) return jfail(ctx, QK_EARG, "qk_sweep_compiled: too many tiles");
         struct {
             const double* slots;
@@ -106,7 +114,8 @@ int qk_sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* p,
             void* state;
             double* pjob;
             int64_t n_jobs;
-        } args{job_slots, job_sign, workspace, pjob, n_jobs};
+            const int64_t* label_off;
+        } args{job_slots, job_sign, workspace, pjob, n_jobs, fin ? label_off : nullptr};
         size_t size = sizeof(args);
         void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                        HIP_LAUNCH_PARAM_END};
@@ -115,6 +124,29 @@ int qk_sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* p,
         if (e != hipSuccess) return jfail(ctx, QK_EHIP, std::string("qk_sweep_compiled: ") + hipGetErrorString(e));
     }
     return QK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qk_sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* p, int64_t n_jobs,
+                      const double* job_slots, const double* job_sign, void* workspace,
+                      int64_t workspace_bytes, double* pjob) {
+    return sweep_compiled(ctx, module, p, n_jobs, job_slots, job_sign, workspace, workspace_bytes, pjob, 0,
+                          nullptr);
+}
+
+int qk_sweep_compiled_labels(qk_ctx* ctx, const qk_module* module, const qk_program* p, int64_t n_jobs,
+                             const double* job_slots, const double* job_sign, int64_t n_labels,
+                             const int64_t* label_offsets, void* workspace, int64_t workspace_bytes, double* q) {
+    if (!ctx) return QK_EARG;
+    if (n_labels < 1 || !label_offsets)
+        return jfail(ctx, QK_EARG, "qk_sweep_compiled_labels: need n_labels >= 1 and label offsets");
+    if ((n_labels << (p ? (p->n > QK_TILE_BITS ? p->n - QK_TILE_BITS : 0) : 0)) > 0x7fffffff)
+        return jfail(ctx, QK_EARG, "qk_sweep_compiled_labels: too many tiles");
+    return sweep_compiled(ctx, module, p, n_jobs, job_slots, job_sign, workspace, workspace_bytes, q, n_labels,
+                          label_offsets);
 }
 
 }  // extern "C"

@@ -195,6 +195,29 @@ def sweep_jobs(ctx: Context, dprog: DeviceProgram, slot_t, sign_t, n_jobs: int, 
     return pjob, workspace
 
 
+def sweep_labels(ctx: Context, dprog: DeviceProgram, slot_t, sign_t, n_jobs: int, off_t, n_labels: int,
+                 q=None, workspace=None):
+    """``qk_sweep_compiled_labels``: per-label signed-folded distributions ``[n_labels, 2^m]``
+    straight from the sweep (the FINAL pass sums each label's branch jobs; no per-job rows and
+    no ``qk_reduce_labels``). Compiled (SPLIT) programs only."""
+    T = torch()
+    if dprog.module is None:
+        raise ValueError("sweep_labels needs a compiled (SPLIT) program")
+    dev = T.device("cuda", ctx.device)
+    if q is None:
+        q = T.empty((n_labels, 1 << dprog.enc.m), dtype=T.float64, device=dev)
+    need = ctypes.c_int64()
+    ctx.check(ctx.lib.qk_sweep_workspace_bytes(ctypes.byref(dprog.struct), n_jobs, ctypes.byref(need)),
+              "qk_sweep_workspace_bytes")
+    if workspace is None or workspace.numel() < need.value:
+        workspace = T.empty(max(need.value, 1), dtype=T.uint8, device=dev)
+    ctx.check(ctx.lib.qk_sweep_compiled_labels(ctx.handle, dprog.module, ctypes.byref(dprog.struct), n_jobs,
+                                               slot_t.data_ptr(), sign_t.data_ptr(), n_labels, off_t.data_ptr(),
+                                               workspace.data_ptr(), need.value, q.data_ptr()),
+              "qk_sweep_compiled_labels")
+    return q, workspace
+
+
 def reduce_labels(ctx: Context, pjob, off_t, n_labels: int, q=None):
     T = torch()
     width = pjob.shape[1]
@@ -416,6 +439,8 @@ def sweep_fragment(ctx: Context, fs: FragmentState, label_range=None):
     sub = JobTable(jobs.slot_mats[j0:j1], jobs.sign[j0:j1], jobs.label_offsets[lo : hi + 1] - j0,
                    jobs.branch_bits[j0:j1])
     slot_t, sign_t, off_t = jobs_to_device(sub, ctx.device)
+    if sub.n_jobs != hi - lo and fs.dprog.module is not None:  # branching, compiled: fused FINAL
+        return sweep_labels(ctx, fs.dprog, slot_t, sign_t, sub.n_jobs, off_t, hi - lo)[0]
     pjob, _ = sweep_jobs(ctx, fs.dprog, slot_t, sign_t, sub.n_jobs)
     if sub.n_jobs == hi - lo:  # no branching: jobs are labels
         return pjob

@@ -110,6 +110,13 @@ class HipBackend:
     def sweep(self, fs, slot, sign, n_jobs, pjob, ws):
         engine.sweep_jobs(self.ctx, fs.dprog, slot, sign, n_jobs, pjob=pjob, workspace=ws)
 
+    def fuses_labels(self, fs) -> bool:
+        """Whether the sweep of ``fs`` can emit per-label rows itself (compiled program)."""
+        return fs.dprog is not None and fs.dprog.module is not None
+
+    def sweep_labels(self, fs, slot, sign, n_jobs, off, n_labels, q, ws):
+        engine.sweep_labels(self.ctx, fs.dprog, slot, sign, n_jobs, off, n_labels, q=q, workspace=ws)
+
     def reduce_labels(self, pjob, off, n_labels, q):
         return engine.reduce_labels(self.ctx, pjob, off, n_labels, q=q)
 
@@ -191,8 +198,12 @@ class KnitPipeline:
             rows = -(-nl // self.world) if self.mode == "gather" else max(n_local, 1)
             alloc = be.zeros if self.mode == "gather" else be.empty
             branching = n_jobs != n_local
+            # branching + compiled program: the FINAL pass writes the label rows (no pjob, no reduce)
+            fused = branching and n_jobs > 0 and getattr(be, "fuses_labels", lambda _: False)(fs)
             self.sweeps.append(dict(lo=lo, n_local=n_local, slot=slot_t, sign=sign_t, off=off_t, n_jobs=n_jobs,
-                                    pjob=(be.empty((max(n_jobs, 1), width), T.float64) if branching
+                                    fused=fused,
+                                    pjob=(None if fused else
+                                          be.empty((max(n_jobs, 1), width), T.float64) if branching
                                           else alloc((max(rows, 1), width), T.float64)),
                                     q=alloc((max(rows, 1), width), T.float64) if branching else None,
                                     ws=be.empty((max(need, 1),), T.uint8)))
@@ -269,12 +280,16 @@ class KnitPipeline:
                 ones += 1.0
                 qs[i] = ones
                 continue
-            if sw["n_jobs"]:
-                be.sweep(fs, sw["slot"], sw["sign"], sw["n_jobs"], sw["pjob"], sw["ws"])
-            if sw["q"] is not None:
-                q = be.reduce_labels(sw["pjob"], sw["off"], sw["n_local"], sw["q"])
+            if sw["fused"]:
+                be.sweep_labels(fs, sw["slot"], sw["sign"], sw["n_jobs"], sw["off"], sw["n_local"], sw["q"], sw["ws"])
+                q = sw["q"]
             else:
-                q = sw["pjob"]
+                if sw["n_jobs"]:
+                    be.sweep(fs, sw["slot"], sw["sign"], sw["n_jobs"], sw["pjob"], sw["ws"])
+                if sw["q"] is not None:
+                    q = be.reduce_labels(sw["pjob"], sw["off"], sw["n_local"], sw["q"])
+                else:
+                    q = sw["pjob"]
             if self.mode == "gather":
                 work, qs[i] = self._exchange(i, q)
                 pending.append(work)
@@ -400,9 +415,12 @@ class KnitPipeline:
                 per_job = 2 * tile + out
             else:
                 per_job = 2 * tile + S + (P - 3) * 2 * S + S + out
-            hbm += J * per_job
-            if sw["q"] is not None:
-                hbm += J * out + sw["n_local"] * out
+            if sw.get("fused"):  # FINAL pass sums a label's jobs: one row per label, no reduction
+                hbm += J * (per_job - out) + sw["n_local"] * out
+            else:
+                hbm += J * per_job
+                if sw["q"] is not None:
+                    hbm += J * out + sw["n_local"] * out
             alg += J * len(fs.prog.ops) * 32 * (1 << fs.prog.n)
             flops += J * _sweep_flops_per_job(enc)
         return {"hbm": hbm, "algorithmic": alg, "flops": flops}

@@ -172,19 +172,32 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str) -> list:
     e = _Emitter()
     e(f'extern "C" __global__ __launch_bounds__({NT}) void {name}(', 0)
     e("const double* __restrict__ job_slots, const double* __restrict__ job_sign,", 2)
-    e("double2* __restrict__ state, double* __restrict__ pjob, long long n_jobs) {", 2)
+    e("double2* __restrict__ state, double* __restrict__ pjob, long long n_jobs,", 2)
+    e("const long long* __restrict__ label_off) {", 2)
     e("using namespace qk_sweep_ops;")
     e("__shared__ double2 lds[4096];")
     e("const unsigned tid = threadIdx.x;")
-    e(f"const long long job = (long long)(blockIdx.x >> {tpj_log});")
+    # FINAL: grp is a label when label_off is given (its branch jobs are summed in registers,
+    # qk_sweep_compiled_labels), else a job
+    e(f"const long long grp = (long long)(blockIdx.x >> {tpj_log});")
     if tpj_log:
         e(f"const unsigned long long tj = blockIdx.x & {(1 << tpj_log) - 1}u;")
         e(f"const unsigned long long tbase = {_deposit('tj', list(range(len(outside))), outside)};")
     else:
         e("const unsigned long long tbase = 0ull;")
     e(f"const unsigned long long lo = {_deposit('(unsigned long long)tid', list(range(8)), bitpos[:8])};")
+    e("(void)n_jobs; (void)job_slots; (void)lo; (void)label_off;")
+    keep = [i for i in range(PER) if not ((NT * i) & traced)]
+    if final:
+        e("long long j0 = grp, j1 = grp + 1;")
+        e("if (label_off) { j0 = label_off[grp]; j1 = label_off[grp + 1]; }")
+        for i in keep:
+            e(f"double out{i} = 0.0;")
+        e("for (long long job = j0; job < j1; ++job) {")
+    else:
+        e("const long long job = grp;")
     e(f"double2* st = state + job * {1 << n}ll;")
-    e("(void)n_jobs; (void)job_slots; (void)st; (void)lo;")
+    e("(void)st;")
     zero_tile = init and not init_sparse and tpj_log > 0
     if init:
         e("lds[swz(tid)] = make_double2((tid == 0 && tbase == 0ull) ? 1.0 : 0.0, 0.0);")
@@ -239,17 +252,21 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str) -> list:
             if sub == 0:
                 break
         e(f"const double sgn = job_sign[job];")
-        for i in range(PER):
-            if (NT * i) & traced:
-                continue
-            cond = traced & (NT - 1)
+        cond = traced & (NT - 1)
+        for i in keep:
             e(f"if (!(tid & {cond}u)) {{" if cond else "{")
             e("double acc = 0.0;", 2)
             for sb in subs:
                 e(f"{{ const double2 z = lds[swz((tid + {NT * i}) | {sb}u)]; "
                   f"acc = fma(z.x, z.x, fma(z.y, z.y, acc)); }}", 2)
+            e(f"out{i} += sgn * acc;", 2)
+            e("}")
+        e("__syncthreads();  // the next branch job of the label reuses the tile")
+        e("}")
+        for i in keep:
+            e(f"if (!(tid & {cond}u)) {{" if cond else "{")
             e(f"const unsigned long long x = (tbase | lo | 0x{hi[i]:x}ull) & 0x{mmask:x}ull;", 2)
-            e(f"pjob[(job << {m}) + (long long)x] = sgn * acc;", 2)
+            e(f"pjob[(grp << {m}) + (long long)x] = out{i};", 2)
             e("}")
     else:
         for i in range(PER):

@@ -121,6 +121,13 @@ int qk_sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* pr
                       const double* job_slots, const double* job_sign, void* workspace,
                       int64_t workspace_bytes, double* pjob);
 
+/* qk_sweep_compiled fused with qk_reduce_labels: the FINAL pass runs per (label, tile) and sums the
+ * label's branch jobs [label_offsets[l], label_offsets[l+1]) (DEVICE, n_labels+1) in registers, so
+ * q[l][x] = sum_j sign_j P_j(x) is stored once and no per-job rows exist. */
+int qk_sweep_compiled_labels(qk_ctx* ctx, const qk_module* module, const qk_program* prog, int64_t n_jobs,
+                             const double* job_slots, const double* job_sign, int64_t n_labels,
+                             const int64_t* label_offsets, void* workspace, int64_t workspace_bytes, double* q);
+
 /* q[l][x] = sum_{j in [offsets[l], offsets[l+1])} pjob[j][x]   (offsets: DEVICE, n_labels+1) */
 int qk_reduce_labels(qk_ctx* ctx, int64_t n_labels, const int64_t* offsets, int64_t width,
                      const double* pjob, double* q);
