@@ -195,26 +195,49 @@ def sweep_jobs(ctx: Context, dprog: DeviceProgram, slot_t, sign_t, n_jobs: int, 
     return pjob, workspace
 
 
+def label_chunks(offsets: np.ndarray, max_jobs: int) -> list:
+    """Consecutive label ranges of at most ``max_jobs`` branch jobs each (a label is never split;
+    one with more jobs is a chunk of its own): ``[(l0, l1, j0, j1), ...]``."""
+    n = len(offsets) - 1
+    out, l0 = [], 0
+    while l0 < n:
+        l1 = l0 + 1
+        while l1 < n and offsets[l1 + 1] - offsets[l0] <= max_jobs:
+            l1 += 1
+        out.append((l0, l1, int(offsets[l0]), int(offsets[l1])))
+        l0 = l1
+    return out
+
+
 def sweep_labels(ctx: Context, dprog: DeviceProgram, slot_t, sign_t, n_jobs: int, off_t, n_labels: int,
-                 q=None, workspace=None):
+                 q=None, workspace=None, chunks=None):
     """``qk_sweep_compiled_labels``: per-label signed-folded distributions ``[n_labels, 2^m]``
     straight from the sweep (the FINAL pass sums each label's branch jobs; no per-job rows and
-    no ``qk_reduce_labels``). Compiled (SPLIT) programs only."""
+    no ``qk_reduce_labels``). Compiled (SPLIT) programs only.
+
+    ``chunks`` (``[(l0, l1, j0, j1, chunk_offsets_device), ...]``, :func:`label_chunks`) runs
+    the passes chunk by chunk through one workspace of the largest chunk's size: the states a
+    pass writes and the next reads then stay in the 256 MiB Infinity Cache instead of HBM."""
     T = torch()
     if dprog.module is None:
         raise ValueError("sweep_labels needs a compiled (SPLIT) program")
     dev = T.device("cuda", ctx.device)
+    width = 1 << dprog.enc.m
     if q is None:
-        q = T.empty((n_labels, 1 << dprog.enc.m), dtype=T.float64, device=dev)
+        q = T.empty((n_labels, width), dtype=T.float64, device=dev)
+    if chunks is None:
+        chunks = [(0, n_labels, 0, n_jobs, off_t)]
     need = ctypes.c_int64()
-    ctx.check(ctx.lib.qk_sweep_workspace_bytes(ctypes.byref(dprog.struct), n_jobs, ctypes.byref(need)),
-              "qk_sweep_workspace_bytes")
+    ctx.check(ctx.lib.qk_sweep_workspace_bytes(ctypes.byref(dprog.struct), max(c[3] - c[2] for c in chunks),
+                                               ctypes.byref(need)), "qk_sweep_workspace_bytes")
     if workspace is None or workspace.numel() < need.value:
         workspace = T.empty(max(need.value, 1), dtype=T.uint8, device=dev)
-    ctx.check(ctx.lib.qk_sweep_compiled_labels(ctx.handle, dprog.module, ctypes.byref(dprog.struct), n_jobs,
-                                               slot_t.data_ptr(), sign_t.data_ptr(), n_labels, off_t.data_ptr(),
-                                               workspace.data_ptr(), need.value, q.data_ptr()),
-              "qk_sweep_compiled_labels")
+    slot_row = slot_t[0].numel() * 8 if (dprog.enc.n_slots and slot_t.dim() == 2) else 0
+    for l0, l1, j0, j1, oc in chunks:
+        ctx.check(ctx.lib.qk_sweep_compiled_labels(ctx.handle, dprog.module, ctypes.byref(dprog.struct), j1 - j0,
+                                                   slot_t.data_ptr() + j0 * slot_row, sign_t.data_ptr() + 8 * j0,
+                                                   l1 - l0, oc.data_ptr(), workspace.data_ptr(), need.value,
+                                                   q.data_ptr() + 8 * width * l0), "qk_sweep_compiled_labels")
     return q, workspace
 
 

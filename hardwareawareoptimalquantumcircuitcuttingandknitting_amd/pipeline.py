@@ -28,6 +28,7 @@ collective then assembles the reconstruction:
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -110,12 +111,16 @@ class HipBackend:
     def sweep(self, fs, slot, sign, n_jobs, pjob, ws):
         engine.sweep_jobs(self.ctx, fs.dprog, slot, sign, n_jobs, pjob=pjob, workspace=ws)
 
+    def bind(self):
+        """Point the qk context at torch's current stream (a forked or a graph-capture stream)."""
+        self.ctx.bind_stream()
+
     def fuses_labels(self, fs) -> bool:
         """Whether the sweep of ``fs`` can emit per-label rows itself (compiled program)."""
         return fs.dprog is not None and fs.dprog.module is not None
 
-    def sweep_labels(self, fs, slot, sign, n_jobs, off, n_labels, q, ws):
-        engine.sweep_labels(self.ctx, fs.dprog, slot, sign, n_jobs, off, n_labels, q=q, workspace=ws)
+    def sweep_labels(self, fs, slot, sign, n_jobs, off, n_labels, q, ws, chunks=None):
+        engine.sweep_labels(self.ctx, fs.dprog, slot, sign, n_jobs, off, n_labels, q=q, workspace=ws, chunks=chunks)
 
     def reduce_labels(self, pjob, off, n_labels, q):
         return engine.reduce_labels(self.ctx, pjob, off, n_labels, q=q)
@@ -135,8 +140,13 @@ class HipBackend:
 
 class KnitPipeline:
     def __init__(self, virt, device: int = 0, factored: bool = False, rank: int = 0, world: int = 1,
-                 mode: str | None = None, group=None, backend=None):
+                 mode: str | None = None, group=None, backend=None, chunk_jobs: int | None = None):
         self.be = backend if backend is not None else HipBackend(device)
+        # branch jobs per sweep chunk of a fused (compiled) fragment; 0 = the whole fragment at once
+        self.chunk_jobs = int(os.environ.get("QKNIT_SWEEP_CHUNK_JOBS", "0")) if chunk_jobs is None else chunk_jobs
+        self.fork = False  # single mode: sweep each fragment on its own stream (set by capture_sweep)
+        self._streams = []
+        self._sweep_graph = None
         self.T = engine.torch()
         self.virt = virt
         self.rank, self.world, self.group = rank, world, group
@@ -200,8 +210,14 @@ class KnitPipeline:
             branching = n_jobs != n_local
             # branching + compiled program: the FINAL pass writes the label rows (no pjob, no reduce)
             fused = branching and n_jobs > 0 and getattr(be, "fuses_labels", lambda _: False)(fs)
+            chunks = None
+            if fused and self.chunk_jobs and n_jobs > self.chunk_jobs:
+                offs = sub.label_offsets
+                chunks = [(l0, l1, j0, j1, be.to_device(offs[l0:l1 + 1] - j0))
+                          for l0, l1, j0, j1 in engine.label_chunks(offs, self.chunk_jobs)]
+                need = be.workspace_bytes(fs, max(c[3] - c[2] for c in chunks))
             self.sweeps.append(dict(lo=lo, n_local=n_local, slot=slot_t, sign=sign_t, off=off_t, n_jobs=n_jobs,
-                                    fused=fused,
+                                    fused=fused, chunks=chunks,
                                     pjob=(None if fused else
                                           be.empty((max(n_jobs, 1), width), T.float64) if branching
                                           else alloc((max(rows, 1), width), T.float64)),
@@ -272,32 +288,72 @@ class KnitPipeline:
         T, be = self.T, self.be
         qs = [None] * len(self.frags)
         pending = []
+        fork = self.fork and self.mode == "single"
+        main = T.cuda.current_stream() if fork else None
         # the A side (output rows) first, so its exchange overlaps the other sweeps
-        for i in sorted(range(len(self.frags)), key=lambda i: self.order.index(i)):
+        for k, i in enumerate(sorted(range(len(self.frags)), key=lambda i: self.order.index(i))):
             fs, sw = self.frags[i], self.sweeps[i]
             if sw is None:
                 ones = be.zeros((fs.n_rows, 1), T.float64)
                 ones += 1.0
                 qs[i] = ones
                 continue
-            if sw["fused"]:
-                be.sweep_labels(fs, sw["slot"], sw["sign"], sw["n_jobs"], sw["off"], sw["n_local"], sw["q"], sw["ws"])
-                q = sw["q"]
+            if fork:  # fragments are independent: one stream each, joined below
+                while len(self._streams) <= k:
+                    self._streams.append(T.cuda.Stream(device=main.device))
+                s = self._streams[k]
+                s.wait_stream(main)
+                with T.cuda.stream(s):
+                    be.bind()
+                    q = self._sweep_fragment(fs, sw)
             else:
-                if sw["n_jobs"]:
-                    be.sweep(fs, sw["slot"], sw["sign"], sw["n_jobs"], sw["pjob"], sw["ws"])
-                if sw["q"] is not None:
-                    q = be.reduce_labels(sw["pjob"], sw["off"], sw["n_local"], sw["q"])
-                else:
-                    q = sw["pjob"]
+                q = self._sweep_fragment(fs, sw)
             if self.mode == "gather":
                 work, qs[i] = self._exchange(i, q)
                 pending.append(work)
             else:
                 qs[i] = q[: sw["n_local"]]
+        if fork:
+            for s in self._streams:
+                main.wait_stream(s)
+            be.bind()
         for work in pending:
             work.wait()
         return qs
+
+    def _sweep_fragment(self, fs, sw):
+        be = self.be
+        if sw["fused"]:
+            be.sweep_labels(fs, sw["slot"], sw["sign"], sw["n_jobs"], sw["off"], sw["n_local"], sw["q"], sw["ws"],
+                            chunks=sw["chunks"])
+            return sw["q"]
+        if sw["n_jobs"]:
+            be.sweep(fs, sw["slot"], sw["sign"], sw["n_jobs"], sw["pjob"], sw["ws"])
+        if sw["q"] is not None:
+            return be.reduce_labels(sw["pjob"], sw["off"], sw["n_local"], sw["q"])
+        return sw["pjob"]
+
+    def capture_sweep(self):
+        """Record one step's sweep — every pass launch of every fragment, the fragments on forked
+        streams — as one HIP graph (torch.cuda.CUDAGraph); :meth:`replay_sweep` re-issues it with
+        a single launch call. Single mode only (gather mode's collectives stay eager)."""
+        T = self.T
+        if self.mode != "single":
+            raise ValueError("sweep graphs are for single-GPU pipelines")
+        self.fork = True
+        self.sweep()  # outside the capture: streams, lazy allocations
+        T.cuda.synchronize()
+        g = T.cuda.CUDAGraph()
+        with T.cuda.graph(g):
+            self.be.bind()
+            qs = self.sweep()
+        self.be.bind()
+        self._sweep_graph, self._graph_qs = g, qs
+        return qs
+
+    def replay_sweep(self) -> list:
+        self._sweep_graph.replay()
+        return self._graph_qs
 
     def _exchange(self, i, qpad):
         """Start fragment i's collective on its zero-padded shard ``qpad`` [per, width]."""

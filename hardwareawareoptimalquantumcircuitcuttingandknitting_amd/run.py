@@ -73,6 +73,9 @@ def run_virtual_circuit_dense(virt: VirtualCircuit, shots: int = 20000, *, devic
     """Sweep (or shot-sample, ``sample=True``) + knit; returns ``(dense fp64 tensor [2^N] on
     device, RunTimeInfo)``."""
     ctx = engine.get_context(device)
+    # The factored knit folds labels whose side programs coincide into one operand row; sampled
+    # labels differ in their shots even then, so sampling knits directly over the labels.
+    factored = factored and not sample
     log.info("Running virtualizer with %d %s fragments and %d vgates...",
              len(virt.fragment_circuits),
              tuple(len(f) for f in virt.fragment_circuits), len(virt.vgate_instructions))

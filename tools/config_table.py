@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Per-config results for BASELINE.md §5: every BASELINE.json shape on one MI355X.
+
+  python tools/config_table.py [--steps 5] [--out profiles/r01_configs.json]
+
+Per config: a KnitPipeline (factored knit where there are cuts, direct otherwise) is planned,
+warmed up and stepped; HIP events on the launch stream time the sweep and the contraction, wall
+time the whole step. Reported: reference instances/s, sweep / knit / full-knit ms, the sweep's
+modelled HBM fraction, the contraction's MFMA fraction (2 M N K / time / 78.6
+TF/s) or, for K = 1 outer products, its HBM-write fraction, and parity: small configs against
+the CPU oracle (max |delta|, with the oracle's own time), 32-qubit ones by size-independent
+properties (sum to 1, no entry below -1e-13).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM = 8000.0
+MFMA = 78.6
+CONFIGS = ["bv_5_1_p2", "hwe_16_1_p2", "hwe_16_1_p3", "qft_16_1_p3", "syc_32_1_p2", "syc_32_1_p2_forced",
+           "syc_32_5_p2"]
+
+
+def run(key, steps):
+    import numpy as np
+    import torch
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    name, n, d, p, var = cutting.BASELINE_CONFIGS[key]
+    _, cut, desc = cutting.config_cut_circuit(name, n, d, p, var)
+    virt = VirtualCircuit(cut)
+    factored = len(virt.vgate_instructions) > 0
+    pipe = KnitPipeline(virt, factored=factored)
+    for _ in range(2):
+        res = pipe.step()
+    torch.cuda.synchronize()
+    pipe.record_events = True
+    pipe.events.clear()
+    pipe.sweep_events.clear()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = pipe.step()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    knit_ms = sum(s.elapsed_time(e) for s, e in pipe.events) / len(pipe.events)
+    sweep_ms = sum(s.elapsed_time(e) for s, e in pipe.sweep_events) / len(pipe.sweep_events)
+    M, N, K = pipe.gemm_shape()
+    tr = pipe.sweep_traffic()
+    counts = pipe.instance_counts()
+    row = {
+        "config": key, "workload": f"{name} {n} {d} p={p}" + (" (forced cuts)" if var == "forced" else ""),
+        "cuts": desc, "instances_ref": counts["instances_ref"], "branch_jobs": counts["branch_jobs"],
+        "knit": "factored" if factored else "direct", "gemm_mnk": [M, N, K],
+        "instances_per_s": counts["instances_ref"] / wall, "full_knit_ms": wall * 1e3,
+        "sweep_ms": sweep_ms, "knit_ms": knit_ms,
+        "sweep_hbm_frac": tr["hbm"] / (sweep_ms * 1e-3) / 1e9 / HBM if sweep_ms > 0 else None,
+    }
+    if K > 1:
+        row["knit_mfma_frac"] = 2.0 * M * N * K / (knit_ms * 1e-3) / 1e12 / MFMA
+    else:
+        row["knit_hbm_write_frac"] = 8.0 * M * N / (knit_ms * 1e-3) / 1e9 / HBM
+    if pipe.N <= 20:
+        from oracle import dense
+
+        t1 = time.perf_counter()
+        ref = dense.run_dense(cut)
+        row["cpu_oracle_s"] = time.perf_counter() - t1
+        row["parity_max_abs"] = float(np.abs(res.cpu().numpy() - ref).max())
+    else:
+        row["sum_minus_1"] = float(res.sum()) - 1.0
+        row["min_entry"] = float(res.min())
+    del pipe, res
+    torch.cuda.empty_cache()
+    return row
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--configs", nargs="*", default=CONFIGS)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    rows = []
+    for key in args.configs:
+        row = run(key, args.steps)
+        print(json.dumps(row), flush=True)
+        rows.append(row)
+    if args.out:
+        json.dump(rows, open(args.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

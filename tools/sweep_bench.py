@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
-"""Time the batched sweep alone (per fragment, per pass launch) for a BASELINE workload.
+"""Time the batched sweep alone for a BASELINE workload, per sweep-chunk size (interleaved rounds).
 
-  python tools/sweep_bench.py [--workload syc_32_5_p2] [--reps 5] [--no-dedup]
+  python tools/sweep_bench.py [--workload syc_32_5_p2] [--reps 5] [--chunks 0 512 256 128]
+
+Each chunk size is a KnitPipeline (factored, basis-reduced sweep) whose fused fragments run
+their passes chunk by chunk through one workspace (engine.label_chunks; 0 = no chunking).
 """
 import argparse
 import os
 import sys
-import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -15,35 +17,34 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="syc_32_5_p2")
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--no-dedup", action="store_true")
+    ap.add_argument("--chunks", type=int, nargs="*", default=[0, 640, 320, 256, 160, 128, 64])
     args = ap.parse_args()
     import torch
 
-    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting, engine
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
 
     name, n, d, p, var = cutting.BASELINE_CONFIGS[args.workload]
     _, cut, _ = cutting.config_cut_circuit(name, n, d, p, var)
-    virt = VirtualCircuit(cut)
-    ctx = engine.get_context(0)
-    frags = engine.prepare_fragments(virt, 0, dedup=not args.no_dedup, basis=not args.no_dedup)
-    tabs = []
-    for fs in frags:
-        slot_t, sign_t, off_t = engine.jobs_to_device(fs.jobs, 0)
-        pjob, ws = engine.sweep_jobs(ctx, fs.dprog, slot_t, sign_t, fs.jobs.n_jobs)
-        tabs.append((fs, slot_t, sign_t, pjob, ws))
+    pipes = {c: KnitPipeline(VirtualCircuit(cut), factored=True, chunk_jobs=c) for c in args.chunks}
+    ref = [q.clone() for q in pipes[args.chunks[0]].sweep()]
+    for c, pipe in pipes.items():
+        got = pipe.sweep()
+        assert all(torch.equal(a, b) for a, b in zip(got, ref)), f"chunk {c}: sweep differs"
     torch.cuda.synchronize()
+    times = {c: [] for c in pipes}
     for rep in range(args.reps):
-        t0 = time.perf_counter()
-        for fs, slot_t, sign_t, pjob, ws in tabs:
-            engine.sweep_jobs(ctx, fs.dprog, slot_t, sign_t, fs.jobs.n_jobs, pjob=pjob, workspace=ws)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        jobs = sum(f[0].jobs.n_jobs for f in tabs)
-        print(f"rep {rep}: sweep {dt * 1e3:.3f} ms for {jobs} jobs "
-              f"({sum(len(f[0].labels) for f in tabs)} reference instances)", flush=True)
-    for fs, *_ in tabs:
-        enc = fs.dprog.enc
-        print(f"{fs.fragment.name}: n={enc.n} passes={len(enc.passes)} groups={len(enc.groups)} ops={len(enc.ops)}")
+        for c, pipe in pipes.items():
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            pipe.sweep()
+            e.record()
+            torch.cuda.synchronize()
+            times[c].append(s.elapsed_time(e))
+    jobs = pipes[args.chunks[0]].instance_counts()["branch_jobs"]
+    for c, t in times.items():
+        t = sorted(t)
+        print(f"chunk_jobs {c:5d}: sweep median {t[len(t) // 2]:.3f} ms  min {t[0]:.3f} ms  ({jobs} jobs)", flush=True)
 
 
 if __name__ == "__main__":
