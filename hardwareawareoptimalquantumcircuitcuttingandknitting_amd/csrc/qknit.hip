@@ -918,6 +918,68 @@ __global__ __launch_bounds__(256, 2) void qk_gemm_glds_kernel(GemmArgs g) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// small-K contraction (K <= 8): output-write bound — syc 32 1's uncut knit is a K = 1 outer
+// product that writes 34 GB from 1 MB of operands. A workgroup takes one output row at a time:
+// the row's K values of A are read once (wave-uniform), each lane forms two adjacent outputs from
+// 16-B reads of the B rows (L2-resident) and writes them with one 16-B nontemporal store.
+// ------------------------------------------------------------------------------------------
+constexpr int SK_MAX = 8;
+#ifndef QK_SK_U
+#define QK_SK_U 4
+#endif
+constexpr int SK_U = QK_SK_U;  // 512-output chunks per lane iteration
+
+__global__ __launch_bounds__(256) void qk_gemm_smallk_kernel(GemmArgs g) {
+    const int K = (int)g.K;
+    for (int64_t row = blockIdx.x; row < g.M; row += gridDim.x) {
+        double a[SK_MAX];
+#pragma unroll
+        for (int k = 0; k < SK_MAX; ++k) a[k] = k < K ? g.A[k * g.lda + row] : 0.0;
+        const int64_t base = g.keyA ? g.keyA[row] : row * g.strideA;
+        double* o = g.out + base;
+        if ((base & 1) == 0) {  // 16-B aligned row start (wave-uniform)
+            // SK_U chunks of 512 outputs per iteration: their B loads are all in flight before
+            // the first store issues
+            int64_t j0 = 2 * (int64_t)threadIdx.x;
+            for (; j0 + 512 * (SK_U - 1) < g.N; j0 += 512 * SK_U) {
+                d2_t acc[SK_U];
+#pragma unroll
+                for (int u = 0; u < SK_U; ++u) acc[u] = (d2_t){0.0, 0.0};
+#pragma unroll
+                for (int k = 0; k < SK_MAX; ++k) {
+                    if (k < K) {
+#pragma unroll
+                        for (int u = 0; u < SK_U; ++u) {
+                            const d2_t b = *reinterpret_cast<const d2_t*>(g.B + k * g.ldb + j0 + 512 * u);
+                            acc[u].x = fma(a[k], b.x, acc[u].x);
+                            acc[u].y = fma(a[k], b.y, acc[u].y);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < SK_U; ++u)
+                    __builtin_nontemporal_store(acc[u], reinterpret_cast<d2_t*>(o + j0 + 512 * u));
+            }
+            for (int64_t j = j0; j < g.N; j += 512) {
+                d2_t acc = {0.0, 0.0};
+                for (int k = 0; k < K; ++k) {
+                    const d2_t b = *reinterpret_cast<const d2_t*>(g.B + k * g.ldb + j);
+                    acc.x = fma(a[k], b.x, acc.x);
+                    acc.y = fma(a[k], b.y, acc.y);
+                }
+                __builtin_nontemporal_store(acc, reinterpret_cast<d2_t*>(o + j));
+            }
+        } else {
+            for (int64_t j = threadIdx.x; j < g.N; j += 256) {
+                double acc = 0.0;
+                for (int k = 0; k < K; ++k) acc = fma(a[k], g.B[k * g.ldb + j], acc);
+                __builtin_nontemporal_store(acc, o + j);
+            }
+        }
+    }
+}
+
 __global__ void qk_khatri_rao_kernel(int64_t K, int64_t M, int64_t N, const double* __restrict__ A,
                                      int64_t lda, const double* __restrict__ B, int64_t ldb,
                                      double* __restrict__ out) {
@@ -1094,6 +1156,15 @@ int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A,
     GemmArgs g{M, N, K, A, lda, B, ldb, keyA, strideA, keyB, strideB, out, beta, tm, tn};
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) == 0 &&
                            (lda % 2) == 0 && (ldb % 2) == 0;
+    if (K >= 1 && K <= SK_MAX && !beta && !keyB && strideB == 1 && N % 2 == 0 && aligned16 &&
+        (reinterpret_cast<uintptr_t>(out) & 15) == 0 && M * N >= (int64_t(1) << 16)) {
+        int cus = 0;
+        QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        const int64_t G = M < (int64_t)cus * 8 ? M : (int64_t)cus * 8;
+        hipLaunchKernelGGL(qk_gemm_smallk_kernel, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
+        QK_HIP(ctx, hipGetLastError());
+        return QK_OK;
+    }
     if (QK_GEMM_GLDS && !beta && M % GT == 0 && N % GT == 0 && K % G2K == 0 && K > 0 && aligned16) {
         int cus = 0;
         QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));

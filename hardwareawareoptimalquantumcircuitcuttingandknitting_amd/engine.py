@@ -399,11 +399,13 @@ class FragmentState:
 
 
 def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = True,
-                      basis: bool = False) -> list[FragmentState]:
+                      basis: bool = False, jit: bool | None = None) -> list[FragmentState]:
     """Compile every fragment, dedup its instances and expand them into branch jobs.
 
     ``basis=True`` (factored knit only) additionally sweeps a spanning set of instances
-    (``basis_reduce``); the knit transform folds the expansion back in."""
+    (``basis_reduce``); the knit transform folds the expansion back in. ``jit``: per-program
+    sweep kernels for SPLIT programs — None: only for large sweeps (``_worth_compiling``),
+    True: for every SPLIT program of at most 400 ops, False: never (interpreter kernel)."""
     circ = virt.circuit
     cl = clbit_indexer(circ)
     vg = virt.vgate_instructions
@@ -423,7 +425,8 @@ def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = 
         # run.py:49-58 drops a fragment whose get_counts() raises, i.e. when some instance of
         # it measures nothing at all (no data measurement and no config measurement).
         dropped = prog.m == 0 and _some_label_unmeasured(prog, labels)
-        dp = DeviceProgram.upload(prog, device, jit=_worth_compiling(prog, jobs)) if (upload and not dropped) else None
+        want = _worth_compiling(prog, jobs) if jit is None else (jit and len(prog.ops) <= 400)
+        dp = DeviceProgram.upload(prog, device, jit=want) if (upload and not dropped) else None
         out.append(FragmentState(frag, labels, prog, dp, jobs, touches, dropped, uidx, unique,
                                  red.labels if red is not None else None,
                                  red.expand if red is not None else None))

@@ -87,8 +87,8 @@ class HipBackend:
         self.dev = self.T.device("cuda", device)
         self.ctx = engine.get_context(device)
 
-    def prepare_fragments(self, virt, basis: bool = False):
-        return engine.prepare_fragments(virt, self.device, basis=basis)
+    def prepare_fragments(self, virt, basis: bool = False, jit: bool | None = None):
+        return engine.prepare_fragments(virt, self.device, basis=basis, jit=jit)
 
     def upload_jobs(self, jobs: JobTable):
         return engine.jobs_to_device(jobs, self.device)
@@ -140,7 +140,8 @@ class HipBackend:
 
 class KnitPipeline:
     def __init__(self, virt, device: int = 0, factored: bool = False, rank: int = 0, world: int = 1,
-                 mode: str | None = None, group=None, backend=None, chunk_jobs: int | None = None):
+                 mode: str | None = None, group=None, backend=None, chunk_jobs: int | None = None,
+                 jit: bool | None = None):
         self.be = backend if backend is not None else HipBackend(device)
         # branch jobs per sweep chunk of a fused (compiled) fragment; 0 = the whole fragment at once
         self.chunk_jobs = int(os.environ.get("QKNIT_SWEEP_CHUNK_JOBS", "0")) if chunk_jobs is None else chunk_jobs
@@ -151,7 +152,8 @@ class KnitPipeline:
         self.virt = virt
         self.rank, self.world, self.group = rank, world, group
         self.factored = factored
-        self.frags = self.be.prepare_fragments(virt, basis=factored)
+        self.frags = (self.be.prepare_fragments(virt, basis=factored) if jit is None
+                      else self.be.prepare_fragments(virt, basis=factored, jit=jit))
         self.ops = engine.knit_operands(virt, self.frags, factored)
         self.N = virt.circuit.num_clbits
         q_bytes = sum(len(fs.labels) << fs.prog.m for fs in self.frags) * 8

@@ -446,3 +446,44 @@ def test_foreign_backend_fragment_rows_per_label(T):
                 np.testing.assert_allclose(out.cpu().numpy(), dense.run_dense(cut), atol=1e-10, rtol=0)
     finally:
         pqd.ACCURACY = old
+
+
+def test_chunked_sweep_and_sweep_graph_match_eager(T):
+    """Chunked fused sweeps (Infinity-Cache-resident workspace) and the captured sweep graph
+    (fragments on forked streams) give the eager pipeline's q_f bit for bit (syc 32 5, and the
+    syc 32 1 reference cut on the interpreter kernel)."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    for key, factored in (("syc_32_5_p2", True), ("syc_32_1_p2", False)):
+        name, n, d, p, var = cutting.BASELINE_CONFIGS[key]
+        _, cut, _ = cutting.config_cut_circuit(name, n, d, p, var)
+        ref = [q.clone() for q in KnitPipeline(VirtualCircuit(cut), factored=factored).sweep()]
+        if factored:
+            got = KnitPipeline(VirtualCircuit(cut), factored=True, chunk_jobs=96).sweep()
+            assert all(T.equal(a, b) for a, b in zip(got, ref))
+        pipe = KnitPipeline(VirtualCircuit(cut), factored=factored)
+        pipe.capture_sweep()
+        for _ in range(2):
+            got = pipe.replay_sweep()
+        T.cuda.synchronize()
+        assert all(T.equal(a, b) for a, b in zip(got, ref))
+        del pipe
+        T.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("K,M,N,odd_rows", [(1, 512, 4096, False), (3, 300, 1024, False), (8, 256, 2048, False),
+                                            (2, 257, 512, True)])
+def test_gemm_small_k_path_matches_torch(T, K, M, N, odd_rows):
+    """K <= 8 contractions with contiguous columns take qk_gemm_smallk_kernel (the output-write
+    bound outer product of syc 32 1's uncut knit), incl. row keys that break 16-B alignment."""
+    ctx = engine.get_context(0)
+    g = T.Generator(device="cuda").manual_seed(K * M + N)
+    A = T.randn(K, M, dtype=T.float64, device="cuda", generator=g)
+    B = T.randn(K, N, dtype=T.float64, device="cuda", generator=g)
+    ref = A.T @ B
+    stride = N + 1 if odd_rows else N
+    out = T.full((M * stride,), float("nan"), dtype=T.float64, device="cuda")
+    engine.gemm_keyed(ctx, A, B, out=out, strideA=stride)
+    T.cuda.synchronize()
+    got = out.view(M, stride)[:, :N]
+    assert float((got - ref).abs().max()) <= 1e-12 * K

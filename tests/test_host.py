@@ -282,3 +282,15 @@ def test_gather_mode_rows_dealt_by_jobs():
         assert max(len(r) for r in dealt) <= -(-len(jobs) // world)
         per_rank = [int(jobs[r].sum()) for r in dealt]
         assert max(per_rank) - min(per_rank) <= int(jobs.max())
+
+
+def test_label_chunks_cover_labels_without_splitting():
+    offs = np.array([0, 2, 3, 7, 8, 10, 11], dtype=np.int64)
+    for max_jobs in (1, 2, 3, 4, 5, 100):
+        ch = engine.label_chunks(offs, max_jobs)
+        assert ch[0][0] == 0 and ch[-1][1] == len(offs) - 1
+        for (l0, l1, j0, j1), nxt in zip(ch, ch[1:] + [None]):
+            assert (j0, j1) == (offs[l0], offs[l1])
+            assert j1 - j0 <= max_jobs or l1 == l0 + 1
+            if nxt is not None:
+                assert nxt[0] == l1
