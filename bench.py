@@ -270,8 +270,8 @@ def main():
         "sweep": {
             "kernel": "per-program sweep kernels (sweep_codegen + hiprtc; FINAL pass sums each label's "
                       "branch jobs) (all fragments, per step, this rank)",
-            "bound": "hbm (modelled bytes below; fused passes move far fewer than the per-gate "
-                     "algorithmic model)",
+            "bound": "fp64 VALU / latency: two passes of 13-bit tiles move 0.6 GB per step (modelled "
+                     "hbm_bytes), far below the per-gate algorithmic model",
             "ms_per_step": sweep_ms,
             "branch_jobs": counts["branch_jobs"],
             "hbm_bytes": traffic["hbm"],

@@ -106,7 +106,11 @@ int sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* p, in
         const bool sparse_init = ip == 0 && p->n_passes > 1;  // qk_sweep: INIT tile of each job only
         const bool fin = ip == p->n_passes - 1;
         const int64_t units = (fin && label_off) ? n_labels : n_jobs;
-        const int64_t blocks = sparse_init ? n_jobs : (units << (p->n - QK_TILE_BITS));
+        // tile width of this program (12 or 13 state bits): 2^(bits - 4) threads of 16 amplitudes
+        const int tb = __builtin_popcountll(p->passes[ip].tile_mask);
+        if (tb < QK_TILE_BITS || tb > QK_TILE_BITS + 1 || tb >= p->n)
+            return jfail(ctx, QK_EARG, "qk_sweep_compiled: tiles must hold 12 or 13 state bits");
+        const int64_t blocks = sparse_init ? n_jobs : (units << (p->n - tb));
         if (blocks > 0x7fffffff) return jfail(ctx, QK_EARG, "qk_sweep_compiled: too many tiles");
         struct {
             const double* slots;
@@ -119,7 +123,7 @@ int sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* p, in
         size_t size = sizeof(args);
         void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                        HIP_LAUNCH_PARAM_END};
-        const hipError_t e = hipModuleLaunchKernel(module->fns[ip], (unsigned)blocks, 1, 1, 256, 1, 1, 0,
+        const hipError_t e = hipModuleLaunchKernel(module->fns[ip], (unsigned)blocks, 1, 1, 1u << (tb - 4), 1, 1, 0,
                                                    ctx->stream, nullptr, cfg);
         if (e != hipSuccess) return jfail(ctx, QK_EHIP, std::string("qk_sweep_compiled: ") + hipGetErrorString(e));
     }

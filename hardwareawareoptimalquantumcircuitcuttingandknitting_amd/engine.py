@@ -109,7 +109,8 @@ class DeviceProgram:
     @staticmethod
     def upload(prog: FragmentProgram, device, jit: bool = True) -> "DeviceProgram":
         T = torch()
-        enc = encode(prog)
+        # per-program kernels take 13-bit tiles (128 KiB LDS): fewer passes, less state traffic
+        enc = encode(prog, tile_bits=JIT_TILE_BITS if (jit and _jit_enabled()) else 12)
         dev = T.device("cuda", device)
 
         def to_dev(arr, dtype):
@@ -135,6 +136,13 @@ class DeviceProgram:
                             ops.data_ptr(), groups.data_ptr(), mats.data_ptr())
         module = compiled_module(device, enc) if (jit and not enc.packed) else None
         return DeviceProgram(prog, enc, ops, groups, mats, passes, st, module)
+
+
+JIT_TILE_BITS = int(os.environ.get("QKNIT_JIT_TILE_BITS", "13"))
+
+
+def _jit_enabled() -> bool:
+    return os.environ.get("QKNIT_SWEEP_JIT", "1") != "0"
 
 
 _MODULES: dict = {}

@@ -70,7 +70,7 @@ def _sweep_flops_per_job(enc) -> int:
     P = len(enc.passes)
     for ip in range(P):
         ps = enc.passes[ip]
-        amps = (1 << sweep_plan.TILE_BITS) if (not enc.packed and ip == 0 and P > 1) else n_amp
+        amps = (1 << enc.tile_bits) if (not enc.packed and ip == 0 and P > 1) else n_amp
         for gi in range(int(ps["group_begin"]), int(ps["group_end"])):
             gr = enc.groups[gi]
             for oi in range(int(gr["op_begin"]), int(gr["op_end"])):
@@ -466,7 +466,7 @@ class KnitPipeline:
                 continue
             enc = fs.dprog.enc if getattr(fs, "dprog", None) is not None else sweep_plan.encode(fs.prog)
             J, n, m, P = sw["n_jobs"], enc.n, enc.m, len(enc.passes)
-            S, tile, out = 16 << n, 16 << sweep_plan.TILE_BITS, 8 << m
+            S, tile, out = 16 << n, 16 << enc.tile_bits, 8 << m
             if enc.packed or P == 1:
                 per_job = out
             elif P == 2:

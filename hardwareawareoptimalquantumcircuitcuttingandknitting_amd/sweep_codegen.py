@@ -23,8 +23,7 @@ from . import sweep_plan as sp
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 OPS_HEADER = os.path.join(_HERE, "csrc", "sweep_ops.h")
-NT = 256
-PER = 16
+PER = 16  # amplitudes per thread (4 fiber bits); threads per workgroup = 2^(tile_bits - 4)
 
 
 def _lit(x: float) -> str:
@@ -153,21 +152,23 @@ def _emit_op(e: _Emitter, op, mats, ext, n_slots: int) -> None:
 
 def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str) -> list:
     n, m = enc.n, enc.m
+    TB = enc.tile_bits
+    NT = 1 << (TB - 4)
     P = len(enc.passes)
     ps = enc.passes[ip]
     flags = int(ps["flags"])
     init, final = bool(flags & sp.PASS_INIT), bool(flags & sp.PASS_FINAL)
     tile_mask = int(ps["tile_mask"])
     bitpos = _bits(tile_mask)
-    assert len(bitpos) == sp.TILE_BITS
+    assert len(bitpos) == TB
     nmask = (1 << n) - 1
     outside = _bits(nmask & ~tile_mask)
     init_sparse = ip == 0 and P > 1
     zero_mask = (nmask & ~int(enc.passes[0]["tile_mask"])) if ip == 1 else 0
-    tpj_log = 0 if init_sparse else n - sp.TILE_BITS
+    tpj_log = 0 if init_sparse else n - TB
     traced = int(ps["traced_local"])
     mmask = (1 << m) - 1
-    hi = [sum(((i >> k) & 1) << bitpos[8 + k] for k in range(4)) for i in range(PER)]
+    hi = [sum(((i >> k) & 1) << bitpos[TB - 4 + k] for k in range(4)) for i in range(PER)]
 
     e = _Emitter()
     e(f'extern "C" __global__ __launch_bounds__({NT}) void {name}(', 0)
@@ -175,7 +176,7 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str) -> list:
     e("double2* __restrict__ state, double* __restrict__ pjob, long long n_jobs,", 2)
     e("const long long* __restrict__ label_off) {", 2)
     e("using namespace qk_sweep_ops;")
-    e("__shared__ double2 lds[4096];")
+    e(f"__shared__ double2 lds[{1 << TB}];")
     e("const unsigned tid = threadIdx.x;")
     # FINAL: grp is a label when label_off is given (its branch jobs are summed in registers,
     # qk_sweep_compiled_labels), else a job
@@ -185,7 +186,7 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str) -> list:
         e(f"const unsigned long long tbase = {_deposit('tj', list(range(len(outside))), outside)};")
     else:
         e("const unsigned long long tbase = 0ull;")
-    e(f"const unsigned long long lo = {_deposit('(unsigned long long)tid', list(range(8)), bitpos[:8])};")
+    e(f"const unsigned long long lo = {_deposit('(unsigned long long)tid', list(range(TB - 4)), bitpos[:TB - 4])};")
     e("(void)n_jobs; (void)job_slots; (void)lo; (void)label_off;")
     keep = [i for i in range(PER) if not ((NT * i) & traced)]
     if final:
@@ -219,9 +220,9 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str) -> list:
     for gi in range(int(ps["group_begin"]), int(ps["group_end"])):
         gr = enc.groups[gi]
         pos = [int(x) for x in gr["pos"]]
-        nonfib = [p for p in range(sp.TILE_BITS) if p not in pos]
+        nonfib = [p for p in range(TB) if p not in pos]
         e("{")
-        e(f"const unsigned base = {_deposit('tid', list(range(8)), nonfib)};", 2)
+        e(f"const unsigned base = {_deposit('tid', list(range(TB - 4)), nonfib)};", 2)
         cst = [sum(((r >> k) & 1) << pos[k] for k in range(4)) for r in range(PER)]
         e("double2 v[16];", 2)
         for r in range(PER):

@@ -21,6 +21,8 @@ takes (``include/qknit.h``: ``qk_op``, ``qk_group``, ``qk_pass``).
 """
 from __future__ import annotations
 
+import itertools
+import math
 from dataclasses import dataclass
 
 import numpy as np
@@ -77,17 +79,15 @@ class Pass:
     ops: list  # HostOps in order
 
 
-def schedule_passes(prog: FragmentProgram) -> list[Pass]:
-    n = prog.n
-    if n <= TILE_BITS:
-        return [Pass(list(range(n)), list(prog.ops))]
-    traced = set(range(prog.m, n))
-    if len(traced) > TILE_BITS - LOW_BITS:
-        raise NotImplementedError("more traced qubits than a tile can hold")
-    remaining = list(prog.ops)
+def _greedy_passes(ops: list, tile_bits: int, first_tile: set | None = None) -> list[Pass] | None:
+    """Greedy schedule: each pass takes ops in order while their non-diagonal qubits fit the tile
+    (an op touching a qubit of a deferred op is deferred too). ``first_tile`` fixes the first
+    pass's tile instead of growing it (None when that pass could take nothing)."""
+    remaining = list(ops)
     passes: list[Pass] = []
+    fixed = first_tile
     while remaining:
-        tile = set(range(LOW_BITS))
+        tile = set(fixed) if fixed is not None else set(range(LOW_BITS))
         taken, blocked, rest = [], set(), []
         for op in remaining:
             qs = set(op.qubits)
@@ -96,16 +96,44 @@ def schedule_passes(prog: FragmentProgram) -> list[Pass]:
                 blocked |= qs
                 rest.append(op)
                 continue
-            if need <= tile or len(tile | need) <= TILE_BITS:
+            if need <= tile or (fixed is None and len(tile | need) <= tile_bits):
                 tile |= need
                 taken.append(op)
             else:
                 blocked |= qs
                 rest.append(op)
-        if not taken:  # cannot happen: first op always fits (need <= 2 qubits)
-            raise RuntimeError("pass scheduler made no progress")
+        if not taken:
+            if fixed is not None:
+                return None
+            raise RuntimeError("pass scheduler made no progress")  # first op always fits
+        fixed = None
         passes.append(Pass(sorted(tile), taken))
         remaining = rest
+    return passes
+
+
+def schedule_passes(prog: FragmentProgram, tile_bits: int = TILE_BITS) -> list[Pass]:
+    """Pass schedule for SPLIT programs with ``tile_bits``-bit tiles (PACKED: one pass).
+
+    Greedy in op order; when that needs more than two passes, every choice of the first pass's
+    tile (the low bits plus ``tile_bits - LOW_BITS`` of the others, at most 200 choices) is tried
+    with the greedy after it, and the schedule with the fewest passes is kept (first found)."""
+    n = prog.n
+    if n <= TILE_BITS:
+        return [Pass(list(range(n)), list(prog.ops))]
+    traced = set(range(prog.m, n))
+    if len(traced) > tile_bits - LOW_BITS:
+        raise NotImplementedError("more traced qubits than a tile can hold")
+    passes = _greedy_passes(prog.ops, tile_bits)
+    free = list(range(LOW_BITS, n))
+    extra = tile_bits - LOW_BITS
+    if len(passes) > 2 and 0 < extra < len(free) and math.comb(len(free), extra) <= 200:
+        for combo in itertools.combinations(free, extra):
+            cand = _greedy_passes(prog.ops, tile_bits, set(range(LOW_BITS)) | set(combo))
+            if cand is not None and len(cand) < len(passes):
+                passes = cand
+                if len(passes) <= 2:
+                    break
     if not passes:
         passes.append(Pass(sorted(set(range(LOW_BITS))), []))
     # final pass must hold every traced qubit; prefer swapping in unused bits
@@ -115,7 +143,7 @@ def schedule_passes(prog: FragmentProgram) -> list[Pass]:
     for op in last.ops:
         used |= op_need(op)
     for q in traced - tile:
-        if len(tile) < TILE_BITS:
+        if len(tile) < tile_bits:
             tile.add(q)
             continue
         spare = sorted(tile - used - traced)
@@ -131,7 +159,7 @@ def schedule_passes(prog: FragmentProgram) -> list[Pass]:
     for p in passes:
         t = set(p.tile)
         for q in range(n):
-            if len(t) >= TILE_BITS:
+            if len(t) >= tile_bits:
                 break
             t.add(q)
         p.tile = sorted(t)
@@ -151,6 +179,7 @@ class EncodedProgram:
     passes: np.ndarray  # PASS_DTYPE
     mats: np.ndarray  # float64, interleaved complex
     n_host_ops: int
+    tile_bits: int = TILE_BITS  # SPLIT: state bits per tile (12 interpreter; 13 compiled kernels)
 
     @property
     def jobs_per_tile(self) -> int:
@@ -158,7 +187,7 @@ class EncodedProgram:
 
     @property
     def tiles_per_job(self) -> int:
-        return 1 if self.packed else 1 << (self.n - TILE_BITS)
+        return 1 if self.packed else 1 << (self.n - self.tile_bits)
 
 
 class _Mats:
@@ -283,17 +312,21 @@ def _emit(op: HostOp, fib: dict, mats: _Mats) -> list:
     return [rec(K_U2, a=a, b=b, mat=mats.add(mm))]
 
 
-def encode(prog: FragmentProgram) -> EncodedProgram:
+def encode(prog: FragmentProgram, tile_bits: int = TILE_BITS) -> EncodedProgram:
+    """``tile_bits`` (SPLIT programs only; PACKED programs always use 12-bit tiles): 12 for the
+    interpreter kernel, 13 for per-program kernels (128 KiB LDS, 512 threads)."""
     n = prog.n
     packed = n <= TILE_BITS
     n_eff = max(n, FIBER_BITS) if packed else n
-    passes = schedule_passes(prog)
+    if packed or tile_bits >= n:
+        tile_bits = TILE_BITS
+    passes = schedule_passes(prog, tile_bits)
     mats = _Mats()
     ops_out, groups_out, passes_out = [], [], []
     for pi, p in enumerate(passes):
         tile = list(range(n_eff)) if packed else p.tile
         local = {q: i for i, q in enumerate(tile)}  # state bit -> local position
-        n_local = n_eff if packed else TILE_BITS
+        n_local = n_eff if packed else tile_bits
         g_begin = len(groups_out)
         # cut the pass into fiber groups
         cur: list = []
@@ -342,4 +375,4 @@ def encode(prog: FragmentProgram) -> EncodedProgram:
     mat_arr = np.asarray(mats.buf if mats.buf else [0.0], dtype=np.float64)
     return EncodedProgram(n=n, n_eff=n_eff, m=prog.m, n_slots=prog.num_slots, packed=packed,
                           ops=ops_arr, groups=grp_arr, passes=pass_arr, mats=mat_arr,
-                          n_host_ops=len(prog.ops))
+                          n_host_ops=len(prog.ops), tile_bits=tile_bits)

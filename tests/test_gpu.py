@@ -249,8 +249,9 @@ def test_compiled_sweep_matches_interpreter(T):
         assert fs.dprog.module is not None, "SPLIT programs run as compiled kernels"
         slot_t, sign_t, _ = engine.jobs_to_device(fs.jobs, 0)
         jit, _ = engine.sweep_jobs(ctx, fs.dprog, slot_t, sign_t, fs.jobs.n_jobs)
-        interp, _ = engine.sweep_jobs(ctx, dataclasses.replace(fs.dprog, module=None), slot_t, sign_t,
-                                      fs.jobs.n_jobs)
+        assert fs.dprog.enc.tile_bits == 13
+        interp_prog = engine.DeviceProgram.upload(fs.prog, 0, jit=False)  # 12-bit tiles
+        interp, _ = engine.sweep_jobs(ctx, interp_prog, slot_t, sign_t, fs.jobs.n_jobs)
         T.cuda.synchronize()
         assert float((jit - interp).abs().max()) <= 1e-13
         # fused FINAL pass (qk_sweep_compiled_labels) == per-job rows + qk_reduce_labels, bit for bit

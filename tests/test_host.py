@@ -197,8 +197,10 @@ def test_syc_32_5_schedule_shape():
         assert jobs.n_jobs == 4096  # (4 + 2*2)^4 branch jobs: 4/6 unmeasured + 2/6 measured sides
 
 
-def test_split_mode_emulated_16_qubits():
-    """A 16-qubit SPLIT-mode fragment (3 passes) of syc 32 5 through the emulator vs the oracle."""
+@pytest.mark.parametrize("tile_bits", [12, 13])
+def test_split_mode_emulated_16_qubits(tile_bits):
+    """A 16-qubit SPLIT-mode fragment of syc 32 5 (12-bit tiles: 3 passes, the interpreter's
+    layout; 13-bit: 2 passes, the per-program kernels') through the emulator vs the oracle."""
     _, cut = cutting.config_cut_circuit("syc", 32, 5, 2)[:2]
     virt = VirtualCircuit(cut)
     view = qvm.CutView(cut)
@@ -208,8 +210,9 @@ def test_split_mode_emulated_16_qubits():
     all_labels = virt.get_instance_labels(frag)
     labels = [all_labels[0], all_labels[500], all_labels[1295]]
     jobs = build_jobs(prog, labels)
-    enc = sweep_plan.encode(prog)
-    assert not enc.packed and len(enc.passes) >= 2
+    enc = sweep_plan.encode(prog, tile_bits=tile_bits)
+    assert not enc.packed and len(enc.passes) >= 2 and enc.tile_bits == tile_bits
+    assert all(bin(int(ps["tile_mask"])).count("1") == tile_bits for ps in enc.passes)
     p = emulate(enc, jobs.slot_mats, jobs.sign)
     offs = jobs.label_offsets
     q = np.stack([p[offs[i]:offs[i + 1]].sum(0) for i in range(len(labels))])
@@ -257,8 +260,8 @@ def test_generated_sweep_kernels_compile_for_gfx950(tmp_path):
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     _, cut, _ = cutting.config_cut_circuit("syc", 32, 5, 2)
     virt = VirtualCircuit(cut)
-    for fs in engine.prepare_fragments(virt, upload=False, basis=True)[:1]:
-        enc = sweep_plan.encode(fs.prog)
+    for fs, tb in zip(engine.prepare_fragments(virt, upload=False, basis=True), (12, 13)):
+        enc = sweep_plan.encode(fs.prog, tile_bits=tb)
         src, names = sweep_codegen.generate(enc)
         assert len(names) == len(enc.passes)
         f = tmp_path / "k.hip"
