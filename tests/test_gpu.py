@@ -488,3 +488,32 @@ def test_gemm_small_k_path_matches_torch(T, K, M, N, odd_rows):
     T.cuda.synchronize()
     got = out.view(M, stride)[:, :N]
     assert float((got - ref).abs().max()) <= 1e-12 * K
+
+
+def test_edge_cases_empty_and_degenerate(T):
+    """K = 0 contraction writes zeros; zero labels / zero shots are no-ops; one shot per label
+    puts all mass on one outcome; a fragment with one label samples like the oracle."""
+    from oracle import sampling
+
+    ctx = engine.get_context(0)
+    out = T.full((64 * 64,), 7.0, dtype=T.float64, device="cuda")
+    A = T.zeros((0, 64), dtype=T.float64, device="cuda")
+    engine.gemm_keyed(ctx, A, T.zeros((0, 64), dtype=T.float64, device="cuda"), out=out, strideA=64)
+    T.cuda.synchronize()
+    assert float(out.abs().max()) == 0.0
+    assert ctx.lib.qk_sample_counts(ctx.handle, 0, 0, None, None, None, 4, None, 10, 0, None) == 0
+    assert ctx.lib.qk_sample_counts(ctx.handle, 3, 0, None, None, None, 4, None, 0, 0, None) == 0
+    assert ctx.lib.qk_fold_counts(ctx.handle, 2, None, 4, None, None, 0, 0.0, None) != 0  # shots must be > 0
+    _, cut = CASES["cx"]()
+    virt = VirtualCircuit(cut)
+    for i, fs in enumerate(engine.prepare_fragments(virt, 0)):
+        q = engine.sample_fragment(ctx, fs, 1, engine.fragment_seed(5, i), 0.0).cpu().numpy()
+        assert np.all(np.abs(q).sum(axis=1) == 1.0)  # one draw: a single +-1 entry per label
+    _, cut = CASES["partial"]()
+    view = qvm.CutView(cut)
+    for i, fs in enumerate(engine.prepare_fragments(VirtualCircuit(cut), 0)):
+        if fs.dropped:
+            continue
+        q = engine.sample_fragment(ctx, fs, 777, engine.fragment_seed(2, i), 1e-5).cpu().numpy()
+        ref = np.stack([r[1] for r in sampling.sampled_fragment(view, list(fs.fragment), i, 777, 2, 1e-5)])
+        np.testing.assert_allclose(q, ref, atol=1e-15, rtol=0)

@@ -42,3 +42,12 @@ def test_no_compute_without_device():
     assert lib.qk_ctx_create(0, None) != 0
     assert lib.qk_sweep(None, None, 0, None, None, None, 0, None) != 0
     assert lib.qk_last_error(None) == b"null context"
+
+
+def test_new_entry_points_validate_arguments_without_device():
+    """Sampling and fused-sweep entry points reject a null context before touching the GPU."""
+    lib = _lib.lib()
+    assert lib.qk_sample_cdf(None, 1, None, 4, None, None) != 0
+    assert lib.qk_sample_counts(None, 1, 0, None, None, None, 4, None, 10, 0, None) != 0
+    assert lib.qk_fold_counts(None, 1, None, 4, None, None, 10, 0.0, None) != 0
+    assert lib.qk_sweep_compiled_labels(None, None, None, 1, None, None, 1, None, None, 0, None) != 0
