@@ -128,7 +128,8 @@ def north_star_sweep(steps: int) -> dict:
             torch.cuda.synchronize()
             return s.elapsed_time(e) / steps
 
-        ways = {"eager, fragments in sequence": timed(pipe.sweep)}
+        ways = {("eager, one launch per pass round for all fragments" if pipe._multi is not None
+                 else "eager, fragments in sequence"): timed(pipe.sweep)}
         pipe.fork = True  # one stream per fragment (independent sweeps overlap)
         ways["eager, fragments on forked streams"] = timed(pipe.sweep)
         pipe.capture_sweep()  # the same launches as one HIP graph

@@ -141,6 +141,80 @@ int qk_sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* p,
                           nullptr);
 }
 
+// Kernel argument of a multi-fragment pass launch (sweep_codegen.generate_multi declares the same).
+#define QK_MULTI_MAX 4
+struct qk_multi_args {
+    const double* slots[QK_MULTI_MAX];
+    const double* sign[QK_MULTI_MAX];
+    void* state[QK_MULTI_MAX];
+    double* out[QK_MULTI_MAX];
+    const int64_t* label_off[QK_MULTI_MAX];
+    int64_t n_jobs[QK_MULTI_MAX];
+    int64_t begin[QK_MULTI_MAX];
+    int64_t end[QK_MULTI_MAX];
+};
+
+int qk_sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, const qk_program* progs,
+                            const int64_t* n_jobs, const double* const* job_slots, const double* const* job_sign,
+                            const int64_t* n_labels, const int64_t* const* label_offsets, void* const* workspaces,
+                            const int64_t* workspace_bytes, double* const* outs) {
+    if (!ctx) return QK_EARG;
+    if (!module || !progs || n_prog < 1 || n_prog > QK_MULTI_MAX || !n_jobs || !job_slots || !job_sign ||
+        !n_labels || !label_offsets || !workspaces || !workspace_bytes || !outs)
+        return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: bad arguments");
+    int rounds = 0, tb = 0;
+    for (int f = 0; f < n_prog; ++f) {
+        const qk_program& p = progs[f];
+        if (p.packed || !p.passes || p.n_passes < 1 || p.n > 40)
+            return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: SPLIT programs only");
+        const int t = __builtin_popcountll(p.passes[0].tile_mask);
+        if ((f && t != tb) || t < QK_TILE_BITS || t > QK_TILE_BITS + 1 || t >= p.n)
+            return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: programs need one tile width of 12 or 13 bits");
+        tb = t;
+        if (n_jobs[f] < 1 || !job_sign[f] || !outs[f] || (p.n_slots > 0 && !job_slots[f]))
+            return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: empty program or null buffer");
+        if (label_offsets[f] && n_labels[f] < 1)
+            return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: label offsets need n_labels >= 1");
+        const int64_t need = n_jobs[f] * ((int64_t)1 << p.n) * (int64_t)(2 * sizeof(double));
+        if (!workspaces[f] || workspace_bytes[f] < need)
+            return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: workspace too small");
+        if (p.n_passes > rounds) rounds = p.n_passes;
+    }
+    if ((int)module->fns.size() != rounds)
+        return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: module does not hold one kernel per pass round");
+    if (hipSetDevice(ctx->device) != hipSuccess) return jfail(ctx, QK_EHIP, "qk_sweep_compiled_multi: hipSetDevice");
+    for (int r = 0; r < rounds; ++r) {
+        qk_multi_args a{};
+        int64_t total = 0;
+        for (int f = 0; f < n_prog; ++f) {
+            const qk_program& p = progs[f];
+            a.begin[f] = a.end[f] = total;
+            if (p.n_passes <= r) continue;
+            if (__builtin_popcountll(p.passes[r].tile_mask) != tb)
+                return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: tile width changes between passes");
+            const bool sparse_init = r == 0 && p.n_passes > 1;
+            const bool fin = r == p.n_passes - 1;
+            const int64_t units = (fin && label_offsets[f]) ? n_labels[f] : n_jobs[f];
+            total += sparse_init ? n_jobs[f] : (units << (p.n - tb));
+            a.end[f] = total;
+            a.slots[f] = job_slots[f];
+            a.sign[f] = job_sign[f];
+            a.state[f] = workspaces[f];
+            a.out[f] = outs[f];
+            a.label_off[f] = fin ? label_offsets[f] : nullptr;
+            a.n_jobs[f] = n_jobs[f];
+        }
+        if (total > 0x7fffffff) return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: too many tiles");
+        size_t size = sizeof(a);
+        void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+        const hipError_t e = hipModuleLaunchKernel(module->fns[r], (unsigned)total, 1, 1, 1u << (tb - 4), 1, 1, 0,
+                                                   ctx->stream, nullptr, cfg);
+        if (e != hipSuccess)
+            return jfail(ctx, QK_EHIP, std::string("qk_sweep_compiled_multi: ") + hipGetErrorString(e));
+    }
+    return QK_OK;
+}
+
 int qk_sweep_compiled_labels(qk_ctx* ctx, const qk_module* module, const qk_program* p, int64_t n_jobs,
                              const double* job_slots, const double* job_sign, int64_t n_labels,
                              const int64_t* label_offsets, void* workspace, int64_t workspace_bytes, double* q) {

@@ -156,7 +156,18 @@ def compiled_module(device: int, enc):
         return None
     from . import sweep_codegen
 
-    src, names = sweep_codegen.generate(enc)
+    return _compile_module(device, *sweep_codegen.generate(enc))
+
+
+def compiled_multi_module(device: int, encs: list):
+    """Multi-fragment sweep kernels (sweep_codegen.generate_multi), compiled once per
+    (device, program set) with hiprtc."""
+    from . import sweep_codegen
+
+    return _compile_module(device, *sweep_codegen.generate_multi(encs))
+
+
+def _compile_module(device: int, src: str, names: list):
     key = (device, names[0])
     with _modules_lock:
         if key not in _MODULES:

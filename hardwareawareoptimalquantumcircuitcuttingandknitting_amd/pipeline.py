@@ -32,7 +32,7 @@ import os
 
 import numpy as np
 
-from . import engine
+from . import _lib, engine
 from .fragment_program import JobTable
 
 
@@ -115,6 +115,25 @@ class HipBackend:
         """Point the qk context at torch's current stream (a forked or a graph-capture stream)."""
         self.ctx.bind_stream()
 
+    def plan_multi(self, frags: list, sweeps: list):
+        """ctypes argument arrays of one qk_sweep_compiled_multi call over these fragments."""
+        n = len(frags)
+        vp = lambda xs: (ctypes.c_void_p * n)(*xs)  # noqa: E731
+        i64 = lambda xs: (ctypes.c_int64 * n)(*xs)  # noqa: E731
+        module = engine.compiled_multi_module(self.device, [fs.dprog.enc for fs in frags])
+        outs = [(sw["q"] if sw["fused"] else sw["pjob"]) for sw in sweeps]
+        return (module, (_lib.QkProgram * n)(*[fs.dprog.struct for fs in frags]), i64([sw["n_jobs"] for sw in sweeps]),
+                vp([sw["slot"].data_ptr() for sw in sweeps]), vp([sw["sign"].data_ptr() for sw in sweeps]),
+                i64([sw["n_local"] for sw in sweeps]),
+                vp([sw["off"].data_ptr() if sw["fused"] else None for sw in sweeps]),
+                vp([sw["ws"].data_ptr() for sw in sweeps]), i64([sw["ws"].numel() for sw in sweeps]),
+                vp([o.data_ptr() for o in outs]))
+
+    def sweep_multi(self, plan):
+        module, progs, *rest = plan
+        self.ctx.check(self.ctx.lib.qk_sweep_compiled_multi(self.ctx.handle, module, len(progs), progs, *rest),
+                       "qk_sweep_compiled_multi")
+
     def fuses_labels(self, fs) -> bool:
         """Whether the sweep of ``fs`` can emit per-label rows itself (compiled program)."""
         return fs.dprog is not None and fs.dprog.module is not None
@@ -146,6 +165,7 @@ class KnitPipeline:
         # branch jobs per sweep chunk of a fused (compiled) fragment; 0 = the whole fragment at once
         self.chunk_jobs = int(os.environ.get("QKNIT_SWEEP_CHUNK_JOBS", "0")) if chunk_jobs is None else chunk_jobs
         self.fork = False  # single mode: sweep each fragment on its own stream (set by capture_sweep)
+        self._multi = None
         self._streams = []
         self._sweep_graph = None
         self.T = engine.torch()
@@ -228,6 +248,24 @@ class KnitPipeline:
         self._plan_knit()
         if self.mode == "gather":
             self._plan_exchange()
+        self._plan_multi()
+
+    def _plan_multi(self):
+        """Single mode: when every swept fragment runs compiled kernels of one tile width (2-4
+        fragments, not chunked), the whole sweep is one qk_sweep_compiled_multi call — pass round
+        r of all fragments in one launch — instead of a launch sequence per fragment."""
+        self._multi = None
+        if self.mode != "single" or os.environ.get("QKNIT_SWEEP_MULTI", "1") == "0":
+            return
+        if not hasattr(self.be, "plan_multi"):
+            return
+        idx = [i for i, sw in enumerate(self.sweeps) if sw is not None]
+        ok = all(self.sweeps[i]["n_jobs"] and self.sweeps[i]["chunks"] is None
+                 and getattr(self.frags[i], "dprog", None) is not None and self.frags[i].dprog.module is not None
+                 for i in idx)
+        if not ok or not 2 <= len(idx) <= 4 or len({self.frags[i].dprog.enc.tile_bits for i in idx}) != 1:
+            return
+        self._multi = (idx, self.be.plan_multi([self.frags[i] for i in idx], [self.sweeps[i] for i in idx]))
 
     def _plan_exchange(self):
         """Collectives of gather mode. With two fragments the A side (output rows) only needs
@@ -290,6 +328,15 @@ class KnitPipeline:
         T, be = self.T, self.be
         qs = [None] * len(self.frags)
         pending = []
+        if self._multi is not None and not self.fork:
+            idx, plan = self._multi
+            be.sweep_multi(plan)
+            for i, (fs, sw) in enumerate(zip(self.frags, self.sweeps)):
+                if sw is None:
+                    qs[i] = be.zeros((fs.n_rows, 1), T.float64) + 1.0
+                else:
+                    qs[i] = (sw["q"] if sw["fused"] else sw["pjob"])[: sw["n_local"]]
+            return qs
         fork = self.fork and self.mode == "single"
         main = T.cuda.current_stream() if fork else None
         # the A side (output rows) first, so its exchange overlaps the other sweeps

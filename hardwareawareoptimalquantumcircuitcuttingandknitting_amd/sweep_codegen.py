@@ -150,7 +150,9 @@ def _emit_op(e: _Emitter, op, mats, ext, n_slots: int) -> None:
     e("}", 1)
 
 
-def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str) -> list:
+def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str, device_fn: bool = False) -> list:
+    """Pass ``ip`` of ``enc`` as an ``extern "C"`` kernel, or (``device_fn``) as a device function
+    of the workgroup's block index within the pass and the shared tile (multi-fragment launches)."""
     n, m = enc.n, enc.m
     TB = enc.tile_bits
     NT = 1 << (TB - 4)
@@ -171,18 +173,23 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str) -> list:
     hi = [sum(((i >> k) & 1) << bitpos[TB - 4 + k] for k in range(4)) for i in range(PER)]
 
     e = _Emitter()
-    e(f'extern "C" __global__ __launch_bounds__({NT}) void {name}(', 0)
+    if device_fn:
+        e(f"__device__ __forceinline__ void {name}(double2* __restrict__ lds, const unsigned blk,", 0)
+    else:
+        e(f'extern "C" __global__ __launch_bounds__({NT}) void {name}(', 0)
     e("const double* __restrict__ job_slots, const double* __restrict__ job_sign,", 2)
     e("double2* __restrict__ state, double* __restrict__ pjob, long long n_jobs,", 2)
     e("const long long* __restrict__ label_off) {", 2)
     e("using namespace qk_sweep_ops;")
-    e(f"__shared__ double2 lds[{1 << TB}];")
+    if not device_fn:
+        e(f"__shared__ double2 lds[{1 << TB}];")
+        e("const unsigned blk = blockIdx.x;")
     e("const unsigned tid = threadIdx.x;")
     # FINAL: grp is a label when label_off is given (its branch jobs are summed in registers,
     # qk_sweep_compiled_labels), else a job
-    e(f"const long long grp = (long long)(blockIdx.x >> {tpj_log});")
+    e(f"const long long grp = (long long)(blk >> {tpj_log});")
     if tpj_log:
-        e(f"const unsigned long long tj = blockIdx.x & {(1 << tpj_log) - 1}u;")
+        e(f"const unsigned long long tj = blk & {(1 << tpj_log) - 1}u;")
         e(f"const unsigned long long tbase = {_deposit('tj', list(range(len(outside))), outside)};")
     else:
         e("const unsigned long long tbase = 0ull;")
@@ -288,5 +295,56 @@ def generate(enc: sp.EncodedProgram) -> tuple[str, list]:
         name = f"qk_sweep_{key}_p{ip}"
         names.append(name)
         body += _pass_kernel(enc, ip, name) + [""]
+    src = open(OPS_HEADER).read() + "\n" + "\n".join(body) + "\n"
+    return src, names
+
+
+MULTI_MAX = 4  # fragments per multi-fragment launch (qknit_jit.hip QK_MULTI_MAX)
+_MULTI_STRUCT = """struct qk_multi_args {
+    const double* slots[4];
+    const double* sign[4];
+    void* state[4];
+    double* out[4];
+    const long long* label_off[4];
+    long long n_jobs[4];
+    long long begin[4];
+    long long end[4];
+};
+"""
+
+
+def generate_multi(encs: list) -> tuple[str, list]:
+    """Several SPLIT programs of one tile width swept together: one kernel per pass round ``r``,
+    in which fragment ``f`` (if it has a pass ``r``) owns the blocks ``[begin[f], end[f])`` and runs
+    its pass ``r`` body on them (``qk_sweep_compiled_multi``). Independent fragments then share
+    each launch instead of queueing behind each other."""
+    if not 1 <= len(encs) <= MULTI_MAX:
+        raise ValueError(f"1..{MULTI_MAX} programs per multi-fragment module")
+    if any(e.packed for e in encs) or len({e.tile_bits for e in encs}) != 1:
+        raise ValueError("multi-fragment kernels need SPLIT programs of one tile width")
+    NT = 1 << (encs[0].tile_bits - 4)
+    h = hashlib.sha1()
+    for e in encs:
+        h.update(e.ops.tobytes() + e.groups.tobytes() + e.passes.tobytes() + e.mats.tobytes()
+                 + bytes([e.n, e.m, e.n_slots]))
+    key = h.hexdigest()[:12]
+    body, names = [_MULTI_STRUCT], []
+    for r in range(max(len(e.passes) for e in encs)):
+        members = [f for f, e in enumerate(encs) if len(e.passes) > r]
+        for f in members:
+            body += _pass_kernel(encs[f], r, f"qk_mb_{key}_f{f}_p{r}", device_fn=True) + [""]
+        name = f"qk_sweepm_{key}_r{r}"
+        names.append(name)
+        body.append(f'extern "C" __global__ __launch_bounds__({NT}) void {name}(qk_multi_args a) {{')
+        body.append(f"    __shared__ double2 lds[{1 << encs[0].tile_bits}];")
+        body.append("    const long long b = blockIdx.x;")
+        for f in members:
+            body.append(f"    if (b >= a.begin[{f}] && b < a.end[{f}]) {{")
+            body.append(f"        qk_mb_{key}_f{f}_p{r}(lds, (unsigned)(b - a.begin[{f}]), a.slots[{f}], a.sign[{f}],")
+            body.append(f"            (double2*)a.state[{f}], a.out[{f}], a.n_jobs[{f}], a.label_off[{f}]);")
+            body.append("        return;")
+            body.append("    }")
+        body.append("}")
+        body.append("")
     src = open(OPS_HEADER).read() + "\n" + "\n".join(body) + "\n"
     return src, names

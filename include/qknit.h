@@ -128,6 +128,16 @@ int qk_sweep_compiled_labels(qk_ctx* ctx, const qk_module* module, const qk_prog
                              const double* job_slots, const double* job_sign, int64_t n_labels,
                              const int64_t* label_offsets, void* workspace, int64_t workspace_bytes, double* q);
 
+/* Up to 4 compiled SPLIT programs of one tile width swept together (module from
+ * sweep_codegen.generate_multi): pass round r of every program that has one runs in ONE launch, each
+ * program on its own block range, so independent fragments share launches. Per program f (HOST
+ * arrays of device pointers): label_offsets[f] non-NULL -> outs[f] = per-label rows as
+ * qk_sweep_compiled_labels; NULL -> per-job rows as qk_sweep_compiled. */
+int qk_sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, const qk_program* progs,
+                            const int64_t* n_jobs, const double* const* job_slots, const double* const* job_sign,
+                            const int64_t* n_labels, const int64_t* const* label_offsets, void* const* workspaces,
+                            const int64_t* workspace_bytes, double* const* outs);
+
 /* q[l][x] = sum_{j in [offsets[l], offsets[l+1])} pjob[j][x]   (offsets: DEVICE, n_labels+1) */
 int qk_reduce_labels(qk_ctx* ctx, int64_t n_labels, const int64_t* offsets, int64_t width,
                      const double* pjob, double* q);

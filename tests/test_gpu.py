@@ -517,3 +517,21 @@ def test_edge_cases_empty_and_degenerate(T):
         q = engine.sample_fragment(ctx, fs, 777, engine.fragment_seed(2, i), 1e-5).cpu().numpy()
         ref = np.stack([r[1] for r in sampling.sampled_fragment(view, list(fs.fragment), i, 777, 2, 1e-5)])
         np.testing.assert_allclose(q, ref, atol=1e-15, rtol=0)
+
+
+def test_multi_fragment_sweep_matches_per_fragment(T, monkeypatch):
+    """qk_sweep_compiled_multi (every fragment's pass r in one launch) == the per-fragment launch
+    sequence, bit for bit: syc 32 5 (fused label rows) and syc 32 1 (per-job rows)."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    for key, factored in (("syc_32_5_p2", True), ("syc_32_1_p2", False)):
+        name, n, d, p, var = cutting.BASELINE_CONFIGS[key]
+        _, cut, _ = cutting.config_cut_circuit(name, n, d, p, var)
+        monkeypatch.setenv("QKNIT_SWEEP_MULTI", "0")
+        ref = [q.clone() for q in KnitPipeline(VirtualCircuit(cut), factored=factored, jit=True).sweep()]
+        monkeypatch.setenv("QKNIT_SWEEP_MULTI", "1")
+        pipe = KnitPipeline(VirtualCircuit(cut), factored=factored, jit=True)
+        assert pipe._multi is not None
+        got = pipe.sweep()
+        T.cuda.synchronize()
+        assert all(T.equal(a, b) for a, b in zip(got, ref))

@@ -297,3 +297,23 @@ def test_label_chunks_cover_labels_without_splitting():
             assert j1 - j0 <= max_jobs or l1 == l0 + 1
             if nxt is not None:
                 assert nxt[0] == l1
+
+
+def test_generated_multi_fragment_kernels_compile_for_gfx950(tmp_path):
+    """generate_multi (both syc 32 5 fragments, 13-bit tiles, one kernel per pass round) compiles."""
+    import shutil
+    import subprocess
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import sweep_codegen
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    _, cut, _ = cutting.config_cut_circuit("syc", 32, 5, 2)
+    frags = engine.prepare_fragments(VirtualCircuit(cut), upload=False, basis=True)
+    encs = [sweep_plan.encode(fs.prog, tile_bits=13) for fs in frags]
+    src, names = sweep_codegen.generate_multi(encs)
+    assert len(names) == max(len(e.passes) for e in encs)
+    f = tmp_path / "m.hip"
+    f.write_text(src)
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-c",
+                        str(f), "-o", str(tmp_path / "m.o")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
