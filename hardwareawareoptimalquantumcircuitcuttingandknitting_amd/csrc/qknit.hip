@@ -779,6 +779,9 @@ __global__ __launch_bounds__(256, 2) void qk_gemm_keyed_kernel(GemmArgs g) {
 #ifndef QK_G2S
 #define QK_G2S 2
 #endif
+#ifndef QK_GLDS_WG_PER_CU
+#define QK_GLDS_WG_PER_CU 2  // persistent workgroups per CU (LDS: 2 x 73.7 KiB at G2K = 16, G2S = 2)
+#endif
 #ifndef QK_GEMM_PRIO
 #define QK_GEMM_PRIO 0  // raise wave priority around each k-step's MFMAs
 #endif
@@ -1168,7 +1171,7 @@ int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A,
     if (QK_GEMM_GLDS && !beta && M % GT == 0 && N % GT == 0 && K % G2K == 0 && K > 0 && aligned16) {
         int cus = 0;
         QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-        int64_t G = (int64_t)cus * 2;
+        int64_t G = (int64_t)cus * QK_GLDS_WG_PER_CU;
         G = G < 8 ? 8 : G - G % 8;
         if (G > nblk) G = nblk;
         hipLaunchKernelGGL(qk_gemm_glds_kernel, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
