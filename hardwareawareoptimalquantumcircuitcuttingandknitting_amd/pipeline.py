@@ -251,11 +251,13 @@ class KnitPipeline:
         self._plan_multi()
 
     def _plan_multi(self):
-        """Single mode: when every swept fragment runs compiled kernels of one tile width (2-4
-        fragments, not chunked), the whole sweep is one qk_sweep_compiled_multi call — pass round
-        r of all fragments in one launch — instead of a launch sequence per fragment."""
+        """Single and gather mode: when every swept fragment runs compiled kernels of one tile
+        width (2-4 fragments, not chunked), the whole sweep is one qk_sweep_compiled_multi call —
+        pass round r of all fragments in one launch — instead of a launch sequence per fragment.
+        In gather mode the collectives then start after the one sweep (a rank's shard is small:
+        one launch beats overlapping the row side's all_to_all with a second sweep)."""
         self._multi = None
-        if self.mode != "single" or os.environ.get("QKNIT_SWEEP_MULTI", "1") == "0":
+        if self.mode == "reduce" or os.environ.get("QKNIT_SWEEP_MULTI", "1") == "0":
             return
         if not hasattr(self.be, "plan_multi"):
             return
@@ -331,11 +333,19 @@ class KnitPipeline:
         if self._multi is not None and not self.fork:
             idx, plan = self._multi
             be.sweep_multi(plan)
-            for i, (fs, sw) in enumerate(zip(self.frags, self.sweeps)):
+            for i in sorted(range(len(self.frags)), key=lambda i: self.order.index(i)):
+                fs, sw = self.frags[i], self.sweeps[i]
                 if sw is None:
                     qs[i] = be.zeros((fs.n_rows, 1), T.float64) + 1.0
+                    continue
+                q = sw["q"] if sw["fused"] else sw["pjob"]
+                if self.mode == "gather":
+                    work, qs[i] = self._exchange(i, q)
+                    pending.append(work)
                 else:
-                    qs[i] = (sw["q"] if sw["fused"] else sw["pjob"])[: sw["n_local"]]
+                    qs[i] = q[: sw["n_local"]]
+            for work in pending:
+                work.wait()
             return qs
         fork = self.fork and self.mode == "single"
         main = T.cuda.current_stream() if fork else None
