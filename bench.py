@@ -35,6 +35,9 @@ def parse():
     ap.add_argument("--direct", action="store_true",
                     help="direct knit over all global labels (K = prod n_inst) instead of the "
                          "default rank-factored knit (K = 4^cuts; exact, same result)")
+    ap.add_argument("--no-light-cone", action="store_true",
+                    help="plain factored knit: no light-cone basis projections, no core rank "
+                         "compression (K = 4^cuts; exact, same result)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-north-star", action="store_true",
                     help="skip the syc 32 1 sweep-only measurement (north_star_sweep)")
@@ -192,7 +195,8 @@ def main():
     circ, cut, desc = cutting.config_cut_circuit(name, n, d, p, variant)
     virt = VirtualCircuit(cut)
     torch.cuda.set_device(local)
-    pipe = KnitPipeline(virt, device=local, factored=not args.direct, rank=rank, world=world)
+    pipe = KnitPipeline(virt, device=local, factored=not args.direct, rank=rank, world=world,
+                        light_cone=not args.no_light_cone)
     counts = pipe.instance_counts()
 
     def barrier():
@@ -226,7 +230,17 @@ def main():
     traffic = pipe.sweep_traffic()
     M, Nn, K = pipe.gemm_shape()
     flops = 2.0 * M * Nn * K
-    achieved = flops / (gemm_ms * 1e-3) / 1e12
+    # algorithmic bytes of the contraction: both operands read once, the output written once
+    gbytes = 8.0 * (M * Nn + K * (M + Nn))
+    t_mfma, t_hbm = flops / (FP64_MFMA_PEAK_TFLOPS * 1e12), gbytes / (HBM_PEAK_GBS * 1e9)
+    if t_mfma >= t_hbm:
+        roof = {"bound": "mfma", "achieved": flops / (gemm_ms * 1e-3) / 1e12, "peak": FP64_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s"}
+    else:
+        roof = {"bound": "hbm", "achieved": gbytes / (gemm_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    kernel = ("qk_gemm_smallk_kernel (knit outer product, output-write bound)" if K <= 8 else
+              "qk_gemm_glds_kernel (knit contraction, LDS-DMA ring)" if K % 16 == 0 else
+              "qk_gemm_keyed_kernel (knit contraction, register-staged)")
     if rank != 0:
         return
     ms_per_step = elapsed / args.steps * 1e3
@@ -251,21 +265,21 @@ def main():
             "instances_unique": counts["instances_unique"],
             "instances_swept": counts["instances_swept"],
             "branch_jobs": counts["branch_jobs"],
-            "labels": counts["labels"],
-            "knit": "direct" if args.direct else "factored",
+            "labels": counts["labels_ref"],
+            "knit": ("direct" if args.direct else
+                     "factored" + ("" if args.no_light_cone else ", light-cone basis + rank-compressed core")),
+            "knit_terms": {"labels": counts["labels_ref"], "factored": counts["terms_factored"], "contracted": K},
             "gemm_mnk": [M, Nn, K],
             "output_entries": 1 << pipe.N,
             "parallelism": f"labels x{world} ({pipe.mode})",
         },
         "roofline": {
-            "kernel": "qk_gemm_glds_kernel (knit contraction, LDS-DMA ring)",
-            "bound": "mfma",
-            "achieved": achieved,
-            "peak": FP64_MFMA_PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
+            "kernel": kernel,
+            **roof,
+            "frac": roof["achieved"] / roof["peak"],
             "traffic": traffic_per_launch(M, Nn, K),
             "flops_per_launch": flops,
+            "algorithmic_bytes_per_launch": gbytes,
             "avg_launch_ms": gemm_ms,
         },
         "sweep": {

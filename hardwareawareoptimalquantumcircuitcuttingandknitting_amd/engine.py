@@ -418,11 +418,12 @@ class FragmentState:
 
 
 def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = True,
-                      basis: bool = False, jit: bool | None = None) -> list[FragmentState]:
+                      basis: bool = False, jit: bool | None = None, relevance: bool = True) -> list[FragmentState]:
     """Compile every fragment, dedup its instances and expand them into branch jobs.
 
     ``basis=True`` (factored knit only) additionally sweeps a spanning set of instances
-    (``basis_reduce``); the knit transform folds the expansion back in. ``jit``: per-program
+    (``basis_reduce``, slot channels compared after the exact light-cone projections unless
+    ``relevance=False``); the knit transform folds the expansion back in. ``jit``: per-program
     sweep kernels for SPLIT programs — None: only for large sweeps (``_worth_compiling``),
     True: for every SPLIT program of at most 400 ops, False: never (interpreter kernel)."""
     circ = virt.circuit
@@ -439,7 +440,7 @@ def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = 
             unique, uidx = dedup_labels(prog, labels)
         else:
             unique, uidx = list(labels), np.arange(len(labels), dtype=np.int64)
-        red = basis_reduce(prog, unique) if (basis and dedup) else None
+        red = basis_reduce(prog, unique, relevance=relevance) if (basis and dedup) else None
         jobs = build_jobs(prog, red.labels if red is not None else unique)
         # run.py:49-58 drops a fragment whose get_counts() raises, i.e. when some instance of
         # it measures nothing at all (no data measurement and no config measurement).
@@ -454,8 +455,8 @@ def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = 
 
 def _worth_compiling(prog: FragmentProgram, jobs: JobTable) -> bool:
     """Per-program kernels pay their hiprtc compile (about 1 s per 100 ops) only on real work:
-    >= 2^24 amplitudes per sweep, and at most 400 ops (qft 16: 586 ops, 20 s, one instance)."""
-    return (jobs.n_jobs << prog.n) >= (1 << 24) and len(prog.ops) <= 400
+    >= 2^22 amplitudes per sweep, and at most 400 ops (qft 16: 586 ops, 20 s, one instance)."""
+    return (jobs.n_jobs << prog.n) >= (1 << 22) and len(prog.ops) <= 400
 
 
 def _some_label_unmeasured(prog: FragmentProgram, labels: list) -> bool:
@@ -501,6 +502,7 @@ class KnitOperands:
     transforms: list  # per fragment: None (gather) or dense [R, L_f] matrix (factored)
     clbits: list  # per included fragment: ascending global clbits of its outcome bits
     num_terms: int
+    factored_terms: int = 0  # factored knit: prod r_j before the core compression
 
     def key_table(self, i: int) -> np.ndarray:
         return deposit_keys(self.clbits[i])
@@ -514,7 +516,7 @@ def _affine_stride(clbits: list):
     return (1 << c0) if list(clbits) == list(range(c0, c0 + len(clbits))) else None
 
 
-def knit_operands(virt, frags: list[FragmentState], factored: bool = False) -> KnitOperands:
+def knit_operands(virt, frags: list[FragmentState], factored: bool = False, compress: bool = True) -> KnitOperands:
     vg = [v.operation for v in virt.vgate_instructions]
     space = LabelSpace([g.num_instantiations for g in vg], [g.knit_coefficients() for g in vg])
     clbits = [[] if fs.dropped else list(fs.prog.clbits) for fs in frags]
@@ -550,7 +552,27 @@ def knit_operands(virt, frags: list[FragmentState], factored: bool = False) -> K
         if fs.expand is not None:  # instances as combinations of the swept basis: W'' = W' E
             W = W @ fs.expand
         transforms.append(W)
-    return KnitOperands([None] * len(frags), [None] * len(frags), transforms, clbits, int(np.prod(ranks)))
+    terms = factored_terms = int(np.prod(ranks))
+    if compress and len(frags) == 2 and not any(fs.dropped for fs in frags):
+        transforms, terms = _compress_core(transforms, terms)
+    return KnitOperands([None] * len(frags), [None] * len(frags), transforms, clbits, terms, factored_terms)
+
+
+def _compress_core(transforms: list, terms: int, tol: float = 1e-10):
+    """Two fragments: ``R = A^T B = q_0^T (W_0^T W_1) q_1`` depends on the transforms only
+    through the core ``C = W_0^T W_1`` ([swept rows_0, swept rows_1]). With C = U S V^T of rank
+    r (the light-cone basis reduction makes it rank-deficient: syc 32 5 has 64 swept rows on
+    one side, so r <= 64 < 256 factored terms) the transforms become ``(U_r S_r)^T`` and
+    ``V_r^T``: the contraction dimension drops from ``prod r_j`` to r, same R up to rounding."""
+    W0, W1 = transforms
+    C = W0.T @ W1
+    if C.size == 0:
+        return transforms, terms
+    U, S, Vt = np.linalg.svd(C, full_matrices=False)
+    r = int((S > tol * S[0]).sum()) if S.size and S[0] > 0 else 0
+    if r == 0 or r >= terms:
+        return transforms, terms
+    return [np.ascontiguousarray((U[:, :r] * S[:r]).T), np.ascontiguousarray(Vt[:r])], r
 
 
 def _endpoints(virt, j):

@@ -326,15 +326,6 @@ def dedup_labels(prog: FragmentProgram, labels: list) -> tuple[list, np.ndarray]
     return unique, uidx
 
 
-def _superoperator(endpoint, inst_id: int) -> np.ndarray:
-    """Real 32-vector of the side program's signed channel ``rho -> sum_k s_k M_k rho M_k^+``
-    (the map a slot applies to the fragment state, config outcome folded as ``(-1)^m``)."""
-    phi = np.zeros((4, 4), dtype=np.complex128)
-    for mat, sign in side_branches(endpoint, inst_id):
-        phi += sign * np.kron(mat, mat.conj())
-    return np.concatenate([phi.real.ravel(), phi.imag.ravel()])
-
-
 @dataclass
 class BasisReduction:
     """Instances of a fragment expressed in a smaller spanning set of instances.
@@ -349,14 +340,84 @@ class BasisReduction:
     expand: np.ndarray  # [n_unique, n_basis] real
 
 
-def basis_reduce(prog: FragmentProgram, unique_labels: list, tol: float = 1e-12) -> BasisReduction | None:
+# vec(rho) of one qubit, row-major (index 2a + b for |a><b|): |0><0| and the diagonal
+_VEC_ZERO = np.diag([1.0, 0.0, 0.0, 0.0])
+_VEC_DIAG = np.diag([1.0, 0.0, 0.0, 1.0])
+
+
+def _superop(mat: np.ndarray) -> np.ndarray:
+    """``vec(M rho M^+) = kron(M, conj(M)) vec(rho)`` (row-major vec)."""
+    return np.kron(mat, mat.conj())
+
+
+def _z_commuting(op: HostOp, q: int, prog: FragmentProgram, insts_of: dict) -> bool:
+    """Whether ``op`` maps |a><b| on qubit ``q`` into |a><b|-blocks (commutes with Z_q): a gate
+    diagonal on q, or a slot whose every branch matrix (with its absorbed gates) is diagonal."""
+    if op.kind != "slot":
+        from .sweep_plan import _diag_qubits
+
+        return q in _diag_qubits(op)
+    s = prog.slots[op.slot]
+    for inst in insts_of[op.slot]:
+        for mat, _ in side_branches(s.endpoint, inst):
+            full = s.post @ mat @ s.pre
+            if full[0, 1] != 0 or full[1, 0] != 0:
+                return False
+    return True
+
+
+def slot_relevance(prog: FragmentProgram, unique_labels: list) -> list:
+    """Per slot, the projectors ``(P_in, P_out)`` on its qubit's vec(rho) with
+    ``q_f(..., Phi_s, ...) == q_f(..., P_out Phi_s P_in, ...)`` exactly, for every instantiation
+    of every slot (light-cone argument on the compiled op list):
+
+    * input: every op on the qubit before the slot commutes with Z there, so the qubit is still
+      |0><0| (``P_in = |0><0|``);
+    * output: every op on the qubit after the slot commutes with Z there (diagonal gates, CZ/CX
+      controls, diagonal slot branches), so coherences of the qubit never reach the final
+      Z-basis outcomes or the partial trace (``P_out`` = the diagonal).
+
+    Otherwise the identity. Both projections keep |a><b| blocks, so they compose across slots
+    on one qubit."""
+    insts_of = {}
+    for k, s in enumerate(prog.slots):
+        if isinstance(s.endpoint, BranchMeasure):
+            insts_of[k] = [0]
+        else:
+            insts_of[k] = list(dict.fromkeys(int(lab[s.vgate_idx]) for lab in unique_labels))
+    where = {op.slot: i for i, op in enumerate(prog.ops) if op.kind == "slot"}
+    out = []
+    for k, s in enumerate(prog.slots):
+        t, q = where[k], s.qubit
+        before = all(_z_commuting(op, q, prog, insts_of) for op in prog.ops[:t] if q in op.qubits)
+        after = all(_z_commuting(op, q, prog, insts_of) for op in prog.ops[t + 1:] if q in op.qubits)
+        out.append((_VEC_ZERO if before else np.eye(4), _VEC_DIAG if after else np.eye(4)))
+    return out
+
+
+def _slot_channel(s: SlotSpec, inst_id: int, rel) -> np.ndarray:
+    """Real 32-vector of the slot's projected channel ``P_out Post Phi_inst Pre P_in``."""
+    phi = np.zeros((4, 4), dtype=np.complex128)
+    for mat, sign in side_branches(s.endpoint, inst_id):
+        phi += sign * _superop(mat)
+    phi = rel[1] @ _superop(s.post) @ phi @ _superop(s.pre) @ rel[0]
+    return np.concatenate([phi.real.ravel(), phi.imag.ravel()])
+
+
+def basis_reduce(prog: FragmentProgram, unique_labels: list, tol: float = 1e-12,
+                 relevance: bool = True) -> BasisReduction | None:
     """Per slot, keep a maximal linearly independent subset of its side programs (fewest
     branch jobs first) and write every other program as a combination of it. Returns None
-    when that does not reduce the fragment's branch-job count."""
+    when that does not reduce the fragment's branch-job count.
+
+    ``relevance``: compare the slot channels after the exact light-cone projections of
+    :func:`slot_relevance` (programs that differ only in what the fragment's outcomes cannot
+    see become equal, and the basis shrinks)."""
     if not prog.slots or not unique_labels:
         return None
+    rels = slot_relevance(prog, unique_labels) if relevance else [(np.eye(4), np.eye(4))] * len(prog.slots)
     per_slot = []  # (representative inst ids of the basis, coefficient map inst -> row of D)
-    for s in prog.slots:
+    for s, rel in zip(prog.slots, rels):
         if isinstance(s.endpoint, BranchMeasure):
             per_slot.append(([0], {0: np.ones(1)}))
             continue
@@ -364,12 +425,14 @@ def basis_reduce(prog: FragmentProgram, unique_labels: list, tol: float = 1e-12)
         sig = {i: _side_signature(s.endpoint, i) for i in insts}
         reps = list({sig[i]: i for i in reversed(insts)}.values())[::-1]  # first inst per program
         nbr = {i: len(side_branches(s.endpoint, i)) for i in reps}
-        phis = {i: _superoperator(s.endpoint, i) for i in reps}
+        phis = {i: _slot_channel(s, i, rel) for i in reps}
         basis: list[int] = []
         for i in sorted(reps, key=lambda i: (nbr[i], reps.index(i))):
             cand = np.stack([phis[b] for b in basis + [i]], axis=1)
             if np.linalg.matrix_rank(cand, tol=tol) > len(basis):
                 basis.append(i)
+        if not basis:  # every program projects to the zero channel: q_f == 0 for all labels
+            basis = [reps[0]]
         basis.sort(key=reps.index)
         Bm = np.stack([phis[b] for b in basis], axis=1)
         coef = {}

@@ -87,8 +87,8 @@ class HipBackend:
         self.dev = self.T.device("cuda", device)
         self.ctx = engine.get_context(device)
 
-    def prepare_fragments(self, virt, basis: bool = False, jit: bool | None = None):
-        return engine.prepare_fragments(virt, self.device, basis=basis, jit=jit)
+    def prepare_fragments(self, virt, basis: bool = False, jit: bool | None = None, relevance: bool = True):
+        return engine.prepare_fragments(virt, self.device, basis=basis, jit=jit, relevance=relevance)
 
     def upload_jobs(self, jobs: JobTable):
         return engine.jobs_to_device(jobs, self.device)
@@ -160,7 +160,7 @@ class HipBackend:
 class KnitPipeline:
     def __init__(self, virt, device: int = 0, factored: bool = False, rank: int = 0, world: int = 1,
                  mode: str | None = None, group=None, backend=None, chunk_jobs: int | None = None,
-                 jit: bool | None = None):
+                 jit: bool | None = None, light_cone: bool = True):
         self.be = backend if backend is not None else HipBackend(device)
         # branch jobs per sweep chunk of a fused (compiled) fragment; 0 = the whole fragment at once
         self.chunk_jobs = int(os.environ.get("QKNIT_SWEEP_CHUNK_JOBS", "0")) if chunk_jobs is None else chunk_jobs
@@ -172,9 +172,14 @@ class KnitPipeline:
         self.virt = virt
         self.rank, self.world, self.group = rank, world, group
         self.factored = factored
-        self.frags = (self.be.prepare_fragments(virt, basis=factored) if jit is None
-                      else self.be.prepare_fragments(virt, basis=factored, jit=jit))
-        self.ops = engine.knit_operands(virt, self.frags, factored)
+        # light_cone (factored knit): exact light-cone projections in the basis reduction and the
+        # rank-compressed two-fragment core (fragment_program.slot_relevance,
+        # engine._compress_core); False keeps the plain factored knit (prod r_j terms)
+        kw = {} if light_cone else {"relevance": False}
+        if jit is not None:
+            kw["jit"] = jit
+        self.frags = self.be.prepare_fragments(virt, basis=factored, **kw)
+        self.ops = engine.knit_operands(virt, self.frags, factored, compress=light_cone)
         self.N = virt.circuit.num_clbits
         q_bytes = sum(len(fs.labels) << fs.prog.m for fs in self.frags) * 8
         out_bytes = (1 << self.N) * 8
@@ -504,6 +509,8 @@ class KnitPipeline:
             "instances_swept": int(sum(fs.n_rows for fs in self.frags)),
             "branch_jobs": int(sum(fs.jobs.n_jobs for fs in self.frags if not fs.dropped)),
             "labels": int(self.ops.num_terms),
+            "labels_ref": int(np.prod([v.operation.num_instantiations for v in self.virt.vgate_instructions])),
+            "terms_factored": int(self.ops.factored_terms or self.ops.num_terms),
         }
 
     def sweep_traffic(self) -> dict:

@@ -121,3 +121,38 @@ def partial_measure(seed: int = 3):
     qc.measure(2, 1)
     qc.measure(3, 2)
     return qc, cut_circuit(qc, CutSpec([[0, 1], [2, 3]], cut))
+
+
+def light_cone(seed: int = 13):
+    """Cuts whose slots the light-cone analysis projects (fragment_program.slot_relevance): a
+    cut on fresh |0> qubits (input projection), late cuts followed only by diagonal gates,
+    CZs and CX controls (output projection, also on a traced qubit), and a cut in the middle."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.circuit import ClassicalRegister
+    rng = random.Random(seed)
+    qr = QuantumRegister(6, "q")
+    cr = ClassicalRegister(5, "c")
+    qc = QuantumCircuit(qr, cr)
+    cuts = [len(qc.data)]
+    qc.cx(2, 3)  # both qubits still |0>
+    _rand_layer(qc, [0, 1, 4, 5], rng)
+    qc.cx(0, 1)
+    qc.cx(4, 5)
+    _rand_layer(qc, range(6), rng)
+    cuts.append(len(qc.data))
+    qc.cx(1, 4)  # middle
+    _rand_layer(qc, range(6), rng)
+    qc.cx(0, 2)
+    qc.cx(5, 3)
+    cuts.append(len(qc.data))
+    qc.cx(2, 3)  # late: afterwards q2 only controls / phases, q3 only diagonal gates
+    qc.rz(0.7, 2)
+    qc.cx(2, 1)
+    qc.cz(3, 5)
+    qc.t(3)
+    cuts.append(len(qc.data))
+    qc.cz(0, 4)  # late cut on the traced qubit 0
+    qc.s(0)
+    qc.cx(0, 1)
+    for i, q in enumerate([1, 2, 3, 4, 5]):
+        qc.measure(q, i)
+    return qc, cut_circuit(qc, CutSpec([[0, 1, 2], [3, 4, 5]], cuts))

@@ -25,8 +25,8 @@ class CpuBackend:
     def __init__(self):
         self.dev = torch.device("cpu")
 
-    def prepare_fragments(self, virt, basis: bool = False):
-        return engine.prepare_fragments(virt, upload=False, basis=basis)
+    def prepare_fragments(self, virt, basis: bool = False, relevance: bool = True):
+        return engine.prepare_fragments(virt, upload=False, basis=basis, relevance=relevance)
 
     def upload_jobs(self, jobs):
         return jobs.slot_mats, torch.from_numpy(jobs.sign.copy()), torch.from_numpy(jobs.label_offsets.copy())

@@ -245,7 +245,7 @@ def test_compiled_sweep_matches_interpreter(T):
     _, cut = cutting.config_cut_circuit("syc", 32, 5, 2)[:2]
     virt = VirtualCircuit(cut)
     ctx = engine.get_context(0)
-    for fs in engine.prepare_fragments(virt, 0, basis=True):
+    for fs in engine.prepare_fragments(virt, 0, basis=True, relevance=False):
         assert fs.dprog.module is not None, "SPLIT programs run as compiled kernels"
         slot_t, sign_t, _ = engine.jobs_to_device(fs.jobs, 0)
         jit, _ = engine.sweep_jobs(ctx, fs.dprog, slot_t, sign_t, fs.jobs.n_jobs)

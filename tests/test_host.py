@@ -32,6 +32,7 @@ CASES = {
     "move_gate": lambda: circuits.wire_cut(3, 2, extra_gate_cut=True),
     "three": lambda: circuits.three_fragment(),
     "partial": lambda: circuits.partial_measure(),
+    "light_cone": lambda: circuits.light_cone(),
     "bv": lambda: cutting.config_cut_circuit("bv", 5, 1)[:2],
     "hwe_p3": lambda: cutting.config_cut_circuit("hwe", 16, 1, 3)[:2],
 }
@@ -139,13 +140,39 @@ def test_basis_reduced_sweep_knits_to_oracle(case):
 
 def test_basis_reduction_counts_syc_32_5():
     """VirtualCX sides span 4 channels with 5 programs (z = s + sdg - id on the control side):
-    syc 32 5 sweeps 4^4 basis instances (625 branch jobs) per fragment instead of 625 (1296)."""
+    syc 32 5 sweeps 4^4 basis instances (625 branch jobs) per fragment instead of 625 (1296).
+    With the light-cone projections (slot_relevance) one fragment's late cut collapses further
+    (64 basis instances, 125 jobs), and the knit core W_0^T W_1 has rank 64: the contraction
+    runs over 64 terms instead of 4^4."""
     _, cut, _ = cutting.config_cut_circuit("syc", 32, 5, 2)
     virt = VirtualCircuit(cut)
-    for fs in engine.prepare_fragments(virt, upload=False, basis=True):
+    for fs in engine.prepare_fragments(virt, upload=False, basis=True, relevance=False):
         assert len(fs.unique_labels) == 625
         assert fs.n_rows == 256 and fs.jobs.n_jobs == 625
         assert fs.expand.shape == (625, 256)
+    frags = engine.prepare_fragments(virt, upload=False, basis=True)
+    assert [(fs.n_rows, fs.jobs.n_jobs) for fs in frags] == [(64, 125), (256, 625)]
+    assert engine.knit_operands(virt, frags, factored=True, compress=False).num_terms == 256
+    ops = engine.knit_operands(virt, frags, factored=True)
+    assert ops.num_terms == 64
+    assert [w.shape for w in ops.transforms] == [(64, 64), (64, 256)]
+
+
+def test_slot_relevance_projections_light_cone():
+    """The light-cone case projects inputs of the fresh-qubit cut and outputs of the late cuts
+    (incl. the traced qubit); its knit is checked against the oracle in the basis tests."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.fragment_program import slot_relevance
+
+    _, cut = CASES["light_cone"]()
+    virt = VirtualCircuit(cut)
+    frags = engine.prepare_fragments(virt, upload=False, basis=True)
+    kinds = set()
+    for fs in frags:
+        for p_in, p_out in slot_relevance(fs.prog, fs.unique_labels):
+            kinds.add((int(np.trace(p_in)), int(np.trace(p_out))))
+    assert (1, 4) in kinds and (4, 2) in kinds
+    full = engine.prepare_fragments(virt, upload=False, basis=True, relevance=False)
+    assert sum(fs.jobs.n_jobs for fs in frags) < sum(fs.jobs.n_jobs for fs in full)
 
 
 @pytest.mark.parametrize("case", ["cx_3cuts", "cp", "rzz", "move_gate", "three", "hwe_p3", "partial"])
