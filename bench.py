@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--no-light-cone", action="store_true",
                     help="plain factored knit: no light-cone basis projections, no core rank "
                          "compression (K = 4^cuts; exact, same result)")
+    ap.add_argument("--no-data-rank", action="store_true",
+                    help="contract the light-cone terms as they are (no per-step data-rank compression)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-north-star", action="store_true",
                     help="skip the syc 32 1 sweep-only measurement (north_star_sweep)")
@@ -196,7 +198,7 @@ def main():
     virt = VirtualCircuit(cut)
     torch.cuda.set_device(local)
     pipe = KnitPipeline(virt, device=local, factored=not args.direct, rank=rank, world=world,
-                        light_cone=not args.no_light_cone)
+                        light_cone=not args.no_light_cone, data_rank=False if args.no_data_rank else None)
     counts = pipe.instance_counts()
 
     def barrier():
@@ -238,7 +240,9 @@ def main():
                 "unit": "TFLOP/s"}
     else:
         roof = {"bound": "hbm", "achieved": gbytes / (gemm_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
-    kernel = ("qk_gemm_smallk_kernel (knit outer product, output-write bound)" if K <= 8 else
+    kernel = ("qk_gemm_smallk_kernel<true> (data-rank knit: keyed outer product, output-write bound)"
+              if K <= 8 and pipe.last_rank is not None else
+              "qk_gemm_smallk_kernel (knit outer product, output-write bound)" if K <= 8 else
               "qk_gemm_glds_kernel (knit contraction, LDS-DMA ring)" if K % 16 == 0 else
               "qk_gemm_keyed_kernel (knit contraction, register-staged)")
     if rank != 0:
@@ -267,8 +271,11 @@ def main():
             "branch_jobs": counts["branch_jobs"],
             "labels": counts["labels_ref"],
             "knit": ("direct" if args.direct else
-                     "factored" + ("" if args.no_light_cone else ", light-cone basis + rank-compressed core")),
-            "knit_terms": {"labels": counts["labels_ref"], "factored": counts["terms_factored"], "contracted": K},
+                     "factored" + ("" if args.no_light_cone else ", light-cone basis + rank-compressed core")
+                     + (", data-rank compressed per step" if pipe.data_rank else "")),
+            "knit_terms": {"labels": counts["labels_ref"], "factored": counts["terms_factored"],
+                           "light_cone": counts["labels"], "contracted": K,
+                           "data_rank": pipe.data_rank, "rank_fallbacks": pipe.rank_fallbacks},
             "gemm_mnk": [M, Nn, K],
             "output_entries": 1 << pipe.N,
             "parallelism": f"labels x{world} ({pipe.mode})",

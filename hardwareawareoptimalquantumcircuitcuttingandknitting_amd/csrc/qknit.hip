@@ -933,6 +933,10 @@ constexpr int SK_MAX = 8;
 #endif
 constexpr int SK_U = QK_SK_U;  // 512-output chunks per lane iteration
 
+// KEYED: the output column of B column j is keyB[j] (caller contract of qk_gemm_outer_paired:
+// keyB[2i + 1] = keyB[2i] + 1 and keyB[2i] even, i.e. the N side holds clbit 0), so each lane's
+// two adjacent outputs are still one 16-B store; the key table (512 KiB at N = 2^16) is L2-resident.
+template <bool KEYED>
 __global__ __launch_bounds__(256) void qk_gemm_smallk_kernel(GemmArgs g) {
     const int K = (int)g.K;
     for (int64_t row = blockIdx.x; row < g.M; row += gridDim.x) {
@@ -961,8 +965,10 @@ __global__ __launch_bounds__(256) void qk_gemm_smallk_kernel(GemmArgs g) {
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < SK_U; ++u)
-                    __builtin_nontemporal_store(acc[u], reinterpret_cast<d2_t*>(o + j0 + 512 * u));
+                for (int u = 0; u < SK_U; ++u) {
+                    const int64_t col = KEYED ? g.keyB[j0 + 512 * u] : j0 + 512 * u;
+                    __builtin_nontemporal_store(acc[u], reinterpret_cast<d2_t*>(o + col));
+                }
             }
             for (int64_t j = j0; j < g.N; j += 512) {
                 d2_t acc = {0.0, 0.0};
@@ -971,13 +977,13 @@ __global__ __launch_bounds__(256) void qk_gemm_smallk_kernel(GemmArgs g) {
                     acc.x = fma(a[k], b.x, acc.x);
                     acc.y = fma(a[k], b.y, acc.y);
                 }
-                __builtin_nontemporal_store(acc, reinterpret_cast<d2_t*>(o + j));
+                __builtin_nontemporal_store(acc, reinterpret_cast<d2_t*>(o + (KEYED ? g.keyB[j] : j)));
             }
         } else {
             for (int64_t j = threadIdx.x; j < g.N; j += 256) {
                 double acc = 0.0;
                 for (int k = 0; k < K; ++k) acc = fma(a[k], g.B[k * g.ldb + j], acc);
-                __builtin_nontemporal_store(acc, o + j);
+                __builtin_nontemporal_store(acc, o + (KEYED ? g.keyB[j] : j));
             }
         }
     }
@@ -1164,7 +1170,7 @@ int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A,
         int cus = 0;
         QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
         const int64_t G = M < (int64_t)cus * 8 ? M : (int64_t)cus * 8;
-        hipLaunchKernelGGL(qk_gemm_smallk_kernel, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
+        hipLaunchKernelGGL(qk_gemm_smallk_kernel<false>, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
         QK_HIP(ctx, hipGetLastError());
         return QK_OK;
     }
@@ -1192,6 +1198,26 @@ int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A,
     if (gy > 65535) return fail(ctx, QK_EARG, "qk_gemm_keyed: too many tiles%s");
     hipLaunchKernelGGL(qk_gemm_keyed_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, ctx->stream, g);
 #endif
+    QK_HIP(ctx, hipGetLastError());
+    return QK_OK;
+}
+
+int qk_gemm_outer_paired(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A, int64_t lda,
+                         const double* B, int64_t ldb, const int64_t* keyA, int64_t strideA,
+                         const int64_t* keyB, double* out) {
+    if (!ctx) return QK_EARG;
+    if (M < 0 || N < 0 || K < 1 || K > SK_MAX) return fail(ctx, QK_EARG, "qk_gemm_outer_paired: bad size%s");
+    if (M == 0 || N == 0) return QK_OK;
+    if (!out || !A || !B || !keyB) return fail(ctx, QK_EARG, "qk_gemm_outer_paired: null buffer%s");
+    if (lda < M || ldb < N) return fail(ctx, QK_EARG, "qk_gemm_outer_paired: leading dimension too small%s");
+    if ((N & 1) || (ldb & 1) || ((reinterpret_cast<uintptr_t>(B) | reinterpret_cast<uintptr_t>(out)) & 15))
+        return fail(ctx, QK_EARG, "qk_gemm_outer_paired: N, ldb even and 16-B aligned B/out required%s");
+    GemmArgs g{M, N, K, A, lda, B, ldb, keyA, strideA, keyB, 0, out, 0, 0, 0};
+    QK_HIP(ctx, hipSetDevice(ctx->device));
+    int cus = 0;
+    QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const int64_t G = M < (int64_t)cus * 8 ? M : (int64_t)cus * 8;
+    hipLaunchKernelGGL(qk_gemm_smallk_kernel<true>, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
     QK_HIP(ctx, hipGetLastError());
     return QK_OK;
 }

@@ -352,6 +352,28 @@ def gemm_keyed(ctx: Context, A, B, keyA=None, keyB=None, out=None, strideA: int 
     return out
 
 
+def gemm_outer_paired(ctx: Context, A, B, keyB, keyA=None, out=None, strideA: int = 0):
+    """Small-K (K <= 8) keyed outer product ``out[kA(i) + keyB[j]] = sum_k A[k, i] * B[k, j]``,
+    output-write bound (``qk_gemm_outer_paired``). ``keyB`` must pair adjacent outputs
+    (``keyB[2i+1] == keyB[2i] + 1``, ``keyB[2i]`` even): :func:`paired_keys` says when."""
+    K, M = A.shape
+    K2, N = B.shape
+    assert K == K2 and 1 <= K <= 8 and A.is_contiguous() and B.is_contiguous()
+    assert keyB.shape[0] == N and keyB.dtype == torch().int64
+    if keyA is not None:
+        assert keyA.shape[0] == M and keyA.dtype == torch().int64
+    ctx.check(ctx.lib.qk_gemm_outer_paired(ctx.handle, M, N, K, A.data_ptr(), M, B.data_ptr(), N,
+                                           _ptr(keyA), strideA, keyB.data_ptr(), out.data_ptr()),
+              "qk_gemm_outer_paired")
+    return out
+
+
+def paired_keys(clbits: list) -> bool:
+    """Whether a fragment's output keys (deposit into ascending ``clbits``) pair adjacent
+    outputs: true exactly when it holds clbit 0 (then key(2i + 1) = key(2i) + 1, key(2i) even)."""
+    return len(clbits) >= 1 and sorted(clbits)[0] == 0
+
+
 def khatri_rao(ctx: Context, A, B):
     T = torch()
     K, M = A.shape
@@ -573,6 +595,34 @@ def _compress_core(transforms: list, terms: int, tol: float = 1e-10):
     if r == 0 or r >= terms:
         return transforms, terms
     return [np.ascontiguousarray((U[:, :r] * S[:r]).T), np.ascontiguousarray(Vt[:r])], r
+
+
+def data_rank_factors(GA: np.ndarray, GB: np.ndarray, lam_tol: float = 1e-12, s_tol: float = 1e-13):
+    """Rank factors of a two-fragment knit ``R = A^T B`` from its Gram matrices.
+
+    ``GA = A A^T``, ``GB = B B^T`` ([K, K]). With ``GA = V_A L_A V_A^T`` (eigenvalues above
+    ``lam_tol * max`` kept), ``A^T V_A = Q_A L_A^{1/2}`` with orthonormal ``Q_A``, so
+    ``R ~= Q_A Y Q_B^T``, ``Y = L_A^{1/2} V_A^T V_B L_B^{1/2}``; the SVD ``Y = U S W^T``
+    truncated at ``s_tol * s_max`` gives ``R ~= A^T T_A^T T_B B`` with
+    ``T_A = (V_A L_A^{-1/2} U_r S_r^{1/2})^T`` and ``T_B = (V_B L_B^{-1/2} W_r S_r^{1/2})^T``
+    ([r, K] each). The dropped directions are checked by the caller on the real operands
+    (``KnitPipeline._rank_compress``), not trusted from the Grams. Returns None for R = 0."""
+    la, Va = np.linalg.eigh(0.5 * (GA + GA.T))
+    lb, Vb = np.linalg.eigh(0.5 * (GB + GB.T))
+    if la[-1] <= 0 or lb[-1] <= 0:
+        return None
+    ka, kb = la > lam_tol * la[-1], lb > lam_tol * lb[-1]
+    Va, la, Vb, lb = Va[:, ka], la[ka], Vb[:, kb], lb[kb]
+    sa, sb = np.sqrt(la), np.sqrt(lb)
+    Y = (sa[:, None] * (Va.T @ Vb)) * sb[None, :]
+    U, s, Wt = np.linalg.svd(Y)
+    if s.size == 0 or s[0] <= 0:
+        return None
+    r = int((s > s_tol * s[0]).sum())
+    rs = np.sqrt(s[:r])
+    TA = ((Va / sa) @ (U[:, :r] * rs)).T
+    TB = ((Vb / sb) @ (Wt[:r].T * rs)).T
+    return np.ascontiguousarray(TA), np.ascontiguousarray(TB)
 
 
 def _endpoints(virt, j):

@@ -36,6 +36,19 @@ from . import _lib, engine
 from .fragment_program import JobTable
 
 
+def _mm_nt(X, Y):
+    """``X @ Y.T`` for short-and-wide operands ([k1, L] x [k2, L], L up to 2^16): a plain GEMM
+    has a k1 x k2 output (one or two tiles) and walks L on a few workgroups; split L into
+    chunks of 256 as a batched GEMM (one output tile per chunk, whole GPU) and sum the chunks."""
+    L = X.shape[1]
+    nb = L // 256 if L % 256 == 0 else 1
+    if nb <= 1:
+        return X @ Y.T
+    Xb = X.view(X.shape[0], nb, 256).transpose(0, 1)
+    Yb = Y.reshape(Y.shape[0], nb, 256).transpose(0, 1)
+    return (Xb @ Yb.transpose(1, 2)).sum(0)
+
+
 def _shard(n: int, rank: int, world: int) -> tuple[int, int]:
     per = -(-n // world)
     lo = min(n, rank * per)
@@ -153,6 +166,9 @@ class HipBackend:
     def khatri_rao(self, A, B):
         return engine.khatri_rao(self.ctx, A, B)
 
+    def gemm_outer_paired(self, A, B, keyB, **kw):
+        return engine.gemm_outer_paired(self.ctx, A, B, keyB, **kw)
+
     def event(self):
         return self.T.cuda.Event(enable_timing=True)
 
@@ -160,7 +176,7 @@ class HipBackend:
 class KnitPipeline:
     def __init__(self, virt, device: int = 0, factored: bool = False, rank: int = 0, world: int = 1,
                  mode: str | None = None, group=None, backend=None, chunk_jobs: int | None = None,
-                 jit: bool | None = None, light_cone: bool = True):
+                 jit: bool | None = None, light_cone: bool = True, data_rank: bool | None = None):
         self.be = backend if backend is not None else HipBackend(device)
         # branch jobs per sweep chunk of a fused (compiled) fragment; 0 = the whole fragment at once
         self.chunk_jobs = int(os.environ.get("QKNIT_SWEEP_CHUNK_JOBS", "0")) if chunk_jobs is None else chunk_jobs
@@ -190,6 +206,17 @@ class KnitPipeline:
         if mode not in ("single", "reduce", "gather"):
             raise ValueError(f"unknown mode {mode}")
         self.mode = mode
+        # data_rank (single mode, factored, two fragments): each step compresses the two knit
+        # operands to the numerical rank of R = A^T B (engine.data_rank_factors), contracts with
+        # the output-write-bound small-K kernel, and verifies the result by random probes
+        # (falls back to the exact contraction if a probe exceeds rank_tol)
+        two = len(self.frags) == 2 and not any(fs.dropped for fs in self.frags)
+        ok = mode == "single" and factored and two
+        self.data_rank = ok if data_rank is None else (data_rank and ok)
+        self.rank_tol = 1e-14  # Frobenius-norm estimate of R - A''^T B'' (probabilities: |R| <= 1)
+        self.rank_fallbacks = 0
+        self.last_rank = None
+        self._probe = None
         self.events = []  # (start, end) events around the main contraction GEMM
         self.sweep_events = []  # (start, end) events around each step's sweep (all fragments)
         self.record_events = False
@@ -452,18 +479,76 @@ class KnitPipeline:
         mats = self.operands(qs)
         if self.out is None:
             self.out = self._alloc_out(mats)
+        low = self._rank_compress(mats) if self.data_rank else None
         if self.record_events:
             start, end = self.be.event(), self.be.event()
             start.record()
-        res = self._contract(mats)
+        res = self._contract_lowrank(low[0]) if low is not None else self._contract(mats)
         if self.record_events:
             end.record()
             self.events.append((start, end))
+        if low is not None and not float(low[1]) <= self.rank_tol:
+            # not numerically low-rank to the tolerance: exact contraction, and for every later step
+            self.data_rank = False
+            self.rank_fallbacks += 1
+            self.last_rank = None
+            res = self._contract(mats)
         if self.mode == "reduce":
             import torch.distributed as dist
 
             dist.reduce(res, dst=0, group=self.group)
         return res
+
+    def _rank_compress(self, mats):
+        """Two-fragment knit R = A^T B ([K, M], [K, N] operands) rewritten as A''^T B'' with
+        r = numerical rank of R rows (engine.data_rank_factors on the two K x K Gram matrices,
+        read back once per step). Returns ``(mats'', err)`` — err a device scalar: the largest
+        ||(R - A''^T B'') x||_2 over 8 fixed Gaussian probes x (an estimate of the Frobenius
+        norm of the error, computed directly in fp64, no Gram squaring) — or None when the
+        compression would not shrink K."""
+        T = self.T
+        ia, ib = self.order[0], self.order[-1]
+        A, B = mats[ia], mats[ib]
+        K = A.shape[0]
+        if self._probe is None or self._probe.shape[0] != B.shape[1]:
+            g = T.Generator().manual_seed(1234)
+            self._probe = T.randn((B.shape[1], 8), generator=g, dtype=T.float64).to(B.device)
+        ref = A.T @ _mm_nt(B, self._probe.T)
+        G = T.stack([_mm_nt(A, A), _mm_nt(B, B)]).cpu().numpy()
+        f = engine.data_rank_factors(G[0], G[1])
+        if f is None or f[0].shape[0] >= K:
+            self.last_rank = K
+            return None
+        TA, TB = (T.from_numpy(t).to(A.device) for t in f)
+        A2, B2 = (TA @ A).contiguous(), (TB @ B).contiguous()
+        err = (A2.T @ _mm_nt(B2, self._probe.T) - ref).norm(dim=0).max()
+        self.last_rank = A2.shape[0]
+        out = list(mats)
+        out[ia], out[ib] = A2, B2
+        return out, err
+
+    def _contract_lowrank(self, mats):
+        """Contraction of the rank-compressed pair: r <= 8 and the N side pairing adjacent
+        outputs (it holds clbit 0) -> the keyed small-K outer-product kernel (output-write
+        bound); otherwise the operands are zero-padded to a multiple of 16 terms for the MFMA
+        kernel."""
+        T = self.T
+        ia, ib = self.order[0], self.order[-1]
+        A, B = mats[ia], mats[ib]
+        r = A.shape[0]
+        cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
+        if r <= 8 and engine.paired_keys(cB) and hasattr(self.be, "gemm_outer_paired"):
+            st = engine._affine_stride(cA)
+            kA = None if st is not None else engine._device_keys(tuple(cA), None, None, A.device)
+            kB = engine._device_keys(tuple(cB), None, None, B.device)
+            return self.be.gemm_outer_paired(A, B, kB, keyA=kA, strideA=st or 0, out=self.out)
+        pad = (-r) % 16
+        if pad:
+            A = T.cat([A, A.new_zeros((pad, A.shape[1]))])
+            B = T.cat([B, B.new_zeros((pad, B.shape[1]))])
+        out = list(mats)
+        out[ia], out[ib] = A, B
+        return self._contract(out)
 
     def _alloc_out(self, mats):
         T = self.T
@@ -549,7 +634,7 @@ class KnitPipeline:
 
     def gemm_shape(self) -> tuple[int, int, int]:
         """(M, N, K) of the main contraction on this rank."""
-        K = self.term_range[1] - self.term_range[0]
+        K = self.term_range[1] - self.term_range[0] if self.last_rank is None else self.last_rank
         widths = [1 << len(c) for c in self.ops.clbits]
         M = 1
         for i in self.order[:-1]:

@@ -149,6 +149,16 @@ int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A,
                   const double* B, int64_t ldb, const int64_t* keyA, int64_t strideA,
                   const int64_t* keyB, int64_t strideB, double* out, int beta);
 
+/* Small-K keyed outer product, output-write bound (1 <= K <= 8): the same result as
+ * qk_gemm_keyed with beta = 0, for a key table whose column pairs are adjacent outputs:
+ * keyB[2i + 1] == keyB[2i] + 1 and keyB[2i] even (the N side holds clbit 0; the caller checks,
+ * the kernel writes each pair with one 16-B store). N even; B and out 16-B aligned. Used for the
+ * data-rank-compressed two-fragment knit (pipeline.KnitPipeline); replaces the same
+ * merge + knit as qk_gemm_keyed (virtual_circuit.py:50-68,165-171, quasi_distr.py:55-60). */
+int qk_gemm_outer_paired(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A, int64_t lda,
+                         const double* B, int64_t ldb, const int64_t* keyA, int64_t strideA,
+                         const int64_t* keyB, double* out);
+
 /* out[k][i + j*M] = A[k*lda + i] * B[k*ldb + j] */
 int qk_khatri_rao(qk_ctx* ctx, int64_t K, int64_t M, int64_t N, const double* A, int64_t lda,
                   const double* B, int64_t ldb, double* out);

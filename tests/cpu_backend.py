@@ -69,6 +69,11 @@ class CpuBackend:
             o[idx] = C.reshape(-1)
         return out
 
+    def gemm_outer_paired(self, A, B, keyB, keyA=None, strideA=0, out=None):
+        kb = keyB.numpy()
+        assert A.shape[0] <= 8 and (kb[1::2] == kb[0::2] + 1).all() and (kb[0::2] % 2 == 0).all()
+        return self.gemm_keyed(A, B, keyA=keyA, strideA=strideA, keyB=keyB, out=out)
+
     def khatri_rao(self, A, B):
         K = A.shape[0]
         return torch.stack([torch.outer(B[k], A[k]).reshape(-1) for k in range(K)])

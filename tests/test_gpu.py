@@ -535,3 +535,56 @@ def test_multi_fragment_sweep_matches_per_fragment(T, monkeypatch):
         got = pipe.sweep()
         T.cuda.synchronize()
         assert all(T.equal(a, b) for a, b in zip(got, ref))
+
+
+@pytest.mark.parametrize("K,odd_rows", [(1, False), (2, False), (5, True), (8, False)])
+def test_gemm_outer_paired_matches_torch(T, K, odd_rows):
+    """qk_gemm_outer_paired: K <= 8 keyed outer product, N side = deposit keys of a fragment
+    holding clbit 0 (adjacent column pairs), A side keyed (or affine with an odd stride, which
+    breaks 16-B row alignment and takes the scalar path)."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.knit_plan import deposit_keys
+
+    ctx = engine.get_context(0)
+    bits_b = [0, 1, 2, 5, 6, 9]  # holds clbit 0
+    bits_a = [3, 4, 7, 8, 10]
+    assert engine.paired_keys(bits_b)
+    M, N = 1 << len(bits_a), 1 << len(bits_b)
+    g = T.Generator(device="cuda").manual_seed(17 + K)
+    A = T.randn(K, M, dtype=T.float64, device="cuda", generator=g)
+    B = T.randn(K, N, dtype=T.float64, device="cuda", generator=g)
+    kb = T.from_numpy(deposit_keys(bits_b)).cuda()
+    ref = (A.T @ B)
+    if odd_rows:
+        stride = (1 << 11) + 1
+        out = T.full((M * stride + N,), float("nan"), dtype=T.float64, device="cuda")
+        engine.gemm_outer_paired(ctx, A, B, kb, strideA=stride, out=out)
+        ka = T.arange(M, device="cuda", dtype=T.int64) * stride
+    else:
+        ka = T.from_numpy(deposit_keys(bits_a)).cuda()
+        out = T.full((1 << 11,), float("nan"), dtype=T.float64, device="cuda")
+        engine.gemm_outer_paired(ctx, A, B, kb, keyA=ka, out=out)
+    T.cuda.synchronize()
+    got = out[(ka[:, None] + kb[None, :]).reshape(-1)].view(M, N)
+    assert float((got - ref).abs().max()) <= 1e-12 * K
+
+
+@pytest.mark.slow
+def test_syc_32_5_data_rank_step_matches_exact_step(T):
+    """The bench step (factored knit, light-cone basis, data-rank compression: the rank-64
+    contraction becomes a rank <= 8 keyed outer product) equals the exact rank-64 MFMA
+    contraction entry for entry (1e-12) over all 2^32 outputs, with no probe fallback."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    cut = cutting.config_cut_circuit("syc", 32, 5, 2, "ref")[1]
+    pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
+    assert pipe.data_rank
+    got = pipe.step()
+    T.cuda.synchronize()
+    assert pipe.rank_fallbacks == 0 and pipe.last_rank is not None and pipe.last_rank <= 8
+    exact = KnitPipeline(VirtualCircuit(cut), factored=True, data_rank=False)
+    ref = exact.step()
+    T.cuda.synchronize()
+    assert _chunked_max_abs_diff(got, ref) <= 1e-12
+    assert abs(float(got.sum()) - 1.0) <= 1e-10
+    del pipe, exact, got, ref
+    T.cuda.empty_cache()
