@@ -240,8 +240,10 @@ def main():
                 "unit": "TFLOP/s"}
     else:
         roof = {"bound": "hbm", "achieved": gbytes / (gemm_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
-    kernel = ("qk_gemm_smallk_kernel<true> (data-rank knit: keyed outer product, output-write bound)"
-              if K <= 8 and pipe.last_rank is not None else
+    kernel = ("qk_knit_outer_stream_kernel (data-rank knit written in output order, output-write bound)"
+              if pipe.last_kernel == "qk_knit_outer_stream_kernel" else
+              "qk_gemm_smallk_kernel<true> (data-rank knit: keyed outer product, output-write bound)"
+              if pipe.last_kernel == "qk_gemm_smallk_kernel<true>" else
               "qk_gemm_smallk_kernel (knit outer product, output-write bound)" if K <= 8 else
               "qk_gemm_glds_kernel (knit contraction, LDS-DMA ring)" if K % 16 == 0 else
               "qk_gemm_keyed_kernel (knit contraction, register-staged)")

@@ -989,6 +989,96 @@ __global__ __launch_bounds__(256) void qk_gemm_smallk_kernel(GemmArgs g) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// small-K knit as a streaming write (two fragments whose clbits cover all N output bits):
+// out[o] = sum_k A[k][pext(o, maskA)] * B[k][pext(o, maskB)] for every o < 2^N, walked in output
+// order, so each wave's 16-B nontemporal stores form one contiguous 1-KiB run (the keyed kernel
+// above scatters a row over 128-B runs 2 KiB apart). Row / column indices come from per-byte pext
+// tables in LDS (4 x 256 entries per side). Operands (K x 2^16 fp64 at syc 32 5: 1 MiB per side
+// at K = 2) are L2-resident gathers.
+// ------------------------------------------------------------------------------------------
+#ifndef QK_OS_U
+#define QK_OS_U 1  // 16-B stores per lane per iteration (syc 32 5, K = 2: U = 1 / 2 / 4 = 6.4-6.5 /
+                   // 6.4-6.5 / 7.3-7.4 ms; 8 workgroups per CU vs 4 / 16 within noise; plain
+                   // stores 7.2 ms; torch fill_ of the same 2^32 fp64 = 5.1 ms)
+#endif
+#ifndef QK_OS_NT
+#define QK_OS_NT 1  // nontemporal output stores
+#endif
+#ifndef QK_OS_WG_PER_CU
+#define QK_OS_WG_PER_CU 8
+#endif
+constexpr int OS_U = QK_OS_U;
+constexpr int64_t OS_CHUNK = 2 * 256 * OS_U;  // outputs per workgroup iteration
+
+struct OuterStreamArgs {
+    int nbits, K;
+    const double* __restrict__ A;
+    int64_t lda;
+    const double* __restrict__ B;
+    int64_t ldb;
+    uint32_t maskA, maskB;
+    double* __restrict__ out;
+};
+
+__device__ __forceinline__ uint32_t pext32(uint32_t x, uint32_t mask) {
+    uint32_t r = 0, bit = 1;
+    for (; mask; mask &= mask - 1, bit <<= 1)
+        if (x & mask & (~mask + 1)) r |= bit;
+    return r;
+}
+
+__global__ __launch_bounds__(256) void qk_knit_outer_stream_kernel(OuterStreamArgs a) {
+    __shared__ uint32_t tab[2][4][256];  // [side][byte][value] -> that byte's pext contribution
+    for (int i = threadIdx.x; i < 4 * 256; i += 256) {
+        const int byte = i >> 8, v = i & 255;
+        tab[0][byte][v] = pext32((uint32_t)v << (8 * byte), a.maskA);
+        tab[1][byte][v] = pext32((uint32_t)v << (8 * byte), a.maskB);
+    }
+    __syncthreads();
+    const int K = a.K;
+    const int64_t total = int64_t(1) << a.nbits;
+    for (int64_t c0 = (int64_t)blockIdx.x * OS_CHUNK; c0 < total; c0 += (int64_t)gridDim.x * OS_CHUNK) {
+        d2_t v[OS_U];
+#pragma unroll
+        for (int u = 0; u < OS_U; ++u) {
+            const int64_t o = c0 + 512 * u + 2 * threadIdx.x;
+            const uint32_t x = (uint32_t)o;
+            uint32_t row = 0, col = 0;
+#pragma unroll
+            for (int byte = 0; byte < 4; ++byte) {
+                const uint32_t b = (x >> (8 * byte)) & 255;
+                row += tab[0][byte][b];
+                col += tab[1][byte][b];
+            }
+            d2_t acc = {0.0, 0.0};
+            if (o < total) {
+#pragma unroll
+                for (int k = 0; k < SK_MAX; ++k) {
+                    if (k < K) {
+                        const double av = a.A[k * a.lda + row];
+                        const d2_t bv = *reinterpret_cast<const d2_t*>(a.B + k * a.ldb + col);
+                        acc.x = fma(av, bv.x, acc.x);
+                        acc.y = fma(av, bv.y, acc.y);
+                    }
+                }
+            }
+            v[u] = acc;
+        }
+#pragma unroll
+        for (int u = 0; u < OS_U; ++u) {
+            const int64_t o = c0 + 512 * u + 2 * threadIdx.x;
+            if (o < total) {
+#if QK_OS_NT
+                __builtin_nontemporal_store(v[u], reinterpret_cast<d2_t*>(a.out + o));
+#else
+                *reinterpret_cast<d2_t*>(a.out + o) = v[u];
+#endif
+            }
+        }
+    }
+}
+
 __global__ void qk_khatri_rao_kernel(int64_t K, int64_t M, int64_t N, const double* __restrict__ A,
                                      int64_t lda, const double* __restrict__ B, int64_t ldb,
                                      double* __restrict__ out) {
@@ -1218,6 +1308,30 @@ int qk_gemm_outer_paired(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const dou
     QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     const int64_t G = M < (int64_t)cus * 8 ? M : (int64_t)cus * 8;
     hipLaunchKernelGGL(qk_gemm_smallk_kernel<true>, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
+    QK_HIP(ctx, hipGetLastError());
+    return QK_OK;
+}
+
+int qk_knit_outer_stream(qk_ctx* ctx, int nbits, int64_t K, const double* A, int64_t lda, const double* B,
+                         int64_t ldb, uint64_t maskA, uint64_t maskB, double* out) {
+    if (!ctx) return QK_EARG;
+    if (nbits < 2 || nbits > 32 || K < 1 || K > SK_MAX)
+        return fail(ctx, QK_EARG, "qk_knit_outer_stream: need 2 <= nbits <= 32, 1 <= K <= 8%s");
+    const uint64_t full = (uint64_t(1) << nbits) - 1;
+    if ((maskA & maskB) || (maskA | maskB) != full || !(maskB & 1))
+        return fail(ctx, QK_EARG, "qk_knit_outer_stream: masks must be disjoint, cover all bits, bit 0 in B%s");
+    if (!out || !A || !B) return fail(ctx, QK_EARG, "qk_knit_outer_stream: null buffer%s");
+    const int64_t M = int64_t(1) << __builtin_popcountll(maskA), N = int64_t(1) << __builtin_popcountll(maskB);
+    if (lda < M || ldb < N || (ldb & 1) || ((reinterpret_cast<uintptr_t>(B) | reinterpret_cast<uintptr_t>(out)) & 15))
+        return fail(ctx, QK_EARG, "qk_knit_outer_stream: leading dimension / alignment%s");
+    QK_HIP(ctx, hipSetDevice(ctx->device));
+    int cus = 0;
+    QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const int64_t chunks = (int64_t(1) << nbits) / OS_CHUNK;
+    const int64_t G0 = (int64_t)cus * QK_OS_WG_PER_CU;
+    const int64_t G = chunks < 1 ? 1 : (chunks < G0 ? chunks : G0);
+    OuterStreamArgs a{nbits, (int)K, A, lda, B, ldb, (uint32_t)maskA, (uint32_t)maskB, out};
+    hipLaunchKernelGGL(qk_knit_outer_stream_kernel, dim3((unsigned)G), dim3(256), 0, ctx->stream, a);
     QK_HIP(ctx, hipGetLastError());
     return QK_OK;
 }

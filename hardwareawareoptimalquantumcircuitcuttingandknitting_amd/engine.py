@@ -368,6 +368,29 @@ def gemm_outer_paired(ctx: Context, A, B, keyB, keyA=None, out=None, strideA: in
     return out
 
 
+def knit_outer_stream(ctx: Context, A, B, clbits_a: list, clbits_b: list, nbits: int, out):
+    """Two-fragment small-K knit written in output order (``qk_knit_outer_stream``):
+    ``out[o] = sum_k A[k, pext(o, mask_a)] * B[k, pext(o, mask_b)]`` for every ``o < 2^nbits``.
+    Needs the fragments' clbits to split ``0..nbits-1`` with clbit 0 on the B side
+    (:func:`stream_knit_ok`)."""
+    K, M = A.shape
+    K2, N = B.shape
+    assert K == K2 and 1 <= K <= 8 and A.is_contiguous() and B.is_contiguous()
+    mA, mB = sum(1 << c for c in clbits_a), sum(1 << c for c in clbits_b)
+    assert M == 1 << len(clbits_a) and N == 1 << len(clbits_b) and out.numel() >= 1 << nbits
+    ctx.check(ctx.lib.qk_knit_outer_stream(ctx.handle, nbits, K, A.data_ptr(), M, B.data_ptr(), N, mA, mB,
+                                           out.data_ptr()), "qk_knit_outer_stream")
+    return out
+
+
+def stream_knit_ok(clbits_a: list, clbits_b: list, nbits: int) -> bool:
+    """Whether :func:`knit_outer_stream` applies: the two clbit sets partition ``0..nbits-1``
+    (2 <= nbits <= 32) and clbit 0 is on the B side."""
+    a, b = set(clbits_a), set(clbits_b)
+    return (2 <= nbits <= 32 and not (a & b) and (a | b) == set(range(nbits)) and 0 in b
+            and len(a) == len(clbits_a) and len(b) == len(clbits_b))
+
+
 def paired_keys(clbits: list) -> bool:
     """Whether a fragment's output keys (deposit into ascending ``clbits``) pair adjacent
     outputs: true exactly when it holds clbit 0 (then key(2i + 1) = key(2i) + 1, key(2i) even)."""

@@ -169,6 +169,9 @@ class HipBackend:
     def gemm_outer_paired(self, A, B, keyB, **kw):
         return engine.gemm_outer_paired(self.ctx, A, B, keyB, **kw)
 
+    def knit_outer_stream(self, A, B, clbits_a, clbits_b, nbits, out):
+        return engine.knit_outer_stream(self.ctx, A, B, clbits_a, clbits_b, nbits, out)
+
     def event(self):
         return self.T.cuda.Event(enable_timing=True)
 
@@ -216,6 +219,7 @@ class KnitPipeline:
         self.rank_tol = 1e-14  # Frobenius-norm estimate of R - A''^T B'' (probabilities: |R| <= 1)
         self.rank_fallbacks = 0
         self.last_rank = None
+        self.last_kernel = None  # kernel of the last compressed contraction (None: qk_gemm_keyed)
         self._probe = None
         self.events = []  # (start, end) events around the main contraction GEMM
         self.sweep_events = []  # (start, end) events around each step's sweep (all fragments)
@@ -528,20 +532,27 @@ class KnitPipeline:
         return out, err
 
     def _contract_lowrank(self, mats):
-        """Contraction of the rank-compressed pair: r <= 8 and the N side pairing adjacent
-        outputs (it holds clbit 0) -> the keyed small-K outer-product kernel (output-write
-        bound); otherwise the operands are zero-padded to a multiple of 16 terms for the MFMA
+        """Contraction of the rank-compressed pair, r <= 8: the two fragments' clbits partition
+        the output bits (clbit 0 on the N side) -> the streaming small-K knit (output order,
+        contiguous stores); else the N side pairing adjacent outputs -> the keyed small-K outer
+        product (both output-write bound); otherwise the operands are zero-padded to a multiple of 16 terms for the MFMA
         kernel."""
         T = self.T
         ia, ib = self.order[0], self.order[-1]
         A, B = mats[ia], mats[ib]
         r = A.shape[0]
         cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
+        stream = os.environ.get("QKNIT_OUTER", "stream") == "stream"  # "paired": keyed kernel (A/B timing)
+        if stream and r <= 8 and engine.stream_knit_ok(cA, cB, self.N) and hasattr(self.be, "knit_outer_stream"):
+            self.last_kernel = "qk_knit_outer_stream_kernel"
+            return self.be.knit_outer_stream(A, B, cA, cB, self.N, self.out)
         if r <= 8 and engine.paired_keys(cB) and hasattr(self.be, "gemm_outer_paired"):
             st = engine._affine_stride(cA)
             kA = None if st is not None else engine._device_keys(tuple(cA), None, None, A.device)
             kB = engine._device_keys(tuple(cB), None, None, B.device)
+            self.last_kernel = "qk_gemm_smallk_kernel<true>"
             return self.be.gemm_outer_paired(A, B, kB, keyA=kA, strideA=st or 0, out=self.out)
+        self.last_kernel = None
         pad = (-r) % 16
         if pad:
             A = T.cat([A, A.new_zeros((pad, A.shape[1]))])

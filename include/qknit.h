@@ -159,6 +159,15 @@ int qk_gemm_outer_paired(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const dou
                          const double* B, int64_t ldb, const int64_t* keyA, int64_t strideA,
                          const int64_t* keyB, double* out);
 
+/* Small-K two-fragment knit as one streaming write over all 2^nbits outputs (nbits <= 32,
+ * 1 <= K <= 8): out[o] = sum_k A[k*lda + pext(o, maskA)] * B[k*ldb + pext(o, maskB)], where
+ * maskA / maskB are the two fragments' clbit masks (disjoint, covering bits 0..nbits-1, bit 0 in
+ * maskB; pext = the outcome index of the fragment's bits). Same result as qk_gemm_outer_paired with
+ * deposit key tables; written in output order (contiguous 1-KiB runs per wave store). B and out
+ * 16-B aligned, ldb even. Replaces the same merge + knit (virtual_circuit.py:50-68,165-171). */
+int qk_knit_outer_stream(qk_ctx* ctx, int nbits, int64_t K, const double* A, int64_t lda, const double* B,
+                         int64_t ldb, uint64_t maskA, uint64_t maskB, double* out);
+
 /* out[k][i + j*M] = A[k*lda + i] * B[k*ldb + j] */
 int qk_khatri_rao(qk_ctx* ctx, int64_t K, int64_t M, int64_t N, const double* A, int64_t lda,
                   const double* B, int64_t ldb, double* out);

@@ -588,3 +588,28 @@ def test_syc_32_5_data_rank_step_matches_exact_step(T):
     assert abs(float(got.sum()) - 1.0) <= 1e-10
     del pipe, exact, got, ref
     T.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("K,bits_b", [(1, [0, 1, 2, 5, 6, 9]), (2, [0, 3, 4, 5, 10]), (8, [0, 1, 2, 3, 8, 9, 10])])
+def test_knit_outer_stream_matches_torch(T, K, bits_b):
+    """qk_knit_outer_stream: the small-K two-fragment knit written in output order equals
+    A^T B scattered through the deposit keys of the two clbit sets (11 output bits; partial
+    last chunk and several interleavings)."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.knit_plan import deposit_keys
+
+    ctx = engine.get_context(0)
+    nbits = 11
+    bits_a = [b for b in range(nbits) if b not in bits_b]
+    assert engine.stream_knit_ok(bits_a, bits_b, nbits)
+    M, N = 1 << len(bits_a), 1 << len(bits_b)
+    g = T.Generator(device="cuda").manual_seed(29 + K)
+    A = T.randn(K, M, dtype=T.float64, device="cuda", generator=g)
+    B = T.randn(K, N, dtype=T.float64, device="cuda", generator=g)
+    out = T.full((1 << nbits,), float("nan"), dtype=T.float64, device="cuda")
+    engine.knit_outer_stream(ctx, A, B, bits_a, bits_b, nbits, out)
+    T.cuda.synchronize()
+    ka = T.from_numpy(deposit_keys(bits_a)).cuda()
+    kb = T.from_numpy(deposit_keys(bits_b)).cuda()
+    got = out[(ka[:, None] + kb[None, :]).reshape(-1)].view(M, N)
+    assert not bool(out.isnan().any())
+    assert float((got - A.T @ B).abs().max()) <= 1e-12 * K
