@@ -620,13 +620,15 @@ def _compress_core(transforms: list, terms: int, tol: float = 1e-10):
     return [np.ascontiguousarray((U[:, :r] * S[:r]).T), np.ascontiguousarray(Vt[:r])], r
 
 
-def data_rank_factors(GA: np.ndarray, GB: np.ndarray, lam_tol: float = 1e-12, s_tol: float = 1e-13):
+def data_rank_factors(GA: np.ndarray, GB: np.ndarray, lam_tol: float = 1e-12, s_tol: float = 1e-13,
+                      s_abs: float = 1e-15):
     """Rank factors of a two-fragment knit ``R = A^T B`` from its Gram matrices.
 
     ``GA = A A^T``, ``GB = B B^T`` ([K, K]). With ``GA = V_A L_A V_A^T`` (eigenvalues above
     ``lam_tol * max`` kept), ``A^T V_A = Q_A L_A^{1/2}`` with orthonormal ``Q_A``, so
     ``R ~= Q_A Y Q_B^T``, ``Y = L_A^{1/2} V_A^T V_B L_B^{1/2}``; the SVD ``Y = U S W^T``
-    truncated at ``s_tol * s_max`` gives ``R ~= A^T T_A^T T_B B`` with
+    truncated at ``max(s_tol * s_max, s_abs)`` (a dropped singular value moves entries of R by at
+    most itself; ``s_abs`` = 1e-15 is three orders below the 1e-12 per-entry tolerance) gives ``R ~= A^T T_A^T T_B B`` with
     ``T_A = (V_A L_A^{-1/2} U_r S_r^{1/2})^T`` and ``T_B = (V_B L_B^{-1/2} W_r S_r^{1/2})^T``
     ([r, K] each). The dropped directions are checked by the caller on the real operands
     (``KnitPipeline._rank_compress``), not trusted from the Grams. Returns None for R = 0."""
@@ -641,7 +643,12 @@ def data_rank_factors(GA: np.ndarray, GB: np.ndarray, lam_tol: float = 1e-12, s_
     U, s, Wt = np.linalg.svd(Y)
     if s.size == 0 or s[0] <= 0:
         return None
-    r = int((s > s_tol * s[0]).sum())
+    r = int((s > max(s_tol * s[0], s_abs)).sum())
+    if os.environ.get("QKNIT_DEBUG_RANK"):
+        print(f"data_rank: kept eig {int(ka.sum())}/{ka.size}, {int(kb.sum())}/{kb.size}; core svals "
+              f"{np.array2string(s[:10], precision=2)} -> r = {r}", flush=True)
+    if r == 0:
+        return None
     rs = np.sqrt(s[:r])
     TA = ((Va / sa) @ (U[:, :r] * rs)).T
     TB = ((Vb / sb) @ (Wt[:r].T * rs)).T

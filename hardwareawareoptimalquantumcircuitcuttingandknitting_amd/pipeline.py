@@ -214,7 +214,7 @@ class KnitPipeline:
         # the output-write-bound small-K kernel, and verifies the result by random probes
         # (falls back to the exact contraction if a probe exceeds rank_tol)
         two = len(self.frags) == 2 and not any(fs.dropped for fs in self.frags)
-        ok = mode == "single" and factored and two
+        ok = mode in ("single", "gather") and factored and two
         self.data_rank = ok if data_rank is None else (data_rank and ok)
         self.rank_tol = 1e-14  # Frobenius-norm estimate of R - A''^T B'' (probabilities: |R| <= 1)
         self.rank_fallbacks = 0
@@ -513,6 +513,9 @@ class KnitPipeline:
         T = self.T
         ia, ib = self.order[0], self.order[-1]
         A, B = mats[ia], mats[ib]
+        if self.mode == "gather" and not self.split_a:  # this rank's block of output rows
+            lo, hi = self.row_block
+            A = A[:, lo:hi].contiguous()
         K = A.shape[0]
         if self._probe is None or self._probe.shape[0] != B.shape[1]:
             g = T.Generator().manual_seed(1234)
@@ -541,6 +544,14 @@ class KnitPipeline:
         ia, ib = self.order[0], self.order[-1]
         A, B = mats[ia], mats[ib]
         r = A.shape[0]
+        if self.mode == "gather":  # compact [rows, 2^m_B] block: affine keys, K <= 8 -> small-K kernel
+            pad = (-r) % 16 if r > 8 else 0
+            if pad:
+                A = T.cat([A, A.new_zeros((pad, A.shape[1]))])
+                B = T.cat([B, B.new_zeros((pad, B.shape[1]))])
+            self.last_kernel = "qk_gemm_smallk_kernel" if r <= 8 else None
+            return self.be.gemm_keyed(A.contiguous(), B.contiguous(), keyA=None, strideA=B.shape[1], keyB=None,
+                                      strideB=1, out=self.out)
         cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
         stream = os.environ.get("QKNIT_OUTER", "stream") == "stream"  # "paired": keyed kernel (A/B timing)
         if stream and r <= 8 and engine.stream_knit_ok(cA, cB, self.N) and hasattr(self.be, "knit_outer_stream"):

@@ -71,7 +71,7 @@ def _worker(rank, world, port, case, mode, factored, q):
             dist.reduce(t, dst=0)
             res = t.numpy()
         if rank == 0:
-            q.put((pipe.mode, res))
+            q.put((pipe.mode, res, pipe.data_rank, pipe.last_rank, pipe.ops.num_terms))
     finally:
         dist.destroy_process_group()
 
@@ -93,11 +93,14 @@ def test_multi_rank_pipeline_matches_oracle(case, mode, factored, world):
              for r in range(world)]
     for p in procs:
         p.start()
-    got_mode, res = q.get(timeout=240)
+    got_mode, res, data_rank, last_rank, terms = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got_mode == mode
+    if factored and mode == "gather" and case != "three":
+        # two fragments: each rank compresses its own row block to its data rank (no collective)
+        assert data_rank and last_rank is not None and last_rank < terms
     _, cut = _case(case)
     ref = dense.run_dense(cut)
     np.testing.assert_allclose(res, ref, atol=1e-12, rtol=0)
