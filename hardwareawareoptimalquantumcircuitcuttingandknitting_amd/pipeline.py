@@ -215,7 +215,9 @@ class KnitPipeline:
         # (falls back to the exact contraction if a probe exceeds rank_tol)
         two = len(self.frags) == 2 and not any(fs.dropped for fs in self.frags)
         ok = mode in ("single", "gather") and factored and two
-        self.data_rank = ok if data_rank is None else (data_rank and ok)
+        # default: only where the write dominates (>= 2^24 outputs); below that the mid-step readback
+        # and host factorisation (~0.2 ms) cost more than the whole knit (bv 5 / hwe 16: < 0.02 ms)
+        self.data_rank = (ok and virt.circuit.num_clbits >= 24) if data_rank is None else (data_rank and ok)
         self.rank_tol = 1e-14  # Frobenius-norm estimate of R - A''^T B'' (probabilities: |R| <= 1)
         self.rank_fallbacks = 0
         self.last_rank = None
@@ -487,7 +489,12 @@ class KnitPipeline:
         if self.record_events:
             start, end = self.be.event(), self.be.event()
             start.record()
-        res = self._contract_lowrank(low[0]) if low is not None else self._contract(mats)
+        if low is not None:
+            res = self._contract_lowrank(low[0])
+        elif self.data_rank and self.mode == "single" and mats[self.order[0]].shape[0] <= 8:
+            res = self._contract_lowrank(mats)  # already small-K (e.g. the light-cone core): write-bound kernels
+        else:
+            res = self._contract(mats)
         if self.record_events:
             end.record()
             self.events.append((start, end))

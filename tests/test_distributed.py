@@ -53,7 +53,7 @@ def _worker(rank, world, port, case, mode, factored, q):
 
         _, cut = _case(case)
         pipe = KnitPipeline(VirtualCircuit(cut), rank=rank, world=world, mode=mode, factored=factored,
-                            backend=CpuBackend())
+                            backend=CpuBackend(), data_rank=True)
         res = pipe.step().numpy().copy()
         if mode == "gather":
             # place this rank's (x_A block, x_B) rows at their global keys, then sum over ranks

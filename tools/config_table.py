@@ -7,7 +7,7 @@ Per config: a KnitPipeline (factored knit where there are cuts, direct otherwise
 warmed up and stepped; HIP events on the launch stream time the sweep and the contraction, wall
 time the whole step. Reported: reference instances/s, sweep / knit / full-knit ms, the sweep's
 modelled HBM fraction, the contraction's MFMA fraction (2 M N K / time / 78.6
-TF/s) or, for K = 1 outer products, its HBM-write fraction, and parity: small configs against
+TF/s) or, for K <= 8 (write-bound small-K kernels), its HBM-write fraction, and parity: small configs against
 the CPU oracle (max |delta|, with the oracle's own time), 32-qubit ones by size-independent
 properties (sum to 1, no entry below -1e-13).
 """
@@ -63,7 +63,9 @@ def run(key, steps):
         "sweep_ms": sweep_ms, "knit_ms": knit_ms,
         "sweep_hbm_frac": tr["hbm"] / (sweep_ms * 1e-3) / 1e9 / HBM if sweep_ms > 0 else None,
     }
-    if K > 1:
+    row["data_rank"] = pipe.data_rank
+    row["knit_kernel"] = pipe.last_kernel or "qk_gemm_keyed (smallk / glds / keyed by shape)"
+    if K > 8:
         row["knit_mfma_frac"] = 2.0 * M * N * K / (knit_ms * 1e-3) / 1e12 / MFMA
     else:
         row["knit_hbm_write_frac"] = 8.0 * M * N / (knit_ms * 1e-3) / 1e9 / HBM
