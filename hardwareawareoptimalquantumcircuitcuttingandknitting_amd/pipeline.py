@@ -223,6 +223,7 @@ class KnitPipeline:
         self.last_rank = None
         self.last_kernel = None  # kernel of the last compressed contraction (None: qk_gemm_keyed)
         self._probe = None
+        self._pinned = None  # host staging of the two Gram matrices (pinned on a GPU)
         self.events = []  # (start, end) events around the main contraction GEMM
         self.sweep_events = []  # (start, end) events around each step's sweep (all fragments)
         self.record_events = False
@@ -527,13 +528,30 @@ class KnitPipeline:
         if self._probe is None or self._probe.shape[0] != B.shape[1]:
             g = T.Generator().manual_seed(1234)
             self._probe = T.randn((B.shape[1], 8), generator=g, dtype=T.float64).to(B.device)
+        # Grams first, their readback started at once; the probe reference runs on the GPU while
+        # the host factorises (no pageable copies: they would wait for the whole queue)
+        G = T.stack([_mm_nt(A, A), _mm_nt(B, B)])
+        on_gpu = G.device.type == "cuda"
+        if self._pinned is None or self._pinned.shape != G.shape:
+            self._pinned = T.empty(G.shape, dtype=G.dtype, pin_memory=on_gpu)
+        self._pinned.copy_(G, non_blocking=on_gpu)
+        ready = T.cuda.Event() if on_gpu else None
+        if on_gpu:
+            ready.record()
         ref = A.T @ _mm_nt(B, self._probe.T)
-        G = T.stack([_mm_nt(A, A), _mm_nt(B, B)]).cpu().numpy()
-        f = engine.data_rank_factors(G[0], G[1])
+        if on_gpu:
+            ready.synchronize()
+        Gh = self._pinned.numpy()
+        f = engine.data_rank_factors(Gh[0], Gh[1])
         if f is None or f[0].shape[0] >= K:
             self.last_rank = K
             return None
-        TA, TB = (T.from_numpy(t).to(A.device) for t in f)
+        r = f[0].shape[0]
+        tt = T.from_numpy(np.concatenate([f[0], f[1]]))
+        if on_gpu:
+            tt = tt.pin_memory()
+        tt = tt.to(A.device, non_blocking=on_gpu)
+        TA, TB = tt[:r], tt[r:]
         A2, B2 = (TA @ A).contiguous(), (TB @ B).contiguous()
         err = (A2.T @ _mm_nt(B2, self._probe.T) - ref).norm(dim=0).max()
         self.last_rank = A2.shape[0]
