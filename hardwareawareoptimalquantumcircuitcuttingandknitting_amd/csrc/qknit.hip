@@ -1008,8 +1008,13 @@ __global__ __launch_bounds__(256) void qk_gemm_smallk_kernel(GemmArgs g) {
 #ifndef QK_OS_WG_PER_CU
 #define QK_OS_WG_PER_CU 8
 #endif
+#ifndef QK_OS_P
+#define QK_OS_P 1  // adjacent output pairs per lane (16 * P contiguous bytes per lane); P = 2 / 4: 17 /
+                   // 46 ms on syc 32 5 (a wave store no longer covers whole lines), P = 1: 6.3 ms
+#endif
 constexpr int OS_U = QK_OS_U;
-constexpr int64_t OS_CHUNK = 2 * 256 * OS_U;  // outputs per workgroup iteration
+constexpr int OS_P = QK_OS_P;
+constexpr int64_t OS_CHUNK = 2 * OS_P * 256 * OS_U;  // outputs per workgroup iteration
 
 struct OuterStreamArgs {
     int nbits, K;
@@ -1039,10 +1044,11 @@ __global__ __launch_bounds__(256) void qk_knit_outer_stream_kernel(OuterStreamAr
     const int K = a.K;
     const int64_t total = int64_t(1) << a.nbits;
     for (int64_t c0 = (int64_t)blockIdx.x * OS_CHUNK; c0 < total; c0 += (int64_t)gridDim.x * OS_CHUNK) {
-        d2_t v[OS_U];
+        d2_t v[OS_U * OS_P];
 #pragma unroll
-        for (int u = 0; u < OS_U; ++u) {
-            const int64_t o = c0 + 512 * u + 2 * threadIdx.x;
+        for (int up = 0; up < OS_U * OS_P; ++up) {
+            const int u = up / OS_P, pp = up % OS_P;
+            const int64_t o = c0 + 512 * OS_P * u + 2 * (OS_P * threadIdx.x + pp);
             const uint32_t x = (uint32_t)o;
             uint32_t row = 0, col = 0;
 #pragma unroll
@@ -1063,16 +1069,17 @@ __global__ __launch_bounds__(256) void qk_knit_outer_stream_kernel(OuterStreamAr
                     }
                 }
             }
-            v[u] = acc;
+            v[up] = acc;
         }
 #pragma unroll
-        for (int u = 0; u < OS_U; ++u) {
-            const int64_t o = c0 + 512 * u + 2 * threadIdx.x;
+        for (int up = 0; up < OS_U * OS_P; ++up) {
+            const int u = up / OS_P, pp = up % OS_P;
+            const int64_t o = c0 + 512 * OS_P * u + 2 * (OS_P * threadIdx.x + pp);
             if (o < total) {
 #if QK_OS_NT
-                __builtin_nontemporal_store(v[u], reinterpret_cast<d2_t*>(a.out + o));
+                __builtin_nontemporal_store(v[up], reinterpret_cast<d2_t*>(a.out + o));
 #else
-                *reinterpret_cast<d2_t*>(a.out + o) = v[u];
+                *reinterpret_cast<d2_t*>(a.out + o) = v[up];
 #endif
             }
         }
