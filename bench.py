@@ -102,6 +102,55 @@ def cpu_baseline(cut, n_labels_sample: int):
     }
 
 
+QVM_MAX_CLBITS = 20  # literal dict knit cap: 2^N dict entries per merged label (syc 32: DNF)
+
+
+def host_info() -> dict:
+    """Cores this process may run on (``sched_getaffinity``) and the host CPU model."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"affinity_cores": len(os.sched_getaffinity(0)), "cpu_model": model}
+
+
+def cpu_baseline_qvm(cut, processes: int = 8, accuracy: float = 1e-5, return_result: bool = False) -> dict:
+    """The reference's own CPU algorithm, restated (``oracle/qvm.py``): exact instance
+    distributions (numpy statevector in place of Aer's sampling, ``run.py:36-58``), then the
+    literal dict merge + per-gate knit through ``Pool(processes)`` (``run.py:64-67``,
+    ``virtual_circuit.py:50-68,216-228``) with ``QuasiDistr``'s shipped ``ACCURACY`` truncation,
+    then ``nearest_probability_distribution`` (``run.py:71``). Timed as ``RunTimeInfo``. Outputs of
+    more than ``QVM_MAX_CLBITS`` clbits (syc 32: 2^32 dict entries) are reported DNF."""
+    from multiprocessing import Pool
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import qvm
+
+    n = sum(len(c) for c in cut.cregs)
+    info = {"kind": "port", "algorithm": "qvm literal: exact instances + dict merge/knit in Pool(%d)" % processes,
+            "processes": processes, **host_info()}
+    if n > QVM_MAX_CLBITS:
+        return {**info, "status": "DNF", "reason": f"{n} clbits: the dict knit holds up to 2^{n} entries per "
+                                                   f"label (cap {QVM_MAX_CLBITS} clbits)"}
+    times = {}
+    t0 = time.perf_counter()
+    with Pool(processes=processes) as pool:
+        _, npd = qvm.run(cut, accuracy, pool=pool, times=times)
+    wall = time.perf_counter() - t0
+    view = qvm.CutView(cut)
+    inst = sum(len(view.labels(list(r))) for r in view.qregs if len(r))
+    out = {**info, "status": "ok", "run_time_s": times["run_time"], "knit_time_s": times["knit_time"],
+           "wall_s": wall, "instances_ref": inst, "value": inst / (times["run_time"] + times["knit_time"]),
+           "unit": "instances/s", "result_entries": len(npd)}
+    if return_result:
+        out["result"] = dict(npd)
+    return out
+
+
 def north_star_sweep(steps: int) -> dict:
     """BASELINE.json north-star target: the batched statevector sweep for syc 32 1 at p=2 on one
     MI355X against the HBM roofline. Per variant (the reference cut: 0 cuts, 2 instances; the

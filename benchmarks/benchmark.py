@@ -1,0 +1,279 @@
+#!/usr/bin/env python3
+"""Counterpart of the reference's benchmark entry point (``benchmarks/benchmark.py``).
+
+  python benchmarks/benchmark.py -p P -q Q <syc|hwe|bv|qft> <nQubits> <depth> [options]
+
+Same positional argv as ``benchmarks/benchmark.py:22-29`` (``-p`` max partitions, ``-q`` max
+qubits per partition, circuit name, qubits, depth), the same steps and the same log lines:
+
+1. ``genCirc(name, n, d)`` (``:39``; ``generators.gen_circ``, pinned seed) and the cutter's
+   ``decompose()`` (``Cutter.py:84``; ``cutting.decompose``);
+2. the cut: the reference runs its z3 ``Cutter`` (``:41-56``, CPU, out of scope); here the cut
+   of SURVEY.md App. C for the config (``cutting.config_cut_circuit``) or ``--cutspec FILE``
+   (JSON ``{"partitions": [[q, ...], ...], "gate_cuts": [i, ...], "wire_cuts": [[i, q, dest], ...]}``,
+   instruction indices into the decomposed circuit). The model key results ``S A L Q C nWireCuts
+   nGateCuts Q_p C_p`` are logged as ``:57-71`` does (``Cutter.py:164-179`` semantics: QPD costs
+   6 per gate cut and 8 per wire cut, ancilla 1 per wire cut, no teleports); a cut that breaks
+   ``-p`` / ``-q`` / the 5-cut caps of ``:41`` logs ``success => False`` and exits 0 (``:53-54``);
+3. ``compareOriginalCircWithCutCirc`` (``:99``, ``Utilities.py:154-226``), ideal half: the cut
+   circuit through ``run_virtual_circuit`` (``run.py:23-71``: the HIP sweep + knit, logging
+   ``Running ...`` / ``Knitted in ...``), the uncut circuit as one 0-cut fragment through the
+   same sweep, and ``cutVsUncutFidelity`` = Hellinger fidelity on the GPU (``:224``). The noisy
+   ``FakeKolkataV2`` fidelities (``:222-223``) are out of scope and logged as such.
+
+Options: ``--cut-only`` (the reference's ``CUT_ONLY = True``, ``:20,90-92``); ``--sample --shots
+N`` (shot-sampled instances as Aer does, ``nShots = 1000`` at ``:94``; default: exact);
+``--cpu-baseline`` (the reference's CPU algorithm restated: exact instances + literal dict knit in
+``Pool(8)``, ``run.py:64-67``, via ``bench.cpu_baseline_qvm``; DNF beyond 20 clbits); ``--no-gpu``
+(stop before the GPU leg, e.g. with ``--cpu-baseline`` on a host without a GPU); ``--gpus N``
+under ``torch.distributed.run`` (one process per GPU; the knit runs sharded through
+``run_virtual_circuit(..., group=...)``). A JSON summary is printed last.
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import json
+import logging
+import logging.handlers
+import os
+import pathlib
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import cutting  # noqa: E402
+from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.generators import gen_circ  # noqa: E402
+from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.virtual_gates import (  # noqa: E402
+    VirtualBinaryGate, VirtualMove)
+
+MAX_CUTS = 5  # maxNQpdCuts = maxNCuts = maxCutsPerPartitions = 5 (benchmark.py:41)
+GATE_CUT_S, WIRE_CUT_S = 6, 8  # QPD overheadSampling (Cutter.py:452-461)
+LOG_FORMAT = "%(asctime)s | %(name)s [%(threadName)s] |  %(levelname)s: %(message)s"  # Logger.py:31-32
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("-p", type=int, required=True, help="max partitions (BENCHMARK_MAX_PARTITIONS)")
+    ap.add_argument("-q", type=int, required=True, help="max qubits per partition (BENCHMARK_MAX_N_QUBITS)")
+    ap.add_argument("name", help="circuit: syc | hwe | bv | qft")
+    ap.add_argument("n", type=int, help="qubits")
+    ap.add_argument("d", type=int, help="depth")
+    ap.add_argument("--cutspec", help="JSON cut-spec file (default: the config's cut, SURVEY.md App. C)")
+    ap.add_argument("--variant", default="ref", help="config cut variant: ref | forced")
+    ap.add_argument("--seed", type=int, default=None, help="generator seed (default: pinned 1234)")
+    ap.add_argument("--cut-only", action="store_true", help="stop after the cut (CUT_ONLY)")
+    ap.add_argument("--sample", action="store_true", help="shot-sample the instances (Aer-like)")
+    ap.add_argument("--shots", type=int, default=1000, help="shots per instance with --sample (nShots)")
+    ap.add_argument("--cpu-baseline", action="store_true", help="time the reference's CPU algorithm too")
+    ap.add_argument("--no-gpu", action="store_true", help="skip the GPU leg")
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs (launch with torch.distributed.run for > 1)")
+    ap.add_argument("--device", type=int, default=None)
+    ap.add_argument("--results-dir", default="./benchmark_results", help="parent of the per-run directory")
+    ap.add_argument("--no-save", action="store_true", help="no results directory / run.log")
+    return ap.parse_args(argv)
+
+
+def get_logger(log_file: pathlib.Path | None) -> logging.Logger:
+    """Reference ``Logger`` behaviour (``Logger.py:20-60``): INFO to the console, DEBUG to a
+    rotating ``run.log``; the package's own ``run_virtual_circuit`` logs through the same handlers."""
+    fmt = logging.Formatter(LOG_FORMAT)
+    handlers = []
+    sh = logging.StreamHandler()
+    sh.setLevel(logging.INFO)
+    sh.setFormatter(fmt)
+    handlers.append(sh)
+    if log_file is not None:
+        fh = logging.handlers.TimedRotatingFileHandler(filename=str(log_file.absolute()), when="midnight",
+                                                       backupCount=30)
+        fh.setLevel(logging.DEBUG)
+        fh.setFormatter(fmt)
+        handlers.append(fh)
+    for name in ("main", "hardwareawareoptimalquantumcircuitcuttingandknitting_amd"):
+        lg = logging.getLogger(name)
+        lg.setLevel(logging.DEBUG)
+        lg.propagate = False
+        for h in list(lg.handlers):
+            lg.removeHandler(h)
+        for h in handlers:
+            lg.addHandler(h)
+    return logging.getLogger("main")
+
+
+def load_cutspec(path: str) -> cutting.CutSpec:
+    spec = json.load(open(path))
+    return cutting.CutSpec([list(p) for p in spec["partitions"]], list(spec.get("gate_cuts", [])),
+                           [tuple(w) for w in spec.get("wire_cuts", [])])
+
+
+def model_key_results(cut_circ, max_partitions: int) -> dict:
+    """``Cutter.getModelKeyResults`` (``Cutter.py:164-179``) of an explicit cut: S = product of the
+    QPD overheads (6 per gate cut, 8 per wire cut), A = ancillas x S (1 per wire cut, ``:508``),
+    L = teleport latency (0: no teleports), Q_p = qubits of fragment p (move qubits included),
+    C_p = cuts with an endpoint in fragment p (``:476-516``), Q / C their maxima."""
+    frags = list(cut_circ.qregs)
+    frag_of = {q: i for i, r in enumerate(frags) for q in r}
+    n_gate = n_wire = 0
+    c_p = [0] * max(max_partitions, len(frags))
+    for instr in cut_circ:
+        op = instr.operation
+        if isinstance(op, VirtualMove):
+            n_wire += 1
+        elif isinstance(op, VirtualBinaryGate):
+            n_gate += 1
+        else:
+            continue
+        for p in {frag_of[q] for q in instr.qubits}:
+            c_p[p] += 1
+    S = GATE_CUT_S ** n_gate * WIRE_CUT_S ** n_wire
+    q_p = [len(r) for r in frags] + [0] * (len(c_p) - len(frags))
+    return {"S": S, "A": n_wire * S, "L": 0, "Q": max(q_p), "C": max(c_p), "nWireCuts": n_wire,
+            "nGateCuts": n_gate, "Q_p": q_p, "C_p": c_p}
+
+
+def _dist():
+    import torch.distributed as dist
+
+    return dist if dist.is_available() and dist.is_initialized() else None
+
+
+def run(args, logger=None) -> dict:
+    """One benchmark run; returns the summary (also printed as JSON by :func:`main`)."""
+    run_dir = None
+    if not args.no_save:
+        stamp = datetime.datetime.now()
+        run_dir = pathlib.Path(args.results_dir) / f"{args.name}_{args.n}_{args.d}_{args.p}_{args.q}_{stamp}"
+        (run_dir / "instantiations").mkdir(parents=True, exist_ok=True)
+    logger = logger or get_logger(run_dir / "run.log" if run_dir else None)
+    summary = {"circuit": f"{args.name} {args.n} {args.d}", "p": args.p, "q": args.q}
+
+    circ = cutting.decompose(gen_circ(args.name, args.n, args.d, args.seed if args.seed is not None
+                                      else cutting_default_seed()))
+    t0 = datetime.datetime.now()
+    logger.info("solving STARTED")
+    try:
+        if args.cutspec:
+            cut = cutting.cut_circuit(circ, load_cutspec(args.cutspec))
+            desc = f"cut-spec {args.cutspec}"
+        else:
+            _, cut, desc = cutting.config_cut_circuit(args.name, args.n, args.d, args.p, args.variant, args.seed)
+    except ValueError as e:
+        logger.info("solving DONE")
+        logger.info(f"success => False ({e})")
+        return {**summary, "success": False, "reason": str(e)}
+    frags = [r for r in cut.qregs]
+    keys = model_key_results(cut, args.p)
+    problems = []
+    if len([r for r in frags if len(r)]) > args.p:
+        problems.append(f"{len(frags)} fragments > -p {args.p}")
+    if keys["Q"] > args.q:
+        problems.append(f"a fragment has {keys['Q']} qubits > -q {args.q}")
+    if keys["nWireCuts"] + keys["nGateCuts"] > MAX_CUTS or keys["C"] > MAX_CUTS:
+        problems.append(f"more than {MAX_CUTS} cuts")
+    logger.info("solving DONE")
+    logger.info(f"solving time elapsed: {datetime.datetime.now() - t0}")
+    logger.info(f"success => {not problems}")
+    summary.update(cut=desc, model=keys)
+    if problems:  # the z3 model would be unsat under these caps (benchmark.py:53-54)
+        logger.info("; ".join(problems))
+        return {**summary, "success": False, "reason": "; ".join(problems)}
+    for k in ("S", "A", "L", "Q", "C", "nWireCuts", "nGateCuts"):
+        logger.info(f"{k}: {keys[k]}")
+    for idx in range(args.p):
+        logger.info(f"  Q_p{idx}: {keys['Q_p'][idx]}")
+    logger.info("")
+    for idx in range(args.p):
+        logger.info(f"  C_p{idx}: {keys['C_p'][idx]}")
+    summary["success"] = True
+    if args.cut_only:
+        logger.info("CUT_ONLY == True => Simulation will not run.")
+        return summary
+
+    if args.cpu_baseline:
+        import bench
+
+        logger.info("CPU baseline: the reference's algorithm (exact instances + dict knit in Pool(8))...")
+        cpu = bench.cpu_baseline_qvm(cut)
+        if cpu["status"] == "ok":
+            logger.info(f"CPU baseline: run {cpu['run_time_s']:.3f}s, knit {cpu['knit_time_s']:.3f}s "
+                        f"({cpu['instances_ref']} instances, {cpu['affinity_cores']} cores, {cpu['cpu_model']})")
+        else:
+            logger.info(f"CPU baseline: DNF ({cpu['reason']})")
+        summary["cpu_baseline"] = cpu
+    if args.no_gpu:
+        return summary
+    summary.update(_gpu_leg(args, circ, cut, logger))
+    return summary
+
+
+def cutting_default_seed() -> int:
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.generators import DEFAULT_SEED
+
+    return DEFAULT_SEED
+
+
+def _gpu_leg(args, circ, cut, logger) -> dict:
+    import torch
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, engine, fidelity, quasi_distr
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.run import run_virtual_circuit_dense
+
+    if not torch.cuda.is_available():
+        raise RuntimeError("the GPU leg needs a HIP device (use --no-gpu to stop before it)")
+    dist = _dist()
+    group = dist.group.WORLD if dist is not None and dist.get_world_size() > 1 else None
+    device = args.device if args.device is not None else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(device)
+    N = circ.num_clbits
+    logger.info(f"Circuits will be run {'with %d shots' % args.shots if args.sample else 'exactly (fp64)'} "
+                f"to calculate fidelity...")
+    virt = VirtualCircuit(cut)
+    kw = {"group": group} if group is not None else {}
+    cut_dense, info = run_virtual_circuit_dense(virt, shots=args.shots, device=device, sample=args.sample,
+                                                factored=not args.sample, **kw)
+    out = {"run_time_s": info.run_time, "knit_time_s": info.knit_time, "n_gpus": 1 if group is None
+           else dist.get_world_size()}
+    if group is not None and dist.get_rank() != 0:
+        return out
+    t0 = time.perf_counter()
+    uncut = fidelity.uncut_distribution(circ, device)
+    torch.cuda.synchronize(device)
+    out["uncut_time_s"] = time.perf_counter() - t0
+    f = fidelity.hellinger_fidelity_dense(uncut, cut_dense, device)
+    logger.info("inputCircFidelity: n/a (noisy FakeKolkataV2 runs are out of scope)")
+    logger.info("cutCircFidelity: n/a (noisy FakeKolkataV2 runs are out of scope)")
+    logger.info(f"cutVsUncutFidelity: {f}")
+    out["cutVsUncutFidelity"] = f
+    if N <= 24:  # reference-shaped result (run.py:71): QuasiDistr truncation + NPD on the GPU
+        keys, vals = engine.nearest_probability_distribution(engine.get_context(device), cut_dense,
+                                                             quasi_distr.ACCURACY)
+        out["result"] = {int(k): float(v) for k, v in zip(keys.tolist(), vals.tolist())}
+    return out
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch
+        import torch.distributed as dist
+
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    summary = run(args)
+    if summary.get("result") is not None:
+        summary["result_entries"] = len(summary["result"])
+        del summary["result"]
+    dist = _dist()
+    if dist is None or dist.get_rank() == 0:
+        print(json.dumps(summary, default=str), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -114,33 +114,49 @@ def instance_distributions(view: CutView, frag, accuracy=0.0):
     return res
 
 
-def knit(view: CutView, results: dict, accuracy=0.0):
-    """``VirtualCircuit.knit`` (``virtual_circuit.py:50-68``) on ``{frag: [QD]}``."""
+def _merge_row(row):
+    """``_merge_distrs`` (``virtual_circuit.py:216-221``): fold ``QuasiDistr.merge`` over a row."""
+    acc = row[0]
+    for d in row[1:]:
+        acc = acc.merge(d)
+    return acc
+
+
+def knit(view: CutView, results: dict, accuracy=0.0, pool=None):
+    """``VirtualCircuit.knit`` (``virtual_circuit.py:50-68``) on ``{frag: [QD]}``.
+
+    ``pool`` (a ``multiprocessing.Pool``) runs the merge and every per-gate knit through
+    ``pool.map`` / ``pool.starmap`` exactly as the reference does with its ``Pool(8)``
+    (``run.py:64-67``, ``virtual_circuit.py:63-66,224-228``); None runs them in-process."""
     glabels = view.global_labels()
     lists = []
     for frag, distrs in results.items():
         by_label = dict(zip(view.labels(frag), distrs))
         lists.append([by_label[tuple(g[j] if view.touches(j, frag) else -1 for j in range(len(g)))]
                       for g in glabels])
-    merged = []
-    for row in zip(*lists):
-        acc = row[0]
-        for d in row[1:]:
-            acc = acc.merge(d)
-        merged.append(acc)
+    merged = pool.map(_merge_row, list(zip(*lists))) if pool is not None else [_merge_row(r) for r in zip(*lists)]
     if not view.vgates:
         return merged[0]
     clbit = view.num_clbits + len(view.vgates) - 1
     for j in reversed(range(len(view.vgates))):
         kind, params, _, _ = view.vgates[j]
         n = view.n_inst(j)
-        merged = [tables.knit(kind, params, merged[i:i + n], clbit) for i in range(0, len(merged), n)]
+        chunks = [merged[i:i + n] for i in range(0, len(merged), n)]
+        if pool is not None:
+            merged = pool.starmap(tables.knit, [(kind, params, c, clbit) for c in chunks])
+        else:
+            merged = [tables.knit(kind, params, c, clbit) for c in chunks]
         clbit -= 1
     return merged[0]
 
 
-def run(circ, accuracy=0.0):
-    """Exact-instance ``run_virtual_circuit``: returns (knit QD before projection, NPD dict)."""
+def run(circ, accuracy=0.0, pool=None, times=None):
+    """Exact-instance ``run_virtual_circuit``: returns (knit QD before projection, NPD dict).
+
+    ``times`` (a dict) receives ``run_time`` / ``knit_time`` split as ``run.py:35,60,65-67``."""
+    import time
+
+    t0 = time.perf_counter()
     view = CutView(circ)
     results = {}
     for qreg in view.qregs:
@@ -150,7 +166,10 @@ def run(circ, accuracy=0.0):
         d = instance_distributions(view, frag, accuracy)
         if d is not None:
             results[tuple(frag)] = d
-    out = knit(view, results, accuracy)
+    t1 = time.perf_counter()
+    out = knit(view, results, accuracy, pool)
+    if times is not None:
+        times["run_time"], times["knit_time"] = t1 - t0, time.perf_counter() - t1
     return out, out.npd()
 
 

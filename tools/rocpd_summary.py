@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Per-kernel summaries from rocprofv3's default rocpd (SQLite) output.
+
+  python tools/rocpd_summary.py trace DB [--top 30]              kernel-trace stats (calls, avg/min/max us)
+  python tools/rocpd_summary.py pmc KERNEL_SUBSTR DB [DB ...]    counter means over the kernel's dispatches
+
+rocprofv3 on ROCm 7.2 writes ``<dir>/<host>/<pid>_results.db`` (or ``-o NAME``: ``NAME_results.db``)
+unless ``--output-format csv`` is given; this reads the ``kernels`` and ``counters_collection``
+views of that database. PMC: values are summed over the counter's per-SE/per-instance rows of
+one dispatch, then averaged over dispatches; with ``--long`` only dispatches at least half as long
+as the kernel's longest are kept (drops the short warm-up/operand launches of a shared kernel).
+Durations are in ns in the database.
+"""
+import argparse
+import collections
+import sqlite3
+
+
+def trace(db: str, top: int):
+    con = sqlite3.connect(db)
+    rows = con.execute("select name, duration from kernels").fetchall()
+    agg = collections.defaultdict(list)
+    for name, dur in rows:
+        agg[name].append(dur / 1e3)
+    total = sum(sum(v) for v in agg.values())
+    print(f"{'kernel':72s} {'calls':>6s} {'total_us':>11s} {'avg_us':>10s} {'min_us':>9s} {'max_us':>9s} {'%':>6s}")
+    for name, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:top]:
+        print(f"{name[:72]:72s} {len(v):6d} {sum(v):11.1f} {sum(v) / len(v):10.1f} {min(v):9.1f} {max(v):9.1f} "
+              f"{100 * sum(v) / total:6.2f}")
+
+
+def pmc(kern: str, dbs: list, long_only: bool):
+    vals = collections.defaultdict(list)
+    durs = {}
+    for db in dbs:
+        con = sqlite3.connect(db)
+        rows = con.execute("select dispatch_id, kernel_name, counter_name, value, duration from counters_collection "
+                           "where kernel_name like ?", (f"%{kern}%",)).fetchall()
+        per = collections.defaultdict(float)
+        dd = {}
+        for did, _, cname, v, dur in rows:
+            per[(did, cname)] += v
+            dd[did] = dur
+        if long_only and dd:
+            tmax = max(dd.values())
+            dd = {k: v for k, v in dd.items() if v >= 0.5 * tmax}
+        for (did, cname), v in per.items():
+            if did in dd:
+                vals[cname].append(v)
+        durs.update({(db, k): v for k, v in dd.items()})
+    if not durs:
+        print(f"no dispatches of *{kern}*")
+        return {}
+    ms = sum(durs.values()) / len(durs) / 1e6
+    print(f"kernel~{kern}: {len(durs)} dispatches, mean {ms:.4f} ms")
+    out = {"dispatches": len(durs), "mean_ms": ms}
+    for name in sorted(vals):
+        v = sum(vals[name]) / len(vals[name])
+        out[name] = v
+        print(f"  {name:36s} {v:18.6g}")
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    t = sub.add_parser("trace")
+    t.add_argument("db")
+    t.add_argument("--top", type=int, default=30)
+    p = sub.add_parser("pmc")
+    p.add_argument("kernel")
+    p.add_argument("dbs", nargs="+")
+    p.add_argument("--long", action="store_true")
+    a = ap.parse_args()
+    if a.cmd == "trace":
+        trace(a.db, a.top)
+    else:
+        pmc(a.kernel, a.dbs, a.long)
+
+
+if __name__ == "__main__":
+    main()
