@@ -143,6 +143,19 @@ __device__ __forceinline__ void ap_d1r(double2 (&v)[PER], const double* d) {
     }
 }
 
+// Sign flip by XOR of the high dwords (mask 0x80000000 or 0): the +-1 diagonals and scalars the
+// per-program kernels select from state bits cost two 32-bit ops instead of two f64 multiplies.
+__device__ __forceinline__ double2 flip_sign(double2 z, unsigned m) {
+    return make_double2(__hiloint2double(__double2hiint(z.x) ^ (int)m, __double2loint(z.x)),
+                        __hiloint2double(__double2hiint(z.y) ^ (int)m, __double2loint(z.y)));
+}
+
+template <int A>
+__device__ __forceinline__ void ap_d1s(double2 (&v)[PER], unsigned m0, unsigned m1) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) v[r] = flip_sign(v[r], (r & (1 << A)) ? m1 : m0);
+}
+
 template <int A, int B>
 __device__ __forceinline__ void ap_d2r(double2 (&v)[PER], const double* d) {
 #pragma unroll

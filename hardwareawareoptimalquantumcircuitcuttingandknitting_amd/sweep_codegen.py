@@ -64,22 +64,84 @@ class _Emitter:
         self.lines.append("    " * ind + s)
 
 
-def _variant(vals: list, ebits: list) -> list:
+def _variant(vals: list, ebits: list, lit=None) -> list:
     """select_variant4 semantics: vals holds up to 4 variants of length N; ebits = [b1 expr or
-    None, b2 expr or None]. Returns per-element C expressions."""
+    None, b2 expr or None]. Returns per-element C expressions (``lit`` formats a value)."""
+    lit = lit or _lit
     b1, b2 = ebits
-    nvar = 1 + (b1 is not None) + 2 * (b2 is not None)
-    del nvar
     N = len(vals[0])
 
     def pick(lo_v, hi_v, cond):
-        return [f"({cond} ? {_lit(h)} : {_lit(l)})" if h != l else _lit(l) for l, h in zip(lo_v, hi_v)]
+        return [f"({cond} ? {lit(h)} : {lit(l)})" if h != l else lit(l) for l, h in zip(lo_v, hi_v)]
 
-    low = pick(vals[0], vals[1], b1) if b1 is not None else [_lit(x) for x in vals[0]]
+    low = pick(vals[0], vals[1], b1) if b1 is not None else [lit(x) for x in vals[0]]
     if b2 is None:
         return low
-    high = pick(vals[2], vals[3], b1) if b1 is not None else [_lit(x) for x in vals[2]]
+    high = pick(vals[2], vals[3], b1) if b1 is not None else [lit(x) for x in vals[2]]
     return [f"({b2} ? {h} : {l})" if h != l else l for l, h in zip(low, high)][:N]
+
+
+def _sign_lit(x: float) -> str:
+    """+-1 as the XOR mask of the high dword of a double (sign flip: no multiply)."""
+    return "0x80000000u" if x < 0 else "0u"
+
+
+def _all_unit(vals: list) -> bool:
+    return all(x in (1.0, -1.0) for v in vals for x in v)
+
+
+# doubles of compile-time matrix data per op kind (variants included: see _emit_op)
+def _op_values(op, mats) -> list:
+    """Every compile-time matrix value an op reads (all variants), as floats; [] for ops without
+    a compile-time matrix (slot matrices come per job at run time; CX / SWAP are permutations)."""
+    kind, e1, e2, mat = int(op["kind"]), int(op["e1"]), int(op["e2"]), int(op["mat"])
+    nvar = 2 if e1 >= 0 else 1
+    size = {sp.K_U1: 8 * nvar, sp.K_D1: 4 * nvar, sp.K_U2: 32, sp.K_D2: 8, sp.K_U1R: 4, sp.K_U1X: 4,
+            sp.K_D1R: 2 * nvar, sp.K_D2R: 4}.get(kind)
+    if kind in (sp.K_SCALE, sp.K_SCALER):
+        size = (2 if kind == sp.K_SCALE else 1) * (4 if e2 >= 0 else 2)
+    if size is None:
+        return []
+    return [float(x) for x in mats[mat: mat + size]]
+
+
+def op_scale(op, mats) -> float:
+    """Positive scalar divided out of an op's compile-time matrix (all its variants alike, so the
+    op times the scalar is the original op for every amplitude). The largest |entry| (complex
+    modulus) becomes 1: the Sycamore / Hadamard-type gates (entries +-1/sqrt2, +-i/sqrt2) turn into
+    +-1 / +-i entries whose multiplies the compiler folds away (x*1 = x, fma(1, a, b) = a + b are
+    exact), and diagonal +-sqrt2 phases into sign flips. 1.0 for ops without a constant matrix."""
+    vals = _op_values(op, mats)
+    if not vals:
+        return 1.0
+    kind = int(op["kind"])
+    if kind in (sp.K_U1, sp.K_D1, sp.K_U2, sp.K_D2, sp.K_SCALE):  # interleaved complex
+        mags = [abs(complex(vals[i], vals[i + 1])) for i in range(0, len(vals), 2)]
+    else:  # real entries (U1X: [m00, Im m01, Im m10, m11], each one an entry's modulus)
+        mags = [abs(v) for v in vals]
+    c = max(mags)
+    return c if c > 0 else 1.0
+
+
+SNAP = 4e-16  # normalised entries this close to 0 / +-1 are those values (cos/sin(pi/4) differ by an ulp)
+
+
+def _snap(x: float) -> float:
+    """Normalised matrix entry, snapped to an exact 0 or +-1 within SNAP (a relative change of
+    < 4e-16 of the entry, below fp64 rounding of the op itself) so its multiply folds away."""
+    for t in (0.0, 1.0, -1.0):
+        if abs(x - t) <= SNAP:
+            return t
+    return x
+
+
+def program_scale(enc) -> float:
+    """Product of :func:`op_scale` over every op of every pass: the true amplitudes are this times
+    the ones the normalised kernels compute (probabilities: its square)."""
+    out = 1.0
+    for op in enc.ops:
+        out *= op_scale(op, enc.mats)
+    return out
 
 
 def _emit_op(e: _Emitter, op, mats, ext, n_slots: int) -> None:
@@ -87,9 +149,10 @@ def _emit_op(e: _Emitter, op, mats, ext, n_slots: int) -> None:
                                      int(op["e2"]), int(op["slot"]), int(op["mat"]))
     b1 = ext(e1) if e1 >= 0 else None
     b2 = ext(e2) if e2 >= 0 else None
+    inv = 1.0 / op_scale(op, mats)
 
     def arr(n, off=0):
-        return [float(x) for x in mats[mat + off: mat + off + n]]
+        return [_snap(float(x) * inv) for x in mats[mat + off: mat + off + n]]
 
     def const_arr(name, exprs):
         e(f"const double {name}[{len(exprs)}] = {{{', '.join(exprs)}}};", 2)
@@ -128,6 +191,10 @@ def _emit_op(e: _Emitter, op, mats, ext, n_slots: int) -> None:
             e(f"const double sr = {s[0]}, si = {s[1]};", 2)
             e("#pragma unroll", 0)
             e(f"for (int r = 0; r < {PER}; ++r) v[r] = cmul(sr, si, v[r]);", 2)
+        elif _all_unit(vals):  # +-1 chosen by external bits: flip the sign bits
+            e(f"const unsigned sg = {_variant(vals, [b1, b2], _sign_lit)[0]};", 2)
+            e("#pragma unroll", 0)
+            e(f"for (int r = 0; r < {PER}; ++r) v[r] = flip_sign(v[r], sg);", 2)
         else:
             e(f"const double sr = {s[0]};", 2)
             e("#pragma unroll", 0)
@@ -140,8 +207,13 @@ def _emit_op(e: _Emitter, op, mats, ext, n_slots: int) -> None:
         e(f"ap_u1x<{a}>(v, m);", 2)
     elif kind == sp.K_D1R:
         vals = [arr(2), arr(2, 2)] if b1 is not None else [arr(2)]
-        const_arr("d", _variant(vals, [b1, None]))
-        e(f"ap_d1r<{a}>(v, d);", 2)
+        if _all_unit(vals):  # diag(+-1, +-1): sign flips, selected by the external bit
+            sg = _variant(vals, [b1, None], _sign_lit)
+            e(f"const unsigned sg0 = {sg[0]}, sg1 = {sg[1]};", 2)
+            e(f"ap_d1s<{a}>(v, sg0, sg1);", 2)
+        else:
+            const_arr("d", _variant(vals, [b1, None]))
+            e(f"ap_d1r<{a}>(v, d);", 2)
     elif kind == sp.K_D2R:
         const_arr("d", [_lit(x) for x in arr(4)])
         e(f"ap_d2r<{a}, {b}>(v, d);", 2)
@@ -259,7 +331,8 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str, device_fn: bool = F
             sub = (sub - traced) & traced
             if sub == 0:
                 break
-        e(f"const double sgn = job_sign[job];")
+        # the ops ran with op_scale divided out: probabilities carry program_scale^2
+        e(f"const double sgn = job_sign[job] * {_lit(program_scale(enc) ** 2)};")
         cond = traced & (NT - 1)
         for i in keep:
             e(f"if (!(tid & {cond}u)) {{" if cond else "{")
