@@ -46,7 +46,7 @@ SIGNATURES = {
     "qk_sweep_compiled_labels": (c_i32, [c_vp, c_vp, ctypes.POINTER(QkProgram), c_i64, c_vp, c_vp, c_i64, c_vp,
                                          c_vp, c_i64, c_vp]),
     "qk_sweep_compiled_multi": (c_i32, [c_vp, c_vp, ctypes.c_int, ctypes.POINTER(QkProgram), c_lp, c_vp, c_vp, c_lp,
-                                        c_vp, c_vp, c_lp, c_vp]),
+                                        c_vp, c_vp, c_lp, c_vp, c_vp]),
     "qk_reduce_labels": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "qk_gemm_keyed": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                               c_vp, c_i64, c_vp, ctypes.c_int]),

@@ -152,12 +152,14 @@ struct qk_multi_args {
     int64_t n_jobs[QK_MULTI_MAX];
     int64_t begin[QK_MULTI_MAX];
     int64_t end[QK_MULTI_MAX];
+    const uint64_t* map;  // block -> (program << 56 | block within its range), or NULL: ranges in order
 };
 
 int qk_sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, const qk_program* progs,
                             const int64_t* n_jobs, const double* const* job_slots, const double* const* job_sign,
                             const int64_t* n_labels, const int64_t* const* label_offsets, void* const* workspaces,
-                            const int64_t* workspace_bytes, double* const* outs) {
+                            const int64_t* workspace_bytes, double* const* outs,
+                            const uint64_t* const* block_maps) {
     if (!ctx) return QK_EARG;
     if (!module || !progs || n_prog < 1 || n_prog > QK_MULTI_MAX || !n_jobs || !job_slots || !job_sign ||
         !n_labels || !label_offsets || !workspaces || !workspace_bytes || !outs)
@@ -205,6 +207,7 @@ int qk_sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, co
             a.n_jobs[f] = n_jobs[f];
         }
         if (total > 0x7fffffff) return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: too many tiles");
+        a.map = block_maps ? block_maps[r] : nullptr;
         size_t size = sizeof(a);
         void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
         const hipError_t e = hipModuleLaunchKernel(module->fns[r], (unsigned)total, 1, 1, 1u << (tb - 4), 1, 1, 0,

@@ -91,6 +91,41 @@ def _sweep_flops_per_job(enc) -> int:
     return total + 4 * n_amp
 
 
+def multi_block_maps(encs: list, sweeps: list) -> list:
+    """Per pass round of a multi-fragment sweep, the block order (``qk_sweep_compiled_multi``
+    block_maps; None = fragments' block ranges in order). A round in which some fragment runs its
+    fused FINAL pass (one workgroup per (label, tile) walking the label's branch jobs serially)
+    has units of unequal work: 1 to 16 jobs per label on syc 32 5. Their blocks go heaviest first
+    (longest-processing-time order, ties in range order), so the long labels start at once instead
+    of in the last dispatch wave; every other round keeps the plain ranges."""
+    rounds = max(len(e.passes) for e in encs)
+    out = []
+    for r in range(rounds):
+        items, mapped = [], False
+        for f, (enc, sw) in enumerate(zip(encs, sweeps)):
+            P = len(enc.passes)
+            if P <= r:
+                continue
+            sparse_init = r == 0 and P > 1
+            fin = r == P - 1
+            if sparse_init:
+                work, bpu = [1] * sw["n_jobs"], 1
+            elif fin and sw["fused"]:
+                offs = sw["label_offsets"]
+                work, bpu = list(np.diff(offs)), 1 << (enc.n - enc.tile_bits)
+                mapped = True
+            else:
+                work, bpu = [1] * sw["n_jobs"], 1 << (enc.n - enc.tile_bits)
+            items += [(-int(w), f, u, bpu) for u, w in enumerate(work)]
+        if not mapped:
+            out.append(None)
+            continue
+        items.sort(key=lambda t: (t[0], t[1], t[2]))
+        m = np.fromiter(((f << 56) | (u * bpu + t) for _, f, u, bpu in items for t in range(bpu)), dtype=np.uint64)
+        out.append(m)
+    return out
+
+
 class HipBackend:
     """Device work of the pipeline on one GPU through the C ABI."""
 
@@ -135,12 +170,16 @@ class HipBackend:
         i64 = lambda xs: (ctypes.c_int64 * n)(*xs)  # noqa: E731
         module = engine.compiled_multi_module(self.device, [fs.dprog.enc for fs in frags])
         outs = [(sw["q"] if sw["fused"] else sw["pjob"]) for sw in sweeps]
+        maps = multi_block_maps([fs.dprog.enc for fs in frags], sweeps)
+        self._maps = [None if m is None else self.to_device(m.view(np.int64)) for m in maps]  # kept alive
+        rounds = len(maps)
         return (module, (_lib.QkProgram * n)(*[fs.dprog.struct for fs in frags]), i64([sw["n_jobs"] for sw in sweeps]),
                 vp([sw["slot"].data_ptr() for sw in sweeps]), vp([sw["sign"].data_ptr() for sw in sweeps]),
                 i64([sw["n_local"] for sw in sweeps]),
                 vp([sw["off"].data_ptr() if sw["fused"] else None for sw in sweeps]),
                 vp([sw["ws"].data_ptr() for sw in sweeps]), i64([sw["ws"].numel() for sw in sweeps]),
-                vp([o.data_ptr() for o in outs]))
+                vp([o.data_ptr() for o in outs]),
+                (ctypes.c_void_p * rounds)(*[None if m is None else m.data_ptr() for m in self._maps]))
 
     def sweep_multi(self, plan):
         module, progs, *rest = plan
@@ -278,7 +317,7 @@ class KnitPipeline:
                           for l0, l1, j0, j1 in engine.label_chunks(offs, self.chunk_jobs)]
                 need = be.workspace_bytes(fs, max(c[3] - c[2] for c in chunks))
             self.sweeps.append(dict(lo=lo, n_local=n_local, slot=slot_t, sign=sign_t, off=off_t, n_jobs=n_jobs,
-                                    fused=fused, chunks=chunks,
+                                    fused=fused, chunks=chunks, label_offsets=sub.label_offsets,
                                     pjob=(None if fused else
                                           be.empty((max(n_jobs, 1), width), T.float64) if branching
                                           else alloc((max(rows, 1), width), T.float64)),

@@ -382,6 +382,7 @@ _MULTI_STRUCT = """struct qk_multi_args {
     long long n_jobs[4];
     long long begin[4];
     long long end[4];
+    const unsigned long long* map;
 };
 """
 
@@ -411,9 +412,21 @@ def generate_multi(encs: list) -> tuple[str, list]:
         body.append(f'extern "C" __global__ __launch_bounds__({NT}) void {name}(qk_multi_args a) {{')
         body.append(f"    __shared__ double2 lds[{1 << encs[0].tile_bits}];")
         body.append("    const long long b = blockIdx.x;")
+        # caller-ordered blocks (qk_sweep_compiled_multi block_maps): program << 56 | block in its range;
+        # otherwise the programs' block ranges in order
+        body.append("    int f = -1;")
+        body.append("    long long lb = 0;")
+        body.append("    if (a.map) {")
+        body.append("        const unsigned long long m = a.map[b];")
+        body.append("        f = (int)(m >> 56);")
+        body.append("        lb = (long long)(m & 0x00ffffffffffffffull);")
+        body.append("    } else {")
         for f in members:
-            body.append(f"    if (b >= a.begin[{f}] && b < a.end[{f}]) {{")
-            body.append(f"        qk_mb_{key}_f{f}_p{r}(lds, (unsigned)(b - a.begin[{f}]), a.slots[{f}], a.sign[{f}],")
+            body.append(f"        if (b >= a.begin[{f}] && b < a.end[{f}]) {{ f = {f}; lb = b - a.begin[{f}]; }}")
+        body.append("    }")
+        for f in members:
+            body.append(f"    if (f == {f} && lb >= 0 && lb < a.end[{f}] - a.begin[{f}]) {{")
+            body.append(f"        qk_mb_{key}_f{f}_p{r}(lds, (unsigned)lb, a.slots[{f}], a.sign[{f}],")
             body.append(f"            (double2*)a.state[{f}], a.out[{f}], a.n_jobs[{f}], a.label_off[{f}]);")
             body.append("        return;")
             body.append("    }")

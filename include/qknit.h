@@ -132,11 +132,15 @@ int qk_sweep_compiled_labels(qk_ctx* ctx, const qk_module* module, const qk_prog
  * sweep_codegen.generate_multi): pass round r of every program that has one runs in ONE launch, each
  * program on its own block range, so independent fragments share launches. Per program f (HOST
  * arrays of device pointers): label_offsets[f] non-NULL -> outs[f] = per-label rows as
- * qk_sweep_compiled_labels; NULL -> per-job rows as qk_sweep_compiled. */
+ * qk_sweep_compiled_labels; NULL -> per-job rows as qk_sweep_compiled.
+ * block_maps (HOST array, one entry per pass round, or NULL): a non-NULL block_maps[r] (DEVICE,
+ * one uint64 per block of round r) sends block b to program (map[b] >> 56), block
+ * (map[b] & (2^56 - 1)) of that program's range, so the caller orders the work (e.g. the FINAL
+ * pass's labels by descending branch-job count); entries outside a range are skipped. */
 int qk_sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, const qk_program* progs,
                             const int64_t* n_jobs, const double* const* job_slots, const double* const* job_sign,
                             const int64_t* n_labels, const int64_t* const* label_offsets, void* const* workspaces,
-                            const int64_t* workspace_bytes, double* const* outs);
+                            const int64_t* workspace_bytes, double* const* outs, const uint64_t* const* block_maps);
 
 /* q[l][x] = sum_{j in [offsets[l], offsets[l+1])} pjob[j][x]   (offsets: DEVICE, n_labels+1) */
 int qk_reduce_labels(qk_ctx* ctx, int64_t n_labels, const int64_t* offsets, int64_t width,
