@@ -16,6 +16,10 @@
 
 #include "internal.h"
 
+// tile widths of the per-program kernels: 2^(bits - 4) threads of 16 amplitudes, 2^bits x 16 B of LDS
+#define QK_JIT_TILE_MIN 10
+#define QK_JIT_TILE_MAX 13
+
 struct qk_module {
     hipModule_t mod = nullptr;
     std::vector<hipFunction_t> fns;
@@ -106,10 +110,10 @@ int sweep_compiled(qk_ctx* ctx, const qk_module* module, const qk_program* p, in
         const bool sparse_init = ip == 0 && p->n_passes > 1;  // qk_sweep: INIT tile of each job only
         const bool fin = ip == p->n_passes - 1;
         const int64_t units = (fin && label_off) ? n_labels : n_jobs;
-        // tile width of this program (12 or 13 state bits): 2^(bits - 4) threads of 16 amplitudes
+        // tile width of this program (10 to 13 state bits): 2^(bits - 4) threads of 16 amplitudes
         const int tb = __builtin_popcountll(p->passes[ip].tile_mask);
-        if (tb < QK_TILE_BITS || tb > QK_TILE_BITS + 1 || tb >= p->n)
-            return jfail(ctx, QK_EARG, "qk_sweep_compiled: tiles must hold 12 or 13 state bits");
+        if (tb < QK_JIT_TILE_MIN || tb > QK_JIT_TILE_MAX || tb >= p->n)
+            return jfail(ctx, QK_EARG, "qk_sweep_compiled: tiles must hold 10 to 13 state bits");
         const int64_t blocks = sparse_init ? n_jobs : (units << (p->n - tb));
         if (blocks > 0x7fffffff) return jfail(ctx, QK_EARG, "qk_sweep_compiled: too many tiles");
         struct {
@@ -170,8 +174,8 @@ int qk_sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, co
         if (p.packed || !p.passes || p.n_passes < 1 || p.n > 40)
             return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: SPLIT programs only");
         const int t = __builtin_popcountll(p.passes[0].tile_mask);
-        if ((f && t != tb) || t < QK_TILE_BITS || t > QK_TILE_BITS + 1 || t >= p.n)
-            return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: programs need one tile width of 12 or 13 bits");
+        if ((f && t != tb) || t < QK_JIT_TILE_MIN || t > QK_JIT_TILE_MAX || t >= p.n)
+            return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: programs need one tile width of 10 to 13 bits");
         tb = t;
         if (n_jobs[f] < 1 || !job_sign[f] || !outs[f] || (p.n_slots > 0 && !job_slots[f]))
             return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: empty program or null buffer");

@@ -107,10 +107,12 @@ class DeviceProgram:
     module: object = None  # qk_module* of the per-program kernels (SPLIT programs), or None
 
     @staticmethod
-    def upload(prog: FragmentProgram, device, jit: bool = True) -> "DeviceProgram":
+    def upload(prog: FragmentProgram, device, jit: bool = True, tile_bits: int | None = None) -> "DeviceProgram":
         T = torch()
-        # per-program kernels take 13-bit tiles (128 KiB LDS): fewer passes, less state traffic
-        enc = encode(prog, tile_bits=JIT_TILE_BITS if (jit and _jit_enabled()) else 12)
+        # per-program kernels take up to 13-bit tiles (128 KiB LDS: fewer passes, less state
+        # traffic); smaller ones when the batch is too small to fill the chip (jit_tile_bits)
+        jit = jit and _jit_enabled()
+        enc = encode(prog, tile_bits=(tile_bits or JIT_TILE_BITS_MAX) if jit else 12)
         dev = T.device("cuda", device)
 
         def to_dev(arr, dtype):
@@ -138,7 +140,24 @@ class DeviceProgram:
         return DeviceProgram(prog, enc, ops, groups, mats, passes, st, module)
 
 
-JIT_TILE_BITS = int(os.environ.get("QKNIT_JIT_TILE_BITS", "13"))
+JIT_TILE_BITS_MAX = 13
+JIT_TILE_BITS_MIN = 10
+JIT_MIN_BLOCKS = 128  # FINAL-pass workgroups a sweep should at least offer (256 CUs)
+
+
+def jit_tile_bits(sizes: list) -> int:
+    """Tile width of the per-program kernels of one sweep: ``sizes`` = (qubits, branch jobs) of its
+    SPLIT fragments (they share launches, so one width). The widest tile (13 bits: fewest passes)
+    whose FINAL pass still offers ``JIT_MIN_BLOCKS`` workgroups, else 10 bits: syc 32 5 (750 jobs)
+    keeps 13, the two single-instance fragments of syc 32 1 get 10 (2 x 64 workgroups instead of
+    2 x 8). ``QKNIT_JIT_TILE_BITS`` forces a width."""
+    env = os.environ.get("QKNIT_JIT_TILE_BITS")
+    if env:
+        return int(env)
+    for tb in range(JIT_TILE_BITS_MAX, JIT_TILE_BITS_MIN - 1, -1):
+        if sum(j << max(n - tb, 0) for n, j in sizes) >= JIT_MIN_BLOCKS:
+            return tb
+    return JIT_TILE_BITS_MIN
 
 
 def _jit_enabled() -> bool:
@@ -474,7 +493,7 @@ def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = 
     circ = virt.circuit
     cl = clbit_indexer(circ)
     vg = virt.vgate_instructions
-    out = []
+    out, want = [], []
     for frag, fcirc in virt.fragment_circuits.items():
         if len(frag) == 0:
             continue
@@ -490,11 +509,15 @@ def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = 
         # run.py:49-58 drops a fragment whose get_counts() raises, i.e. when some instance of
         # it measures nothing at all (no data measurement and no config measurement).
         dropped = prog.m == 0 and _some_label_unmeasured(prog, labels)
-        want = _worth_compiling(prog, jobs) if jit is None else (jit and len(prog.ops) <= 400)
-        dp = DeviceProgram.upload(prog, device, jit=want) if (upload and not dropped) else None
-        out.append(FragmentState(frag, labels, prog, dp, jobs, touches, dropped, uidx, unique,
+        want.append(_worth_compiling(prog, jobs) if jit is None else (jit and len(prog.ops) <= 400))
+        out.append(FragmentState(frag, labels, prog, None, jobs, touches, dropped, uidx, unique,
                                  red.labels if red is not None else None,
                                  red.expand if red is not None else None))
+    split = [(fs.prog.n, fs.jobs.n_jobs) for fs, w in zip(out, want) if w and not fs.dropped and fs.prog.n > 12]
+    tb = jit_tile_bits(split) if split else JIT_TILE_BITS_MAX
+    for fs, w in zip(out, want):
+        if upload and not fs.dropped:
+            fs.dprog = DeviceProgram.upload(fs.prog, device, jit=w, tile_bits=tb)
     return out
 
 
