@@ -54,6 +54,10 @@ SIGNATURES = {
                                      c_vp, c_vp]),
     "qk_knit_outer_stream": (c_i32, [c_vp, ctypes.c_int, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.c_uint64,
                                      ctypes.c_uint64, c_vp]),
+    "qk_knit_outer_stream_range": (c_i32, [c_vp, ctypes.c_int, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.c_uint64,
+                                           ctypes.c_uint64, c_i64, c_i64, c_vp, c_vp]),
+    "qk_rank_factors": (c_i32, [c_vp, c_i64, c_vp, c_vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                ctypes.c_int, c_vp, c_vp, c_vp]),
     "qk_khatri_rao": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "qk_gather_rows": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "qk_npd_workspace_bytes": (c_i32, [c_i64, c_i64, ctypes.POINTER(c_i64)]),

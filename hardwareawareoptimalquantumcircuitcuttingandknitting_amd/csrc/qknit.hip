@@ -1086,6 +1086,99 @@ __global__ __launch_bounds__(256) void qk_knit_outer_stream_kernel(OuterStreamAr
     }
 }
 
+// Blocked form of the same knit (the one used for outputs of >= 2^9 entries): the output is cut into
+// tasks of 2^TB consecutive entries (TB <= 16); within a task the bits >= TB are fixed, so its A / B
+// indices are pext(base) + pext(low bits): two short contiguous index ranges (K x 2^popcount(mask &
+// (2^TB - 1)) values each: syc 32 5, K = 2, TB = 16: 2 x 256 per side, 8 KiB). A workgroup stages
+// them in LDS once per task and then streams the task's 2^TB outputs with LDS reads only; a lane's
+// low-byte pext is hoisted out of the loop (its two output bits 0..7 never change). Each wave's 16-B
+// nontemporal stores cover one 1-KiB run, a task one contiguous 2^(TB+3)-byte block. tools/write_ab:
+// 6.5-6.8 TB/s on syc 32 5 (5.0-5.2 ms per 2^32-entry knit), above a grid-stride fill, where the
+// per-output L2 gathers of qk_knit_outer_stream_kernel reach 5.25 (6.55 ms).
+// Range form: outputs [o_begin, o_begin + o_count) (task-aligned) are written to out[o - o_begin]
+// (a rank's contiguous slice of the distribution); kdev (DEVICE int, or NULL) overrides K at run time,
+// and K <= 0 there skips the launch's work entirely (predicated knit, no host sync).
+struct OuterBlockedArgs {
+    int K, TB;
+    const double* __restrict__ A;
+    int64_t lda;
+    const double* __restrict__ B;
+    int64_t ldb;
+    uint32_t maskA, maskB;
+    int64_t task_begin, task_end;  // tasks [task_begin, task_end) of 2^TB outputs
+    int64_t o_begin;
+    const int32_t* kdev;
+    double* __restrict__ out;
+};
+
+__global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlockedArgs a) {
+    int K = a.K;
+    if (a.kdev) {
+        const int kd = *a.kdev;
+        if (kd <= 0) return;
+        K = kd < K ? kd : K;
+    }
+    __shared__ uint32_t tab[2][2][256];  // pext of bytes 0 / 1 of a task offset, per side
+    extern __shared__ double stage[];    // [K][na] of A then [K][nb] of B
+    const uint32_t low = (1u << a.TB) - 1u;
+    const uint32_t mAl = a.maskA & low, mBl = a.maskB & low;
+    const int na = 1 << __builtin_popcount(mAl), nb = 1 << __builtin_popcount(mBl);
+    double* sA = stage;
+    double* sB = stage + (int64_t)a.K * na;
+    for (int i = threadIdx.x; i < 512; i += 256) {
+        const int byte = i >> 8, v = i & 255;
+        tab[0][byte][v] = pext32((uint32_t)v << (8 * byte), mAl);
+        tab[1][byte][v] = pext32((uint32_t)v << (8 * byte), mBl);
+    }
+    __syncthreads();
+    const uint32_t r0 = tab[0][0][(2 * threadIdx.x) & 255], c0 = tab[1][0][(2 * threadIdx.x) & 255];
+    const int iters = (1 << a.TB) / 512;
+    for (int64_t t = a.task_begin + blockIdx.x; t < a.task_end; t += gridDim.x) {
+        const uint32_t base = (uint32_t)(t << a.TB);
+        const uint32_t ah = pext32(base, a.maskA), bh = pext32(base, a.maskB);
+        __syncthreads();  // the previous task's readers are done with the stage
+        for (int i = threadIdx.x; i < K * na; i += 256) {
+            const int k = i / na;
+            sA[i] = a.A[k * a.lda + ah + (i - k * na)];
+        }
+        for (int i = threadIdx.x; i < K * nb; i += 256) {
+            const int k = i / nb;
+            sB[i] = a.B[k * a.ldb + bh + (i - k * nb)];
+        }
+        __syncthreads();
+        double* o = a.out + ((int64_t)base - a.o_begin);
+#pragma unroll 4
+        for (int it = 0; it < iters; ++it) {
+            const uint32_t hi = (uint32_t)(2 * it + (threadIdx.x >> 7));  // byte 1 of the task offset
+            const uint32_t row = r0 + tab[0][1][hi], col = c0 + tab[1][1][hi];
+            d2_t acc = {0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < SK_MAX; ++k)
+                if (k < K) {
+                    const double av = sA[k * na + row];
+                    const d2_t bv = *reinterpret_cast<const d2_t*>(sB + k * nb + col);
+                    acc.x = fma(av, bv.x, acc.x);
+                    acc.y = fma(av, bv.y, acc.y);
+                }
+            __builtin_nontemporal_store(acc, reinterpret_cast<d2_t*>(o + 512 * it + 2 * threadIdx.x));
+        }
+    }
+}
+
+constexpr int64_t OB_STAGE_BYTES = 24 * 1024;  // LDS budget of the blocked kernel's operand stage
+constexpr int OB_WG_PER_CU = 16;
+
+// Widest task (TB <= 16, >= 9: one 512-output iteration) whose operand stage fits OB_STAGE_BYTES; 0: none.
+int outer_blocked_tile(int nbits, int64_t K, uint64_t maskA, uint64_t maskB) {
+    for (int tb = nbits < 16 ? nbits : 16; tb >= 9; --tb) {
+        const uint64_t low = (uint64_t(1) << tb) - 1;
+        const int64_t bytes = 8 * K * ((int64_t(1) << __builtin_popcountll(maskA & low)) +
+                                       (int64_t(1) << __builtin_popcountll(maskB & low)));
+        if (bytes <= OB_STAGE_BYTES) return tb;
+    }
+    return 0;
+}
+
 __global__ void qk_khatri_rao_kernel(int64_t K, int64_t M, int64_t N, const double* __restrict__ A,
                                      int64_t lda, const double* __restrict__ B, int64_t ldb,
                                      double* __restrict__ out) {
@@ -1322,6 +1415,15 @@ int qk_gemm_outer_paired(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const dou
 int qk_knit_outer_stream(qk_ctx* ctx, int nbits, int64_t K, const double* A, int64_t lda, const double* B,
                          int64_t ldb, uint64_t maskA, uint64_t maskB, double* out) {
     if (!ctx) return QK_EARG;
+    if (nbits < 2 || nbits > 32) return fail(ctx, QK_EARG, "qk_knit_outer_stream: need 2 <= nbits <= 32%s");
+    return qk_knit_outer_stream_range(ctx, nbits, K, A, lda, B, ldb, maskA, maskB, 0, int64_t(1) << nbits,
+                                      nullptr, out);
+}
+
+int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* A, int64_t lda, const double* B,
+                               int64_t ldb, uint64_t maskA, uint64_t maskB, int64_t o_begin, int64_t o_count,
+                               const int32_t* k_dev, double* out) {
+    if (!ctx) return QK_EARG;
     if (nbits < 2 || nbits > 32 || K < 1 || K > SK_MAX)
         return fail(ctx, QK_EARG, "qk_knit_outer_stream: need 2 <= nbits <= 32, 1 <= K <= 8%s");
     const uint64_t full = (uint64_t(1) << nbits) - 1;
@@ -1331,9 +1433,29 @@ int qk_knit_outer_stream(qk_ctx* ctx, int nbits, int64_t K, const double* A, int
     const int64_t M = int64_t(1) << __builtin_popcountll(maskA), N = int64_t(1) << __builtin_popcountll(maskB);
     if (lda < M || ldb < N || (ldb & 1) || ((reinterpret_cast<uintptr_t>(B) | reinterpret_cast<uintptr_t>(out)) & 15))
         return fail(ctx, QK_EARG, "qk_knit_outer_stream: leading dimension / alignment%s");
+    if (o_begin < 0 || o_count < 0 || o_begin + o_count > (int64_t(1) << nbits))
+        return fail(ctx, QK_EARG, "qk_knit_outer_stream: output range outside 0..2^nbits%s");
+    if (o_count == 0) return QK_OK;
     QK_HIP(ctx, hipSetDevice(ctx->device));
     int cus = 0;
     QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const int tb = outer_blocked_tile(nbits, K, maskA, maskB);
+    const int64_t tmask = (int64_t(1) << tb) - 1;
+    if (tb && !(o_begin & tmask) && !(o_count & tmask)) {
+        const uint64_t low = (uint64_t(1) << tb) - 1;
+        const size_t stage = 8 * (size_t)K * ((size_t(1) << __builtin_popcountll(maskA & low)) +
+                                              (size_t(1) << __builtin_popcountll(maskB & low)));
+        const int64_t tasks = o_count >> tb;
+        const int64_t G0 = (int64_t)cus * OB_WG_PER_CU;
+        OuterBlockedArgs b{(int)K, tb, A, lda, B, ldb, (uint32_t)maskA, (uint32_t)maskB, o_begin >> tb,
+                           (o_begin >> tb) + tasks, o_begin, k_dev, out};
+        hipLaunchKernelGGL(qk_knit_outer_blocked_kernel, dim3((unsigned)(tasks < G0 ? tasks : G0)), dim3(256), stage,
+                           ctx->stream, b);
+        QK_HIP(ctx, hipGetLastError());
+        return QK_OK;
+    }
+    if (o_begin != 0 || o_count != (int64_t(1) << nbits) || k_dev)
+        return fail(ctx, QK_EARG, "qk_knit_outer_stream: output ranges / device K need task-aligned ranges of >= 2^9%s");
     const int64_t chunks = (int64_t(1) << nbits) / OS_CHUNK;
     const int64_t G0 = (int64_t)cus * QK_OS_WG_PER_CU;
     const int64_t G = chunks < 1 ? 1 : (chunks < G0 ? chunks : G0);

@@ -1,0 +1,264 @@
+// qknit_rank.hip — data-rank factors of a two-fragment knit on the GPU, one workgroup, no host trip.
+//
+// Device form of data_rank.rank_factors (see that module for the math): pivoted Cholesky of the two
+// Gram matrices GA = A A^T, GB = B B^T (one wave per side, stopped on the residual trace), core
+// C = L_A^T L_B, its SVD by one-sided (Hestenes) Jacobi rotations on C's columns, the numerical rank r,
+// and T_X = S_r^{1/2} V_r^T L_X[P_X]^{-1} in the pivot columns, written as [rmax][K] (rows >= r zero)
+// with r in *r_out. r_out = 0 means "no usable factorisation" (R = 0, no convergence within 32 pivot
+// steps, or r > rmax): the caller's exact contraction then runs (predicated on the same int).
+// The step that consumes these (KnitPipeline) verifies the compressed product with probes on the
+// real operands before trusting it, on the device too.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "internal.h"
+
+namespace {
+
+constexpr int RK_K = 64;   // operand rows (K) the kernel handles
+constexpr int RK_RC = 32;  // pivoted-Cholesky steps per side
+constexpr int RK_R = 8;    // largest rank written (rows of TA / TB)
+constexpr int RK_THREADS = 128;
+constexpr int RK_MAX_SWEEPS = 40;
+
+struct RankArgs {
+    int K, rmax;
+    const double* GA;
+    const double* GB;
+    double lam_tol, s_tol, s_abs;
+    double* TA;
+    double* TB;
+    int32_t* r_out;
+};
+
+__device__ __forceinline__ double wsum(double v, int width = 64) {
+    for (int o = width >> 1; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a) {
+    __shared__ double G[2][RK_K][RK_K + 1];
+    __shared__ double L[2][RK_K][RK_RC + 1];
+    __shared__ double C[RK_RC][RK_RC + 1];   // core, then U S in its columns
+    __shared__ double W[RK_RC][RK_RC + 1];   // right rotations
+    __shared__ double Y[2][RK_R][RK_RC];     // triangular-solve results
+    __shared__ double sv[RK_RC];
+    __shared__ int piv[2][RK_RC], nsteps[2], conv[2], order[RK_RC], rank_s, rotated;
+
+    const int tid = threadIdx.x, lane = tid & 63, side = tid >> 6, K = a.K;
+    for (int e = tid; e < 2 * K * K; e += RK_THREADS) {
+        const int s = e / (K * K), i = (e / K) % K, j = e % K;
+        const double* g = s ? a.GB : a.GA;
+        G[s][i][j] = 0.5 * (g[i * K + j] + g[j * K + i]);
+    }
+    __syncthreads();
+
+    // ---- 1. pivoted Cholesky, wave `side` on Gram `side`, lane = row
+    double d = lane < K ? G[side][lane][lane] : 0.0;
+    bool alive = lane < K;
+    double dmax = d;
+    for (int o = 32; o >= 1; o >>= 1) dmax = fmax(dmax, __shfl_xor(dmax, o, 64));
+    bool active = dmax > 0.0, converged = !(dmax > 0.0);
+    int steps = 0;
+    for (int j = 0; j <= RK_RC; ++j) {  // both waves iterate alike: the barrier below is uniform
+        if (active) {
+            const double res = wsum(alive ? fmax(d, 0.0) : 0.0);
+            if (res <= a.lam_tol * dmax) {
+                converged = true;
+                active = false;
+            } else if (j == RK_RC) {
+                active = false;
+            } else {
+                double v = alive ? d : -1.0;
+                int idx = lane;
+                for (int o = 32; o >= 1; o >>= 1) {  // argmax, lowest index on ties
+                    const double v2 = __shfl_xor(v, o, 64);
+                    const int i2 = __shfl_xor(idx, o, 64);
+                    if (v2 > v || (v2 == v && i2 < idx)) {
+                        v = v2;
+                        idx = i2;
+                    }
+                }
+                const int p = idx;
+                const double dp = v;
+                if (!(dp > 0.0)) {
+                    active = false;
+                } else {
+                    double s = lane < K ? G[side][lane][p] : 0.0;
+                    for (int i = 0; i < j; ++i) s -= L[side][lane][i] * L[side][p][i];
+                    const double col = lane < K ? s / sqrt(dp) : 0.0;
+                    if (lane < K) L[side][lane][j] = col;
+                    d -= col * col;
+                    if (lane == p) {
+                        d = 0.0;
+                        alive = false;
+                        piv[side][j] = p;
+                    }
+                    steps = j + 1;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (lane == 0) {
+        nsteps[side] = steps;
+        conv[side] = converged ? 1 : 0;
+    }
+    __syncthreads();
+    const int ra = nsteps[0], rb = nsteps[1];
+    bool ok = conv[0] && conv[1] && ra > 0 && rb > 0;
+
+    // ---- 2. core C = L_A^T L_B, W = I
+    if (ok) {
+        for (int e = tid; e < ra * rb; e += RK_THREADS) {
+            const int i = e / rb, j = e % rb;
+            double s = 0.0;
+            for (int k = 0; k < K; ++k) s += L[0][k][i] * L[1][k][j];
+            C[i][j] = s;
+        }
+        for (int e = tid; e < rb * rb; e += RK_THREADS) W[e / rb][e % rb] = (e / rb == e % rb) ? 1.0 : 0.0;
+    }
+    __syncthreads();
+
+    // ---- 3. one-sided Jacobi on C's columns (round-robin pairs, one thread group per pair)
+    if (ok && rb > 1) {
+        const int n = rb + (rb & 1), npair = n / 2;
+        int tpp = RK_THREADS / npair;
+        tpp = tpp > 64 ? 64 : tpp;
+        int pw = 1;
+        while (pw * 2 <= tpp) pw *= 2;
+        tpp = pw;  // power of two, within one wave
+        const int g = tid / tpp, t = tid % tpp;
+        for (int sweep = 0; sweep < RK_MAX_SWEEPS; ++sweep) {
+            if (tid == 0) rotated = 0;
+            __syncthreads();
+            for (int round = 0; round < n - 1; ++round) {
+                int p = -1, q = -1;
+                if (g < npair) {
+                    if (g == 0) {
+                        p = round;
+                        q = n - 1;
+                    } else {
+                        p = (round + g) % (n - 1);
+                        q = (round - g + (n - 1)) % (n - 1);
+                    }
+                    if (p > q) {
+                        const int x = p;
+                        p = q;
+                        q = x;
+                    }
+                }
+                const bool live = g < npair && q < rb;
+                double al = 0.0, be = 0.0, ga = 0.0;
+                if (live)
+                    for (int i = t; i < ra; i += tpp) {
+                        const double cp = C[i][p], cq = C[i][q];
+                        al += cp * cp;
+                        be += cq * cq;
+                        ga += cp * cq;
+                    }
+                al = wsum(al, tpp);
+                be = wsum(be, tpp);
+                ga = wsum(ga, tpp);
+                if (live && ga != 0.0 && fabs(ga) > 1e-15 * sqrt(al * be)) {
+                    const double zeta = (be - al) / (2.0 * ga);
+                    const double tt = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                    const double c = 1.0 / sqrt(1.0 + tt * tt), s = c * tt;
+                    for (int i = t; i < ra; i += tpp) {
+                        const double cp = C[i][p], cq = C[i][q];
+                        C[i][p] = c * cp - s * cq;
+                        C[i][q] = s * cp + c * cq;
+                    }
+                    for (int i = t; i < rb; i += tpp) {
+                        const double wp = W[i][p], wq = W[i][q];
+                        W[i][p] = c * wp - s * wq;
+                        W[i][q] = s * wp + c * wq;
+                    }
+                    if (t == 0) rotated = 1;
+                }
+                __syncthreads();
+            }
+            const int any = rotated;
+            __syncthreads();
+            if (!any) break;
+        }
+    }
+
+    // ---- 4. singular values (column norms), descending order, rank
+    if (ok && tid < rb) {
+        double s = 0.0;
+        for (int i = 0; i < ra; ++i) s += C[i][tid] * C[i][tid];
+        sv[tid] = sqrt(s);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int r = 0;
+        if (ok) {
+            for (int j = 0; j < rb; ++j) order[j] = j;
+            for (int j = 0; j < rb; ++j)  // selection sort, stable
+                for (int k = j + 1; k < rb; ++k)
+                    if (sv[order[k]] > sv[order[j]]) {
+                        const int x = order[j];
+                        order[j] = order[k];
+                        order[k] = x;
+                    }
+            const double s0 = sv[order[0]];
+            const double cut = fmax(a.s_tol * s0, a.s_abs);
+            if (s0 > 0.0)
+                for (int j = 0; j < rb; ++j) r += sv[order[j]] > cut ? 1 : 0;
+            if (r > a.rmax || r > ra) r = 0;
+        }
+        rank_s = r;
+    }
+    for (int e = tid; e < a.rmax * K; e += RK_THREADS) {
+        a.TA[e] = 0.0;
+        a.TB[e] = 0.0;
+    }
+    __syncthreads();
+    const int r = rank_s;
+
+    // ---- 5. T_X[j][piv_X[i]] = sqrt(s_j) y_i,  L_X[P_X]^T y = v_j  (back-substitution, one thread each)
+    if (tid < 2 * r) {
+        const int sd = tid / r, j = tid % r, col = order[j];
+        const int rx = sd ? rb : ra;
+        const double sj = sv[col];
+        double* y = Y[sd][j];
+        for (int i = rx - 1; i >= 0; --i) {
+            double v = sd ? W[i][col] : C[i][col] / sj;
+            for (int k = i + 1; k < rx; ++k) v -= L[sd][piv[sd][k]][i] * y[k];
+            y[i] = v / L[sd][piv[sd][i]][i];
+        }
+        double* T = sd ? a.TB : a.TA;
+        const double rs = sqrt(sj);
+        for (int i = 0; i < rx; ++i) T[j * K + piv[sd][i]] = rs * y[i];
+    }
+    if (tid == 0) *a.r_out = r;
+}
+
+}  // namespace
+
+extern "C" int qk_rank_factors(qk_ctx* ctx, int64_t K, const double* GA, const double* GB, double lam_tol,
+                               double s_tol, double s_abs, int rmax, double* TA, double* TB, int32_t* r_out) {
+    if (!ctx) return QK_EARG;
+    if (K < 1 || K > RK_K || rmax < 1 || rmax > RK_R) {
+        ctx->err = "qk_rank_factors: need 1 <= K <= 64 and 1 <= rmax <= 8";
+        return QK_EARG;
+    }
+    if (!GA || !GB || !TA || !TB || !r_out) {
+        ctx->err = "qk_rank_factors: null buffer";
+        return QK_EARG;
+    }
+    if (hipSetDevice(ctx->device) != hipSuccess) {
+        ctx->err = "qk_rank_factors: hipSetDevice";
+        return QK_EHIP;
+    }
+    RankArgs args{(int)K, rmax, GA, GB, lam_tol, s_tol, s_abs, TA, TB, r_out};
+    hipLaunchKernelGGL(qk_rank_factors_kernel, dim3(1), dim3(RK_THREADS), 0, ctx->stream, args);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        ctx->err = std::string("qk_rank_factors: ") + hipGetErrorString(e);
+        return QK_EHIP;
+    }
+    return QK_OK;
+}

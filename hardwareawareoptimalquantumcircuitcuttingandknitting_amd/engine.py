@@ -387,18 +387,25 @@ def gemm_outer_paired(ctx: Context, A, B, keyB, keyA=None, out=None, strideA: in
     return out
 
 
-def knit_outer_stream(ctx: Context, A, B, clbits_a: list, clbits_b: list, nbits: int, out):
-    """Two-fragment small-K knit written in output order (``qk_knit_outer_stream``):
-    ``out[o] = sum_k A[k, pext(o, mask_a)] * B[k, pext(o, mask_b)]`` for every ``o < 2^nbits``.
-    Needs the fragments' clbits to split ``0..nbits-1`` with clbit 0 on the B side
-    (:func:`stream_knit_ok`)."""
+def knit_outer_stream(ctx: Context, A, B, clbits_a: list, clbits_b: list, nbits: int, out,
+                      o_begin: int = 0, o_count: int | None = None, k_dev=None):
+    """Two-fragment small-K knit written in output order (``qk_knit_outer_stream_range``):
+    ``out[o - o_begin] = sum_k A[k, pext(o, mask_a)] * B[k, pext(o, mask_b)]`` for
+    ``o_begin <= o < o_begin + o_count`` (default: all ``2^nbits``). Needs the fragments' clbits to
+    split ``0..nbits-1`` with clbit 0 on the B side (:func:`stream_knit_ok`). ``k_dev`` (device
+    int32 tensor): run-time K (0: write nothing)."""
     K, M = A.shape
     K2, N = B.shape
     assert K == K2 and 1 <= K <= 8 and A.is_contiguous() and B.is_contiguous()
     mA, mB = sum(1 << c for c in clbits_a), sum(1 << c for c in clbits_b)
-    assert M == 1 << len(clbits_a) and N == 1 << len(clbits_b) and out.numel() >= 1 << nbits
-    ctx.check(ctx.lib.qk_knit_outer_stream(ctx.handle, nbits, K, A.data_ptr(), M, B.data_ptr(), N, mA, mB,
-                                           out.data_ptr()), "qk_knit_outer_stream")
+    if o_count is None:
+        o_count = (1 << nbits) - o_begin
+    assert M == 1 << len(clbits_a) and N == 1 << len(clbits_b) and out.numel() >= o_count
+    if k_dev is not None:
+        assert k_dev.dtype == torch().int32 and k_dev.device == out.device
+    ctx.check(ctx.lib.qk_knit_outer_stream_range(ctx.handle, nbits, K, A.data_ptr(), M, B.data_ptr(), N, mA, mB,
+                                                 o_begin, o_count, _ptr(k_dev), out.data_ptr()),
+              "qk_knit_outer_stream_range")
     return out
 
 
@@ -643,72 +650,29 @@ def _compress_core(transforms: list, terms: int, tol: float = 1e-10):
     return [np.ascontiguousarray((U[:, :r] * S[:r]).T), np.ascontiguousarray(Vt[:r])], r
 
 
-def _dominant_eig(G: np.ndarray, tol: float):
-    """Eigenpairs of the PSD matrix G with eigenvalue above ``tol * max``, ascending. A greedy
-    pivoted Cholesky ``G ~= L L^T`` (stopped when every residual diagonal is below ``tol *
-    max diag / 4``) first finds the dominant subspace, so the eigensolver runs on the small
-    ``L^T L`` (r x r; 64x64 LAPACK eigh costs ~0.2 ms on the host, r = 8 a few us). Falls back
-    to the full eigh when the pivoting does not reduce the size."""
-    K = G.shape[0]
-    d = np.diag(G).copy()
-    dmax = d.max() if K else 0.0
-    if dmax <= 0:
-        return np.zeros(0), np.zeros((K, 0))
-    L = np.zeros((K, K))
-    r = 0
-    while r < K // 2:
-        p = int(np.argmax(d))
-        if d[p] <= 0.25 * tol * dmax:
-            break
-        col = (G[:, p] - L[:, :r] @ L[p, :r]) / np.sqrt(d[p])
-        L[:, r] = col
-        d -= col * col
-        d[p] = 0.0
-        r += 1
-    if r >= K // 2:
-        lam, V = np.linalg.eigh(G)
-    else:
-        Lr = L[:, :r]
-        mu, U = np.linalg.eigh(Lr.T @ Lr)  # G ~= (Lr U) diag(mu) (Lr U)^T / mu^2 scaling below
-        keep = mu > 0
-        lam, V = mu[keep], (Lr @ U[:, keep]) / np.sqrt(mu[keep])
-    keep = lam > tol * lam.max() if lam.size else lam.astype(bool)
-    return lam[keep], V[:, keep]
+def data_rank_factors(GA: np.ndarray, GB: np.ndarray, **kw):
+    """Rank factors of a two-fragment knit from its Grams (:func:`data_rank.rank_factors`)."""
+    from .data_rank import rank_factors
+
+    return rank_factors(GA, GB, **kw)
 
 
-def data_rank_factors(GA: np.ndarray, GB: np.ndarray, lam_tol: float = 1e-12, s_tol: float = 1e-13,
-                      s_abs: float = 1e-15):
-    """Rank factors of a two-fragment knit ``R = A^T B`` from its Gram matrices.
+def rank_factors_device(ctx: Context, GA, GB, rmax: int = 8, out=None):
+    """``qk_rank_factors`` on device Grams: ``(TA, TB, r)`` device tensors ([rmax, K] fp64 twice,
+    int32 [1]); no host synchronisation. ``r = 0``: no usable factorisation."""
+    from . import data_rank as dr
 
-    ``GA = A A^T``, ``GB = B B^T`` ([K, K]). With ``GA = V_A L_A V_A^T`` (eigenvalues above
-    ``lam_tol * max`` kept), ``A^T V_A = Q_A L_A^{1/2}`` with orthonormal ``Q_A``, so
-    ``R ~= Q_A Y Q_B^T``, ``Y = L_A^{1/2} V_A^T V_B L_B^{1/2}``; the SVD ``Y = U S W^T``
-    truncated at ``max(s_tol * s_max, s_abs)`` (a dropped singular value moves entries of R by at
-    most itself; ``s_abs`` = 1e-15 is three orders below the 1e-12 per-entry tolerance) gives ``R ~= A^T T_A^T T_B B`` with
-    ``T_A = (V_A L_A^{-1/2} U_r S_r^{1/2})^T`` and ``T_B = (V_B L_B^{-1/2} W_r S_r^{1/2})^T``
-    ([r, K] each). The dropped directions are checked by the caller on the real operands
-    (``KnitPipeline._rank_compress``), not trusted from the Grams. Returns None for R = 0."""
-    la, Va = _dominant_eig(0.5 * (GA + GA.T), lam_tol)
-    lb, Vb = _dominant_eig(0.5 * (GB + GB.T), lam_tol)
-    if la.size == 0 or lb.size == 0 or la[-1] <= 0 or lb[-1] <= 0:
-        return None
-    ka, kb = la > lam_tol * la[-1], lb > lam_tol * lb[-1]
-    Va, la, Vb, lb = Va[:, ka], la[ka], Vb[:, kb], lb[kb]
-    sa, sb = np.sqrt(la), np.sqrt(lb)
-    Y = (sa[:, None] * (Va.T @ Vb)) * sb[None, :]
-    U, s, Wt = np.linalg.svd(Y)
-    if s.size == 0 or s[0] <= 0:
-        return None
-    r = int((s > max(s_tol * s[0], s_abs)).sum())
-    if os.environ.get("QKNIT_DEBUG_RANK"):
-        print(f"data_rank: kept eig {int(ka.sum())}/{ka.size}, {int(kb.sum())}/{kb.size}; core svals "
-              f"{np.array2string(s[:10], precision=2)} -> r = {r}", flush=True)
-    if r == 0:
-        return None
-    rs = np.sqrt(s[:r])
-    TA = ((Va / sa) @ (U[:, :r] * rs)).T
-    TB = ((Vb / sb) @ (Wt[:r].T * rs)).T
-    return np.ascontiguousarray(TA), np.ascontiguousarray(TB)
+    T = torch()
+    K = GA.shape[0]
+    assert GA.shape == (K, K) and GB.shape == (K, K) and GA.is_contiguous() and GB.is_contiguous()
+    if out is None:
+        out = (T.empty((rmax, K), dtype=T.float64, device=GA.device), T.empty((rmax, K), dtype=T.float64,
+                                                                              device=GA.device),
+               T.empty(1, dtype=T.int32, device=GA.device))
+    TA, TB, r = out
+    ctx.check(ctx.lib.qk_rank_factors(ctx.handle, K, GA.data_ptr(), GB.data_ptr(), dr.LAM_TOL, dr.S_TOL, dr.S_ABS,
+                                      rmax, TA.data_ptr(), TB.data_ptr(), r.data_ptr()), "qk_rank_factors")
+    return TA, TB, r
 
 
 def _endpoints(virt, j):

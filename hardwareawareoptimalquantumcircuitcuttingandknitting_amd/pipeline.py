@@ -581,7 +581,7 @@ class KnitPipeline:
         if on_gpu:
             ready.synchronize()
         Gh = self._pinned.numpy()
-        f = engine.data_rank_factors(Gh[0], Gh[1])
+        f = engine.data_rank_factors(Gh[0], Gh[1], rmax=K, rc_max=K)
         if f is None or f[0].shape[0] >= K:
             self.last_rank = K
             return None

@@ -172,6 +172,16 @@ int qk_gemm_outer_paired(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const dou
 int qk_knit_outer_stream(qk_ctx* ctx, int nbits, int64_t K, const double* A, int64_t lda, const double* B,
                          int64_t ldb, uint64_t maskA, uint64_t maskB, double* out);
 
+/* qk_knit_outer_stream over the output range [o_begin, o_begin + o_count) only, written to
+ * out[o - o_begin] (a rank's contiguous slice of the distribution: multi-GPU slice mode). k_dev
+ * (DEVICE int32, or NULL) overrides K at run time (min(K, *k_dev)); *k_dev <= 0 makes the call write
+ * nothing (a knit predicated on a device-side check, no host sync). Ranges and k_dev need the blocked
+ * kernel: o_begin and o_count multiples of its task size 2^TB (TB <= 16, chosen so the K x (2^a + 2^b)
+ * staged operand values fit 24 KiB of LDS; 2^16 for syc 32 5 at K <= 8). */
+int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* A, int64_t lda, const double* B,
+                               int64_t ldb, uint64_t maskA, uint64_t maskB, int64_t o_begin, int64_t o_count,
+                               const int32_t* k_dev, double* out);
+
 /* out[k][i + j*M] = A[k*lda + i] * B[k*ldb + j] */
 int qk_khatri_rao(qk_ctx* ctx, int64_t K, int64_t M, int64_t N, const double* A, int64_t lda,
                   const double* B, int64_t ldb, double* out);
@@ -179,6 +189,17 @@ int qk_khatri_rao(qk_ctx* ctx, int64_t K, int64_t M, int64_t N, const double* A,
 /* dst[r][x] = coef[r] * src[idx[r]][x]  (width columns, rows R) */
 int qk_gather_rows(qk_ctx* ctx, int64_t R, int64_t width, const int64_t* idx, const double* coef,
                    const double* src, double* dst);
+
+/* ---- data-rank factors (qknit_rank.hip; data_rank.py is the host form) ----------------------
+ * Two-fragment knit R = A^T B (A: [K][M], B: [K][N] operands of virtual_circuit.py:50-68's knit)
+ * from its Gram matrices GA = A A^T, GB = B B^T ([K][K], DEVICE): pivoted Cholesky of each Gram
+ * (stopped when the residual trace is <= lam_tol * max diagonal, at most 32 steps), core SVD by
+ * one-sided Jacobi, rank r = #{s > max(s_tol s_0, s_abs)}; writes TA, TB ([rmax][K], DEVICE, rows >= r
+ * zero) with R ~= (TA A)^T (TB B), and *r_out (DEVICE int32) = r, or 0 when there is no usable
+ * factorisation (R = 0, no convergence, r > rmax). One workgroup; K <= 64, rmax <= 8. The caller
+ * verifies the product before trusting it (KnitPipeline: probes on the real operands). */
+int qk_rank_factors(qk_ctx* ctx, int64_t K, const double* GA, const double* GB, double lam_tol, double s_tol,
+                    double s_abs, int rmax, double* TA, double* TB, int32_t* r_out);
 
 /* ---- post-processing (reference-shaped results; quasi_distr.py:3-43, run.py:71) ---------- */
 

@@ -592,15 +592,19 @@ def test_syc_32_5_data_rank_step_matches_exact_step(T):
     T.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("K,bits_b", [(1, [0, 1, 2, 5, 6, 9]), (2, [0, 3, 4, 5, 10]), (8, [0, 1, 2, 3, 8, 9, 10])])
-def test_knit_outer_stream_matches_torch(T, K, bits_b):
-    """qk_knit_outer_stream: the small-K two-fragment knit written in output order equals
-    A^T B scattered through the deposit keys of the two clbit sets (11 output bits; partial
-    last chunk and several interleavings)."""
+@pytest.mark.parametrize("K,nbits,bits_b", [(1, 11, [0, 1, 2, 5, 6, 9]), (2, 11, [0, 3, 4, 5, 10]),
+                                            (8, 11, [0, 1, 2, 3, 8, 9, 10]), (2, 3, [0, 2]), (3, 9, [0, 2, 5, 6]),
+                                            (2, 17, [0, 1, 2, 3, 8, 9, 10, 11, 16]),
+                                            (8, 18, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])])
+def test_knit_outer_stream_matches_torch(T, K, nbits, bits_b):
+    """qk_knit_outer_stream: the small-K two-fragment knit written in output order equals A^T B
+    scattered through the deposit keys of the two clbit sets. nbits 3: the per-output kernel on a
+    single partial chunk (8 outputs, grid of 1); nbits >= 9: the blocked kernel (tasks of 2^TB
+    outputs, TB <= 16, the operand stage in LDS); nbits 18 / K 8 / 14 low B bits: no task size fits
+    the stage budget, the per-output kernel again."""
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.knit_plan import deposit_keys
 
     ctx = engine.get_context(0)
-    nbits = 11
     bits_a = [b for b in range(nbits) if b not in bits_b]
     assert engine.stream_knit_ok(bits_a, bits_b, nbits)
     M, N = 1 << len(bits_a), 1 << len(bits_b)
@@ -615,3 +619,83 @@ def test_knit_outer_stream_matches_torch(T, K, bits_b):
     got = out[(ka[:, None] + kb[None, :]).reshape(-1)].view(M, N)
     assert not bool(out.isnan().any())
     assert float((got - A.T @ B).abs().max()) <= 1e-12 * K
+
+
+def test_knit_outer_stream_range_slices_and_device_k(T):
+    """qk_knit_outer_stream_range: 4 task-aligned slices written separately concatenate to the
+    whole knit bit for bit (multi-GPU slice mode); a device K of 0 writes nothing, a device K of 1
+    keeps only the first term (predicated knit)."""
+    ctx = engine.get_context(0)
+    nbits, K = 18, 3
+    bits_b = [0, 1, 2, 3, 8, 9, 10, 11, 16, 17]
+    bits_a = [b for b in range(nbits) if b not in bits_b]
+    g = T.Generator(device="cuda").manual_seed(5)
+    A = T.randn(K, 1 << len(bits_a), dtype=T.float64, device="cuda", generator=g)
+    B = T.randn(K, 1 << len(bits_b), dtype=T.float64, device="cuda", generator=g)
+    full = T.empty(1 << nbits, dtype=T.float64, device="cuda")
+    engine.knit_outer_stream(ctx, A, B, bits_a, bits_b, nbits, full)
+    parts = []
+    step = (1 << nbits) // 4
+    for r in range(4):
+        part = T.full((step,), float("nan"), dtype=T.float64, device="cuda")
+        engine.knit_outer_stream(ctx, A, B, bits_a, bits_b, nbits, part, o_begin=r * step, o_count=step)
+        parts.append(part)
+    T.cuda.synchronize()
+    assert T.equal(T.cat(parts), full)
+    kd = T.zeros(1, dtype=T.int32, device="cuda")
+    sentinel = T.full((1 << nbits,), 7.0, dtype=T.float64, device="cuda")
+    engine.knit_outer_stream(ctx, A, B, bits_a, bits_b, nbits, sentinel, k_dev=kd)
+    T.cuda.synchronize()
+    assert bool((sentinel == 7.0).all())
+    kd.fill_(1)
+    one = T.empty(1 << nbits, dtype=T.float64, device="cuda")
+    engine.knit_outer_stream(ctx, A, B, bits_a, bits_b, nbits, one, k_dev=kd)
+    ref = T.empty(1 << nbits, dtype=T.float64, device="cuda")
+    engine.knit_outer_stream(ctx, A[:1].contiguous(), B[:1].contiguous(), bits_a, bits_b, nbits, ref)
+    T.cuda.synchronize()
+    assert T.equal(one, ref)
+
+
+@pytest.mark.parametrize("K,ra,rb,r", [(64, 8, 8, 2), (64, 5, 12, 4), (24, 3, 3, 3), (64, 20, 20, 8), (16, 16, 16, 12)])
+def test_rank_factors_device_matches_host(T, K, ra, rb, r):
+    """qk_rank_factors (one-workgroup pivoted Cholesky + one-sided Jacobi SVD) reproduces the
+    low-rank product like data_rank.rank_factors (host form); rank > 8 reports r = 0 (exact path)."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import data_rank
+
+    rng = np.random.default_rng(K + ra + rb + r)
+    M, N = 3000, 2000
+    core = rng.standard_normal((ra, r)) @ rng.standard_normal((r, rb))
+    PA = rng.standard_normal((K, ra))
+    PB = np.linalg.pinv(PA.T) @ core
+    XA, XB = rng.standard_normal((ra, M)), rng.standard_normal((rb, N))
+    A, B = PA @ XA, PB @ XB
+    R = A.T @ B
+    At, Bt = T.from_numpy(A).cuda(), T.from_numpy(B).cuda()
+    GA, GB = (At @ At.T).contiguous(), (Bt @ Bt.T).contiguous()
+    TA, TB, rd = engine.rank_factors_device(engine.get_context(0), GA, GB)
+    T.cuda.synchronize()
+    got_r = int(rd.item())
+    host = data_rank.rank_factors(GA.cpu().numpy(), GB.cpu().numpy())
+    if r > 8:
+        assert got_r == 0 and host is None
+        return
+    assert got_r == r and host is not None and host[0].shape[0] == r
+    assert float(TA[r:].abs().sum()) == 0.0 and float(TB[r:].abs().sum()) == 0.0
+    Rd = ((TA @ At).T @ (TB @ Bt)).cpu().numpy()
+    Rh = (host[0] @ A).T @ (host[1] @ B)
+    scale = np.abs(R).max()
+    assert np.abs(Rd - R).max() <= 1e-9 * scale
+    assert np.abs(Rh - R).max() <= 1e-9 * scale
+
+
+def test_rank_factors_device_degenerate(T):
+    """A zero Gram (R = 0) and a non-PSD garbage Gram give r = 0 and zero factors."""
+    ctx = engine.get_context(0)
+    K = 16
+    Z = T.zeros((K, K), dtype=T.float64, device="cuda")
+    I = T.eye(K, dtype=T.float64, device="cuda")
+    for GA, GB in ((Z, I), (I, Z), (-I, I)):
+        TA, TB, rd = engine.rank_factors_device(ctx, GA.contiguous(), GB.contiguous())
+        T.cuda.synchronize()
+        assert int(rd.item()) == 0
+        assert float(TA.abs().max()) == 0.0 and float(TB.abs().max()) == 0.0

@@ -1,0 +1,269 @@
+// write_ab.hip — A/B of output-write-bound knit kernels on one MI355X (standalone, hipcc).
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/write_ab.hip -o tools/write_ab && tools/write_ab [K]
+//
+// out[o] = sum_k A[k][pext(o, mA)] * B[k][pext(o, mB)] over all o < 2^32 (syc 32 5: mA = 0xF0F0F0F0,
+// mB = 0x0F0F0F0F, K = 2 after data-rank compression), 34.4 GB of fp64 written per launch. Variants:
+//   fill      16-B nontemporal stores of a constant (the write ceiling of this store pattern)
+//   stream    the product kernel's scheme (qk_knit_outer_stream_kernel): per-byte pext tables in LDS,
+//             A/B gathered from L1/L2 per output pair
+//   noload    stream's index math and stores, no operand loads
+//   blocked   tasks of 2^16 consecutive outputs: the task's A/B index ranges staged in LDS once
+//             (K x 2 x 256 values), then per pair only LDS reads; byte-0 pext per lane hoisted
+// Each variant is timed 6 times (first dropped, median printed) and checked against stream on
+// sampled outputs. Not product code: a measurement tool whose result decides the product kernel.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHECK(x)                                                                  \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                              \
+        }                                                                         \
+    } while (0)
+
+typedef double d2_t __attribute__((ext_vector_type(2)));
+constexpr int KMAX = 8;
+
+__host__ __device__ inline uint32_t pext32(uint32_t x, uint32_t mask) {
+    uint32_t r = 0, bit = 1;
+    for (; mask; mask &= mask - 1, bit <<= 1)
+        if (x & mask & (~mask + 1)) r |= bit;
+    return r;
+}
+
+__global__ __launch_bounds__(256) void k_fill(double* __restrict__ out, int64_t total) {
+    const d2_t v = {1.0, 2.0};
+    for (int64_t o = 2 * ((int64_t)blockIdx.x * 256 + threadIdx.x); o < total; o += 2 * (int64_t)gridDim.x * 256)
+        __builtin_nontemporal_store(v, reinterpret_cast<d2_t*>(out + o));
+}
+
+template <bool LOAD>
+__global__ __launch_bounds__(256) void k_stream(int K, const double* __restrict__ A, const double* __restrict__ B,
+                                                int64_t ld, uint32_t mA, uint32_t mB, double* __restrict__ out,
+                                                int64_t total) {
+    __shared__ uint32_t tab[2][4][256];
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+        const int byte = i >> 8, v = i & 255;
+        tab[0][byte][v] = pext32((uint32_t)v << (8 * byte), mA);
+        tab[1][byte][v] = pext32((uint32_t)v << (8 * byte), mB);
+    }
+    __syncthreads();
+    for (int64_t c0 = (int64_t)blockIdx.x * 512; c0 < total; c0 += (int64_t)gridDim.x * 512) {
+        const int64_t o = c0 + 2 * threadIdx.x;
+        const uint32_t x = (uint32_t)o;
+        uint32_t row = 0, col = 0;
+#pragma unroll
+        for (int byte = 0; byte < 4; ++byte) {
+            const uint32_t b = (x >> (8 * byte)) & 255;
+            row += tab[0][byte][b];
+            col += tab[1][byte][b];
+        }
+        d2_t acc = {0.0, 0.0};
+        if (LOAD) {
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k)
+                if (k < K) {
+                    const double av = A[k * ld + row];
+                    const d2_t bv = *reinterpret_cast<const d2_t*>(B + k * ld + col);
+                    acc.x = fma(av, bv.x, acc.x);
+                    acc.y = fma(av, bv.y, acc.y);
+                }
+        } else {
+            acc.x = (double)row;
+            acc.y = (double)col;
+        }
+        __builtin_nontemporal_store(acc, reinterpret_cast<d2_t*>(out + o));
+    }
+}
+
+// tasks of 2^TB outputs; per task the A / B index ranges (2^popcount(m & low) values each) in LDS
+template <int TB>
+__global__ __launch_bounds__(256) void k_blocked(int K, const double* __restrict__ A, const double* __restrict__ B,
+                                                 int64_t ld, uint32_t mA, uint32_t mB, double* __restrict__ out,
+                                                 int64_t total) {
+    constexpr uint32_t LOW = (1u << TB) - 1;
+    __shared__ uint32_t tab[2][2][256];  // low two bytes of the task offset
+    __shared__ double sA[KMAX * 256];
+    __shared__ double sB[KMAX * 256];
+    const uint32_t mAl = mA & LOW, mBl = mB & LOW;
+    const int na = 1 << __builtin_popcount(mAl), nb = 1 << __builtin_popcount(mBl);
+    for (int i = threadIdx.x; i < 512; i += 256) {
+        const int byte = i >> 8, v = i & 255;
+        tab[0][byte][v] = pext32((uint32_t)v << (8 * byte), mAl);
+        tab[1][byte][v] = pext32((uint32_t)v << (8 * byte), mBl);
+    }
+    __syncthreads();
+    const uint32_t r0 = tab[0][0][(2 * threadIdx.x) & 255], c0 = tab[1][0][(2 * threadIdx.x) & 255];
+    const int64_t tasks = total >> TB;
+    for (int64_t t = blockIdx.x; t < tasks; t += gridDim.x) {
+        const uint32_t base = (uint32_t)(t << TB);
+        const uint32_t ah = pext32(base, mA), bh = pext32(base, mB);
+        __syncthreads();  // previous task's readers are done
+        for (int i = threadIdx.x; i < K * na; i += 256) sA[i] = A[(i / na) * ld + ah + (i % na)];
+        for (int i = threadIdx.x; i < K * nb; i += 256) sB[i] = B[(i / nb) * ld + bh + (i % nb)];
+        __syncthreads();
+        double* o = out + base;
+#pragma unroll 4
+        for (int it = 0; it < (1 << TB) / 512; ++it) {
+            const uint32_t hi = (uint32_t)(2 * it + (threadIdx.x >> 7));  // byte 1 of the pair index
+            const uint32_t row = r0 + tab[0][1][hi & 255], col = c0 + tab[1][1][hi & 255];
+            d2_t acc = {0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k)
+                if (k < K) {
+                    const double av = sA[k * na + row];
+                    const d2_t bv = *reinterpret_cast<const d2_t*>(sB + k * nb + col);
+                    acc.x = fma(av, bv.x, acc.x);
+                    acc.y = fma(av, bv.y, acc.y);
+                }
+            __builtin_nontemporal_store(acc, reinterpret_cast<d2_t*>(o + 512 * it + 2 * threadIdx.x));
+        }
+    }
+}
+
+// as k_blocked, LDS sized for K at launch (dynamic), optional contiguous task ranges per workgroup
+template <int TB, bool CONTIG>
+__global__ __launch_bounds__(256) void k_blocked_dyn(int K, const double* __restrict__ A, const double* __restrict__ B,
+                                                     int64_t ld, uint32_t mA, uint32_t mB, double* __restrict__ out,
+                                                     int64_t total) {
+    constexpr uint32_t LOW = (1u << TB) - 1;
+    __shared__ uint32_t tab[2][2][256];
+    extern __shared__ double dyn[];
+    const uint32_t mAl = mA & LOW, mBl = mB & LOW;
+    const int na = 1 << __builtin_popcount(mAl), nb = 1 << __builtin_popcount(mBl);
+    double* sA = dyn;
+    double* sB = dyn + K * na;
+    for (int i = threadIdx.x; i < 512; i += 256) {
+        const int byte = i >> 8, v = i & 255;
+        tab[0][byte][v] = pext32((uint32_t)v << (8 * byte), mAl);
+        tab[1][byte][v] = pext32((uint32_t)v << (8 * byte), mBl);
+    }
+    __syncthreads();
+    const uint32_t r0 = tab[0][0][(2 * threadIdx.x) & 255], c0 = tab[1][0][(2 * threadIdx.x) & 255];
+    const int64_t tasks = total >> TB;
+    const int64_t per = (tasks + gridDim.x - 1) / gridDim.x;
+    const int64_t t0 = CONTIG ? blockIdx.x * per : blockIdx.x, t1 = CONTIG ? std::min(tasks, t0 + per) : tasks;
+    const int64_t step = CONTIG ? 1 : gridDim.x;
+    for (int64_t t = t0; t < t1; t += step) {
+        const uint32_t base = (uint32_t)(t << TB);
+        const uint32_t ah = pext32(base, mA), bh = pext32(base, mB);
+        __syncthreads();
+        for (int i = threadIdx.x; i < K * na; i += 256) sA[i] = A[(i / na) * ld + ah + (i % na)];
+        for (int i = threadIdx.x; i < K * nb; i += 256) sB[i] = B[(i / nb) * ld + bh + (i % nb)];
+        __syncthreads();
+        double* o = out + base;
+#pragma unroll 4
+        for (int it = 0; it < (1 << TB) / 512; ++it) {
+            const uint32_t hi = (uint32_t)(2 * it + (threadIdx.x >> 7));
+            const uint32_t row = r0 + tab[0][1][hi & 255], col = c0 + tab[1][1][hi & 255];
+            d2_t acc = {0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k)
+                if (k < K) {
+                    const double av = sA[k * na + row];
+                    const d2_t bv = *reinterpret_cast<const d2_t*>(sB + k * nb + col);
+                    acc.x = fma(av, bv.x, acc.x);
+                    acc.y = fma(av, bv.y, acc.y);
+                }
+            __builtin_nontemporal_store(acc, reinterpret_cast<d2_t*>(o + 512 * it + 2 * threadIdx.x));
+        }
+    }
+}
+
+int main(int argc, char** argv) {
+    const int K = argc > 1 ? atoi(argv[1]) : 2;
+    const int nbits = 32;
+    const int64_t total = int64_t(1) << nbits, N = 1 << 16;
+    const uint32_t mA = 0xF0F0F0F0u, mB = 0x0F0F0F0Fu;
+    std::vector<double> hA(K * N), hB(K * N);
+    srand(1);
+    for (auto& x : hA) x = rand() / (double)RAND_MAX;
+    for (auto& x : hB) x = rand() / (double)RAND_MAX;
+    double *A, *B, *out, *ref;
+    CHECK(hipMalloc(&A, K * N * 8));
+    CHECK(hipMalloc(&B, K * N * 8));
+    CHECK(hipMalloc(&out, total * 8));
+    CHECK(hipMemcpy(A, hA.data(), K * N * 8, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(B, hB.data(), K * N * 8, hipMemcpyHostToDevice));
+    int cus = 0;
+    CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    auto timeit = [&](const char* name, auto launch) {
+        std::vector<float> ms;
+        for (int r = 0; r < 6; ++r) {
+            CHECK(hipEventRecord(e0));
+            launch();
+            CHECK(hipEventRecord(e1));
+            CHECK(hipEventSynchronize(e1));
+            float t;
+            CHECK(hipEventElapsedTime(&t, e0, e1));
+            if (r) ms.push_back(t);
+        }
+        std::sort(ms.begin(), ms.end());
+        const float med = ms[ms.size() / 2];
+        printf("%-22s median %.3f ms  min %.3f ms  = %.2f TB/s\n", name, med, ms[0], total * 8.0 / med / 1e9);
+        fflush(stdout);
+    };
+    // sampled check of a variant against host math
+    auto check = [&](const char* name) {
+        std::vector<double> h(4096);
+        double err = 0;
+        for (int s = 0; s < 64; ++s) {
+            const int64_t o = ((int64_t)rand() * 2654435761ll) & (total - 4096);
+            CHECK(hipMemcpy(h.data(), out + o, 4096 * 8, hipMemcpyDeviceToHost));
+            for (int i = 0; i < 4096; ++i) {
+                const uint32_t x = (uint32_t)(o + i);
+                double r = 0;
+                for (int k = 0; k < K; ++k) r += hA[k * N + pext32(x, mA)] * hB[k * N + pext32(x, mB)];
+                err = std::max(err, std::abs(r - h[i]));
+            }
+        }
+        printf("  %s max |err| on samples %.3e\n", name, err);
+    };
+    const bool round2 = argc > 2;
+    for (int wpc : {4, 8, 16}) {
+        if (round2) break;
+        const int G = cus * wpc;
+        char nm[64];
+        snprintf(nm, sizeof nm, "fill wg/cu=%d", wpc);
+        timeit(nm, [&] { hipLaunchKernelGGL(k_fill, dim3(G), dim3(256), 0, 0, out, total); });
+        snprintf(nm, sizeof nm, "noload wg/cu=%d", wpc);
+        timeit(nm, [&] { hipLaunchKernelGGL(k_stream<false>, dim3(G), dim3(256), 0, 0, K, A, B, N, mA, mB, out, total); });
+        snprintf(nm, sizeof nm, "stream wg/cu=%d", wpc);
+        timeit(nm, [&] { hipLaunchKernelGGL(k_stream<true>, dim3(G), dim3(256), 0, 0, K, A, B, N, mA, mB, out, total); });
+        if (wpc == 8) check("stream");
+        snprintf(nm, sizeof nm, "blocked16 wg/cu=%d", wpc);
+        timeit(nm, [&] { hipLaunchKernelGGL(k_blocked<16>, dim3(G), dim3(256), 0, 0, K, A, B, N, mA, mB, out, total); });
+        if (wpc == 8) check("blocked16");
+        snprintf(nm, sizeof nm, "blocked14 wg/cu=%d", wpc);
+        timeit(nm, [&] { hipLaunchKernelGGL(k_blocked<14>, dim3(G), dim3(256), 0, 0, K, A, B, N, mA, mB, out, total); });
+    }
+    if (round2) {
+        const size_t lds16 = (size_t)K * (256 + 256) * 8, lds15 = (size_t)K * (128 + 256) * 8;
+        for (int wpc : {8, 16, 32}) {
+            const int G = cus * wpc;
+            char nm[64];
+            snprintf(nm, sizeof nm, "fill wg/cu=%d", wpc);
+            timeit(nm, [&] { hipLaunchKernelGGL(k_fill, dim3(G), dim3(256), 0, 0, out, total); });
+            snprintf(nm, sizeof nm, "dyn16 stride wg/cu=%d", wpc);
+            timeit(nm, [&] { hipLaunchKernelGGL((k_blocked_dyn<16, false>), dim3(G), dim3(256), lds16, 0, K, A, B, N, mA, mB, out, total); });
+            if (wpc == 16) check("dyn16");
+            snprintf(nm, sizeof nm, "dyn16 contig wg/cu=%d", wpc);
+            timeit(nm, [&] { hipLaunchKernelGGL((k_blocked_dyn<16, true>), dim3(G), dim3(256), lds16, 0, K, A, B, N, mA, mB, out, total); });
+            snprintf(nm, sizeof nm, "dyn15 stride wg/cu=%d", wpc);
+            timeit(nm, [&] { hipLaunchKernelGGL((k_blocked_dyn<15, false>), dim3(G), dim3(256), lds15, 0, K, A, B, N, mA, mB, out, total); });
+        }
+    }
+    (void)ref;
+    return 0;
+}
