@@ -276,6 +276,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    pipe.sync_stats()  # device data rank: accepted ranks / fallbacks of the timed steps
     gemm_ms = sum(s.elapsed_time(e) for s, e in pipe.events) / max(len(pipe.events), 1)
     sweep_ms = sum(s.elapsed_time(e) for s, e in pipe.sweep_events) / max(len(pipe.sweep_events), 1)
     traffic = pipe.sweep_traffic()
@@ -289,7 +290,9 @@ def main():
                 "unit": "TFLOP/s"}
     else:
         roof = {"bound": "hbm", "achieved": gbytes / (gemm_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
-    kernel = ("qk_knit_outer_stream_kernel (data-rank knit written in output order, output-write bound)"
+    kernel = ("qk_knit_outer_blocked_kernel (data-rank knit: 2^16-output tasks, operands staged in LDS, "
+              "output-write bound)" if pipe.last_kernel == "qk_knit_outer_blocked_kernel" else
+              "qk_knit_outer_stream_kernel (data-rank knit written in output order, output-write bound)"
               if pipe.last_kernel == "qk_knit_outer_stream_kernel" else
               "qk_gemm_smallk_kernel<true> (data-rank knit: keyed outer product, output-write bound)"
               if pipe.last_kernel == "qk_gemm_smallk_kernel<true>" else
@@ -326,7 +329,8 @@ def main():
                      + (", data-rank compressed per step" if pipe.data_rank else "")),
             "knit_terms": {"labels": counts["labels_ref"], "factored": counts["terms_factored"],
                            "light_cone": counts["labels"], "contracted": K,
-                           "data_rank": pipe.data_rank, "rank_fallbacks": pipe.rank_fallbacks},
+                           "data_rank": pipe.data_rank, "rank_fallbacks": pipe.rank_fallbacks,
+                           "device_rank": pipe.dev_rank},
             "gemm_mnk": [M, Nn, K],
             "output_entries": 1 << pipe.N,
             "parallelism": f"labels x{world} ({pipe.mode})",

@@ -50,6 +50,8 @@ SIGNATURES = {
     "qk_reduce_labels": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "qk_gemm_keyed": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                               c_vp, c_i64, c_vp, ctypes.c_int]),
+    "qk_gemm_keyed_pred": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
+                                   c_vp, c_i64, c_vp, ctypes.c_int, c_vp]),
     "qk_gemm_outer_paired": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                                      c_vp, c_vp]),
     "qk_knit_outer_stream": (c_i32, [c_vp, ctypes.c_int, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.c_uint64,

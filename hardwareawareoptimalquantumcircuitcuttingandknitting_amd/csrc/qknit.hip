@@ -537,7 +537,11 @@ struct GemmArgs {
     double* __restrict__ out;
     int beta;
     int64_t tiles_m, tiles_n;
+    const int32_t* skip = nullptr;  // DEVICE predicate: the launch does nothing when *skip > 0
 };
+
+// predicated launches (qk_gemm_keyed_pred): every workgroup reads the flag and leaves at once
+__device__ __forceinline__ bool gemm_skipped(const GemmArgs& g) { return g.skip && *g.skip > 0; }
 
 // Tile sequence index -> (bm, bn): QK_GEMM_GROUP tile rows x all tile columns, row fastest, so
 // the ~64 tiles an XCD holds at once span 8 A panels x 8 B panels that stay in its 4 MiB L2.
@@ -726,6 +730,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int64_t bm, int64_t
 __global__ __launch_bounds__(256, 2) void qk_gemm_keyed_kernel(GemmArgs g) {
     __shared__ __attribute__((aligned(16))) double As[2][GK][GT + GPAD];
     __shared__ __attribute__((aligned(16))) double Bs[2][GK][GT + GPAD];
+    if (gemm_skipped(g)) return;
     const int64_t nblk = g.tiles_m * g.tiles_n;
     int buf = 0;
     int64_t bm, bn;
@@ -817,6 +822,7 @@ __device__ __forceinline__ void gemm_ring_wait(int n) {
 
 __global__ __launch_bounds__(256, 2) void qk_gemm_glds_kernel(GemmArgs g) {
     __shared__ __attribute__((aligned(16))) GemmRing ring[G2S];
+    if (gemm_skipped(g)) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wm = wave & 1, wn = wave >> 1;
     const int64_t nblk = g.tiles_m * g.tiles_n;
@@ -938,6 +944,7 @@ constexpr int SK_U = QK_SK_U;  // 512-output chunks per lane iteration
 // two adjacent outputs are still one 16-B store; the key table (512 KiB at N = 2^16) is L2-resident.
 template <bool KEYED>
 __global__ __launch_bounds__(256) void qk_gemm_smallk_kernel(GemmArgs g) {
+    if (gemm_skipped(g)) return;
     const int K = (int)g.K;
     for (int64_t row = blockIdx.x; row < g.M; row += gridDim.x) {
         double a[SK_MAX];
@@ -1168,9 +1175,12 @@ __global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlocked
 constexpr int64_t OB_STAGE_BYTES = 24 * 1024;  // LDS budget of the blocked kernel's operand stage
 constexpr int OB_WG_PER_CU = 16;
 
-// Widest task (TB <= 16, >= 9: one 512-output iteration) whose operand stage fits OB_STAGE_BYTES; 0: none.
-int outer_blocked_tile(int nbits, int64_t K, uint64_t maskA, uint64_t maskB) {
-    for (int tb = nbits < 16 ? nbits : 16; tb >= 9; --tb) {
+// Widest task (TB <= 16 and <= align_bits, >= 9: one 512-output iteration) whose operand stage fits
+// OB_STAGE_BYTES; 0: none. align_bits = trailing zero bits of the output range's begin and count.
+int outer_blocked_tile(int nbits, int64_t K, uint64_t maskA, uint64_t maskB, int align_bits) {
+    int top = nbits < 16 ? nbits : 16;
+    top = align_bits < top ? align_bits : top;
+    for (int tb = top; tb >= 9; --tb) {
         const uint64_t low = (uint64_t(1) << tb) - 1;
         const int64_t bytes = 8 * K * ((int64_t(1) << __builtin_popcountll(maskA & low)) +
                                        (int64_t(1) << __builtin_popcountll(maskB & low)));
@@ -1343,6 +1353,12 @@ int qk_reduce_labels(qk_ctx* ctx, int64_t n_labels, const int64_t* offsets, int6
 int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A, int64_t lda,
                   const double* B, int64_t ldb, const int64_t* keyA, int64_t strideA,
                   const int64_t* keyB, int64_t strideB, double* out, int beta) {
+    return qk_gemm_keyed_pred(ctx, M, N, K, A, lda, B, ldb, keyA, strideA, keyB, strideB, out, beta, nullptr);
+}
+
+int qk_gemm_keyed_pred(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A, int64_t lda,
+                       const double* B, int64_t ldb, const int64_t* keyA, int64_t strideA,
+                       const int64_t* keyB, int64_t strideB, double* out, int beta, const int32_t* skip) {
     if (!ctx) return QK_EARG;
     if (M < 0 || N < 0 || K < 0) return fail(ctx, QK_EARG, "qk_gemm_keyed: negative size%s");
     if (M == 0 || N == 0) return QK_OK;
@@ -1352,7 +1368,7 @@ int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A,
     const int64_t nblk = tm * tn;
     QK_HIP(ctx, hipSetDevice(ctx->device));
     if (nblk >= (int64_t(1) << 31)) return fail(ctx, QK_EARG, "qk_gemm_keyed: too many tiles%s");
-    GemmArgs g{M, N, K, A, lda, B, ldb, keyA, strideA, keyB, strideB, out, beta, tm, tn};
+    GemmArgs g{M, N, K, A, lda, B, ldb, keyA, strideA, keyB, strideB, out, beta, tm, tn, skip};
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) == 0 &&
                            (lda % 2) == 0 && (ldb % 2) == 0;
     if (K >= 1 && K <= SK_MAX && !beta && !keyB && strideB == 1 && N % 2 == 0 && aligned16 &&
@@ -1439,9 +1455,9 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
     QK_HIP(ctx, hipSetDevice(ctx->device));
     int cus = 0;
     QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    const int tb = outer_blocked_tile(nbits, K, maskA, maskB);
-    const int64_t tmask = (int64_t(1) << tb) - 1;
-    if (tb && !(o_begin & tmask) && !(o_count & tmask)) {
+    const int align = __builtin_ctzll((uint64_t)(o_begin | o_count));
+    const int tb = outer_blocked_tile(nbits, K, maskA, maskB, align);
+    if (tb) {
         const uint64_t low = (uint64_t(1) << tb) - 1;
         const size_t stage = 8 * (size_t)K * ((size_t(1) << __builtin_popcountll(maskA & low)) +
                                               (size_t(1) << __builtin_popcountll(maskB & low)));

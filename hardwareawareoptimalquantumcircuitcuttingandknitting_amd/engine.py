@@ -353,10 +353,11 @@ def label_rows(fs: "FragmentState") -> "FragmentState":
 
 # ----------------------------------------------------------------------------- GEMM helpers
 def gemm_keyed(ctx: Context, A, B, keyA=None, keyB=None, out=None, strideA: int = 0,
-               strideB: int = 1, beta: int = 0):
+               strideB: int = 1, beta: int = 0, skip=None):
     """out[kA(i) + kB(j)] (=|+=) sum_k A[k, i] * B[k, j] on the GPU (fp64 MFMA).
 
-    ``kA(i) = keyA[i]`` if a key tensor is given, else ``i * strideA`` (same for B).
+    ``kA(i) = keyA[i]`` if a key tensor is given, else ``i * strideA`` (same for B). ``skip``
+    (device int32 tensor): the launch writes nothing when it holds a positive value.
     """
     K, M = A.shape
     K2, N = B.shape
@@ -365,9 +366,9 @@ def gemm_keyed(ctx: Context, A, B, keyA=None, keyB=None, out=None, strideA: int 
         assert keyA.shape[0] == M and keyA.dtype == torch().int64
     if keyB is not None:
         assert keyB.shape[0] == N and keyB.dtype == torch().int64
-    ctx.check(ctx.lib.qk_gemm_keyed(ctx.handle, M, N, K, A.data_ptr(), M, B.data_ptr(), N,
-                                    _ptr(keyA), strideA, _ptr(keyB), strideB, out.data_ptr(), beta),
-              "qk_gemm_keyed")
+    ctx.check(ctx.lib.qk_gemm_keyed_pred(ctx.handle, M, N, K, A.data_ptr(), M, B.data_ptr(), N,
+                                         _ptr(keyA), strideA, _ptr(keyB), strideB, out.data_ptr(), beta, _ptr(skip)),
+              "qk_gemm_keyed_pred")
     return out
 
 

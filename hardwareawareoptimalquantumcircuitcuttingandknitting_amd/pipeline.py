@@ -49,6 +49,18 @@ def _mm_nt(X, Y):
     return (Xb @ Yb.transpose(1, 2)).sum(0)
 
 
+def _pext(x: int, mask: int) -> int:
+    """Bits of ``x`` at the set positions of ``mask``, packed (BMI2 pext)."""
+    out, bit = 0, 0
+    while mask:
+        low = mask & -mask
+        if x & low:
+            out |= 1 << bit
+        bit += 1
+        mask ^= low
+    return out
+
+
 def _shard(n: int, rank: int, world: int) -> tuple[int, int]:
     per = -(-n // world)
     lo = min(n, rank * per)
@@ -208,8 +220,12 @@ class HipBackend:
     def gemm_outer_paired(self, A, B, keyB, **kw):
         return engine.gemm_outer_paired(self.ctx, A, B, keyB, **kw)
 
-    def knit_outer_stream(self, A, B, clbits_a, clbits_b, nbits, out):
-        return engine.knit_outer_stream(self.ctx, A, B, clbits_a, clbits_b, nbits, out)
+    def knit_outer_stream(self, A, B, clbits_a, clbits_b, nbits, out, o_begin=0, o_count=None, k_dev=None):
+        return engine.knit_outer_stream(self.ctx, A, B, clbits_a, clbits_b, nbits, out, o_begin=o_begin,
+                                        o_count=o_count, k_dev=k_dev)
+
+    def rank_factors(self, GA, GB):
+        return engine.rank_factors_device(self.ctx, GA, GB)
 
     def event(self):
         return self.T.cuda.Event(enable_timing=True)
@@ -241,32 +257,72 @@ class KnitPipeline:
         self.N = virt.circuit.num_clbits
         q_bytes = sum(len(fs.labels) << fs.prog.m for fs in self.frags) * 8
         out_bytes = (1 << self.N) * 8
+        self.order = engine.contract_order(self.ops.clbits)
         if mode is None:
-            mode = "single" if world == 1 else ("reduce" if (out_bytes <= q_bytes and not factored) else "gather")
+            if world == 1:
+                mode = "single"
+            elif out_bytes <= q_bytes and not factored:
+                mode = "reduce"
+            else:
+                mode = "slice" if self.slice_ok(world) else "gather"
         if mode == "reduce" and factored:
             raise ValueError("reduce mode needs the direct (label-sliced) knit")
-        if mode not in ("single", "reduce", "gather"):
+        if mode not in ("single", "reduce", "gather", "slice"):
             raise ValueError(f"unknown mode {mode}")
+        if mode == "slice" and not self.slice_ok(world):
+            raise ValueError("slice mode needs a factored two-fragment knit whose fragments partition the output "
+                             "bits, a power-of-two world and >= 2^9 outputs per rank")
         self.mode = mode
         # data_rank (single mode, factored, two fragments): each step compresses the two knit
         # operands to the numerical rank of R = A^T B (engine.data_rank_factors), contracts with
         # the output-write-bound small-K kernel, and verifies the result by random probes
         # (falls back to the exact contraction if a probe exceeds rank_tol)
         two = len(self.frags) == 2 and not any(fs.dropped for fs in self.frags)
-        ok = mode in ("single", "gather") and factored and two
-        # default: only where the write dominates (>= 2^24 outputs); below that the mid-step readback
-        # and host factorisation (~0.2 ms) cost more than the whole knit (bv 5 / hwe 16: < 0.02 ms)
+        ok = mode in ("single", "gather", "slice") and factored and two
+        # default: only where the write dominates (>= 2^24 outputs); below that the factorisation and
+        # its probe check cost more than the whole knit (bv 5 / hwe 16: < 0.02 ms)
         self.data_rank = (ok and virt.circuit.num_clbits >= 24) if data_rank is None else (data_rank and ok)
-        self.rank_tol = 1e-14  # Frobenius-norm estimate of R - A''^T B'' (probabilities: |R| <= 1)
-        self.rank_fallbacks = 0
+        # rank_tol: bound on every probe's ||(R - A''^T B'') x||_2 (x: N_PROBES fixed Gaussian vectors).
+        # With 16 probes, P(max_j ||D x_j|| <= tol while ||D||_F > 10 tol) <= P(chi2_1 <= 0.01)^16 < 3e-18
+        # (rank-one D is the worst case), and every entry of D is at most ||D||_F: the accepted
+        # compression moves no output by more than 1e-13 except with that probability.
+        self.rank_tol = 1e-14
+        self.rank_fallbacks = 0  # steps whose probe check rejected the compression
+        self.rank_incompressible = 0  # device path: steps with no factorisation of rank <= 8
         self.last_rank = None
+        cA, cB = self._stream_bits()
+        # device data rank (single / slice): qk_rank_factors + probe check + the predicated knits,
+        # no host round trip before the write (single mode: none at all)
+        self.dev_rank = bool(self.data_rank and cA is not None and self.ops.num_terms <= 64
+                             and hasattr(self.be, "rank_factors"))
+        self._pending = []  # device (rank, accepted) of steps not yet read back
         self.last_kernel = None  # kernel of the last compressed contraction (None: qk_gemm_keyed)
         self._probe = None
         self._pinned = None  # host staging of the two Gram matrices (pinned on a GPU)
+        self._pinned_k = None  # host staging of a slice step's accepted rank
         self.events = []  # (start, end) events around the main contraction GEMM
         self.sweep_events = []  # (start, end) events around each step's sweep (all fragments)
         self.record_events = False
         self._plan()
+
+    def _stream_bits(self):
+        """(clbits of the row side, of the column side) when two live fragments partition the output
+        bits with clbit 0 on the column side (the streaming knit applies), else (None, None)."""
+        live = [i for i, fs in enumerate(self.frags) if not fs.dropped]
+        if len(live) != 2 or len(self.order) != 2:
+            return None, None
+        cA, cB = self.ops.clbits[self.order[0]], self.ops.clbits[self.order[-1]]
+        return (cA, cB) if engine.stream_knit_ok(cA, cB, self.N) else (None, None)
+
+    def slice_ok(self, world: int) -> bool:
+        """Whether ``slice`` mode applies: each rank owns the contiguous output range
+        ``[rank, rank + 1) * 2^N / world`` of the reference-ordered distribution (factored
+        two-fragment knit written by the streaming kernel; world a power of two; >= 2^9 outputs and
+        whole column blocks of both fragments per rank)."""
+        cA, cB = self._stream_bits()
+        if cA is None or world < 2 or world & (world - 1) or not self.factored:
+            return False
+        return (1 << self.N) // world >= 512 and min(len(cA), len(cB)) >= world.bit_length() - 1
 
     # ------------------------------------------------------------------ plan
     def _plan(self):
@@ -282,7 +338,7 @@ class KnitPipeline:
             nl = fs.n_rows
             jobs = fs.jobs
             lo = 0
-            if self.mode == "gather":
+            if self.mode in ("gather", "slice"):
                 per = -(-nl // self.world)
                 dealt = _deal_rows(jobs.label_jobs(), self.world)
                 place = np.zeros(nl, dtype=np.int64)
@@ -305,8 +361,9 @@ class KnitPipeline:
             need = be.workspace_bytes(fs, n_jobs) if n_jobs else 0
             # gather mode: a rank's rows live in a zero-padded [per, width] buffer (the unit of
             # the collectives); padding rows stay zero
-            rows = -(-nl // self.world) if self.mode == "gather" else max(n_local, 1)
-            alloc = be.zeros if self.mode == "gather" else be.empty
+            sharded = self.mode in ("gather", "slice")
+            rows = -(-nl // self.world) if sharded else max(n_local, 1)
+            alloc = be.zeros if sharded else be.empty
             branching = n_jobs != n_local
             # branching + compiled program: the FINAL pass writes the label rows (no pjob, no reduce)
             fused = branching and n_jobs > 0 and getattr(be, "fuses_labels", lambda _: False)(fs)
@@ -324,7 +381,7 @@ class KnitPipeline:
                                     q=alloc((max(rows, 1), width), T.float64) if branching else None,
                                     ws=be.empty((max(need, 1),), T.uint8)))
         self._plan_knit()
-        if self.mode == "gather":
+        if self.mode in ("gather", "slice"):
             self._plan_exchange()
         self._plan_multi()
 
@@ -361,7 +418,7 @@ class KnitPipeline:
         for i in live:
             per = -(-self.frags[i].n_rows // P)
             width = 1 << self.frags[i].prog.m
-            if self.split_a and i == a_side:
+            if self.mode == "slice" or (self.split_a and i == a_side):
                 bw = width // P
                 self.xbuf[i] = ("a2a", be.empty((P, per, bw), T.float64), be.empty((P * per, bw), T.float64))
             else:
@@ -392,8 +449,11 @@ class KnitPipeline:
                     rows = rows - sw["lo"]
                 self.gather_idx.append(be.to_device(rows))
                 self.gather_coef.append(be.to_device(ops.coefs[i][t0:t1]))
-        self.order = engine.contract_order(ops.clbits)
         self.row_block = None
+        self.slice = None
+        if self.mode == "slice":
+            n_out = (1 << self.N) // self.world
+            self.slice = (self.rank * n_out, n_out)
         if self.mode == "gather":
             width_a = 1
             for i in self.order[:-1]:
@@ -417,7 +477,7 @@ class KnitPipeline:
                     qs[i] = be.zeros((fs.n_rows, 1), T.float64) + 1.0
                     continue
                 q = sw["q"] if sw["fused"] else sw["pjob"]
-                if self.mode == "gather":
+                if self.mode in ("gather", "slice"):
                     work, qs[i] = self._exchange(i, q)
                     pending.append(work)
                 else:
@@ -445,7 +505,7 @@ class KnitPipeline:
                     q = self._sweep_fragment(fs, sw)
             else:
                 q = self._sweep_fragment(fs, sw)
-            if self.mode == "gather":
+            if self.mode in ("gather", "slice"):
                 work, qs[i] = self._exchange(i, q)
                 pending.append(work)
             else:
@@ -521,10 +581,25 @@ class KnitPipeline:
             mats.append(a)
         return mats
 
+    N_PROBES = 16
+
+    def _probes(self, n: int, device):
+        """The fixed Gaussian probes, TRANSPOSED: [N_PROBES, n] (products with the wide operands go
+        through _mm_nt: a plain [K, 2^16] @ [2^16, 16] GEMM runs on a handful of workgroups)."""
+        if self._probe is None or self._probe.shape[1] != n:
+            T = self.T
+            g = T.Generator().manual_seed(1234)
+            self._probe = T.randn((self.N_PROBES, n), generator=g, dtype=T.float64).to(device)
+        return self._probe
+
     def knit(self, qs: list):
         mats = self.operands(qs)
         if self.out is None:
             self.out = self._alloc_out(mats)
+        if self.mode == "slice":
+            return self._knit_slice(mats)
+        if self.dev_rank and self.mode == "single":
+            return self._knit_dev_rank(mats)
         low = self._rank_compress(mats) if self.data_rank else None
         if self.record_events:
             start, end = self.be.event(), self.be.event()
@@ -550,6 +625,156 @@ class KnitPipeline:
             dist.reduce(res, dst=0, group=self.group)
         return res
 
+    def _accept(self, A, B, A2, B2, x, r, ref_rows=None, cmp_rows=None, reduce_err=None):
+        """Device-side probe check of a compressed knit: ``(k_eff, err)``, ``k_eff`` = the rank when
+        every probe's ``||(A^T B - A2^T B2) x||_2 <= rank_tol`` (see ``__init__``), else 0."""
+        T = self.T
+        if ref_rows is None:  # x: probes transposed, [N_PROBES, N]
+            ref_rows = A.T @ _mm_nt(B, x)
+            cmp_rows = A2.T @ _mm_nt(B2, x)
+        e2 = ((ref_rows - cmp_rows) ** 2).sum(dim=0)
+        if reduce_err is not None:
+            e2 = reduce_err(e2)
+        err = e2.max().sqrt()
+        k_eff = T.where((err <= self.rank_tol) & (r > 0), r, T.zeros_like(r))
+        self._pending.append((r, k_eff))
+        return k_eff, err
+
+    def _knit_dev_rank(self, mats):
+        """Single GPU, device data rank: Grams -> qk_rank_factors -> compressed operands -> probe
+        check -> streaming knit with the accepted rank (k_eff) and the exact contraction predicated
+        on k_eff == 0. Nothing waits for the host; ``sync_stats`` reads ranks / fallbacks later."""
+        ia, ib = self.order[0], self.order[-1]
+        A, B = mats[ia], mats[ib]
+        G = self.T.stack([_mm_nt(A, A), _mm_nt(B, B)])
+        TA, TB, r = self.be.rank_factors(G[0].contiguous(), G[1].contiguous())
+        A2, B2 = (TA @ A).contiguous(), (TB @ B).contiguous()
+        k_eff, _ = self._accept(A, B, A2, B2, self._probes(B.shape[1], B.device), r)
+        cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
+        if self.record_events:
+            start, end = self.be.event(), self.be.event()
+            start.record()
+        self.last_kernel = "qk_knit_outer_blocked_kernel"
+        self.be.knit_outer_stream(A2, B2, cA, cB, self.N, self.out, k_dev=k_eff)
+        if self.record_events:
+            end.record()
+            self.events.append((start, end))
+        return self._contract(mats, skip=k_eff)  # exact path: runs only if the check rejected
+
+    def _knit_slice(self, mats):
+        """Slice mode (multi-GPU): this rank writes the contiguous outputs ``self.slice`` of the
+        reference-ordered distribution. ``mats`` are this rank's column blocks of the two operands
+        (the sweep's all_to_all delivered every instance row of one column block per fragment).
+        Collectives: one all_reduce (the two Grams + B x for the probes), one broadcast of the
+        factors (rank 0's, so every rank knits with the same ones), one all_gather of the compressed
+        column blocks (8 x 2^m per fragment), one all_reduce of the probe errors; the write itself
+        is local. A rejected compression (read back after the knit is queued) falls back to the
+        exact contraction of the slice from all-gathered operands."""
+        import torch.distributed as dist
+
+        T, be, P = self.T, self.be, self.world
+        ia, ib = self.order[0], self.order[-1]
+        XA, XB = mats[ia], mats[ib]  # [K, wA / P], [K, wB / P]
+        K = XA.shape[0]
+        cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
+        o_begin, o_count = self.slice
+        if not self.dev_rank:
+            return self._slice_exact(XA, XB, cA, cB)
+        bwA, bwB = XA.shape[1], XB.shape[1]
+        x_full = self._probes(bwB * P, XB.device)  # [N_PROBES, wB]
+        x = x_full[:, self.rank * bwB:(self.rank + 1) * bwB].contiguous()
+        npr = self.N_PROBES
+        red = T.cat([_mm_nt(XA, XA).reshape(-1), _mm_nt(XB, XB).reshape(-1), _mm_nt(XB, x).reshape(-1)])
+        dist.all_reduce(red, group=self.group)
+        GA = red[:K * K].view(K, K).contiguous()
+        GB = red[K * K:2 * K * K].view(K, K).contiguous()
+        Bx = red[2 * K * K:].view(K, npr)
+        TA, TB, r = be.rank_factors(GA, GB)
+        R8 = TA.shape[0]
+        fac = T.cat([TA.reshape(-1), TB.reshape(-1), r.to(T.float64)])
+        dist.broadcast(fac, src=self._group_rank0(), group=self.group)
+        TA = fac[:R8 * K].view(R8, K)
+        TB = fac[R8 * K:2 * R8 * K].view(R8, K)
+        r = fac[-1:].to(T.int32)
+        loc = T.cat([(TA @ XA).reshape(-1), (TB @ XB).reshape(-1)])
+        gat = T.empty(P * loc.numel(), dtype=loc.dtype, device=loc.device)
+        dist.all_gather_into_tensor(gat, loc, group=self.group)
+        gat = gat.view(P, loc.numel())
+        A2 = gat[:, :R8 * bwA].view(P, R8, bwA).permute(1, 0, 2).reshape(R8, P * bwA).contiguous()
+        B2 = gat[:, R8 * bwA:].view(P, R8, bwB).permute(1, 0, 2).reshape(R8, P * bwB).contiguous()
+        # rows of R in this rank's A column block, against all probes
+        ref_rows = XA.T @ Bx
+        cmp_rows = A2[:, self.rank * bwA:(self.rank + 1) * bwA].T @ _mm_nt(B2, x_full)
+
+        def reduce_err(e2):
+            dist.all_reduce(e2, group=self.group)
+            return e2
+
+        k_eff, _ = self._accept(None, None, None, None, None, r, ref_rows, cmp_rows, reduce_err)
+        on_gpu = k_eff.device.type == "cuda"
+        if self._pinned_k is None:
+            self._pinned_k = T.empty(1, dtype=T.int32, pin_memory=on_gpu)
+        self._pinned_k.copy_(k_eff, non_blocking=on_gpu)
+        ready = T.cuda.Event() if on_gpu else None
+        if on_gpu:
+            ready.record()
+        if self.record_events:
+            start, end = be.event(), be.event()
+            start.record()
+        self.last_kernel = "qk_knit_outer_blocked_kernel"
+        be.knit_outer_stream(A2, B2, cA, cB, self.N, self.out, o_begin=o_begin, o_count=o_count, k_dev=k_eff)
+        if self.record_events:
+            end.record()
+            self.events.append((start, end))
+        if on_gpu:
+            ready.synchronize()  # the check only, not the knit queued behind it
+        if int(self._pinned_k[0]) == 0:
+            self._slice_exact(XA, XB, cA, cB)
+        return self.out
+
+    def _group_rank0(self) -> int:
+        import torch.distributed as dist
+
+        return 0 if self.group is None else dist.get_global_rank(self.group, 0)
+
+    def _slice_exact(self, XA, XB, cA, cB):
+        """Exact contraction of this rank's output slice (K terms) from all-gathered operand blocks."""
+        import torch.distributed as dist
+
+        from .knit_plan import deposit_keys
+
+        T, be, P = self.T, self.be, self.world
+        o_begin, o_count = self.slice
+        full = []
+        for X in (XA, XB):
+            g = T.empty((P * X.shape[0], X.shape[1]), dtype=X.dtype, device=X.device)
+            dist.all_gather_into_tensor(g, X.contiguous(), group=self.group)
+            full.append(g.view(P, X.shape[0], X.shape[1]).permute(1, 0, 2).reshape(X.shape[0], -1))
+        mA, mB = sum(1 << c for c in cA), sum(1 << c for c in cB)
+        low = o_count - 1
+        cols = []
+        for X, m, cl in ((full[0], mA, cA), (full[1], mB, cB)):
+            n_lo = bin(m & low).count("1")
+            base = _pext(o_begin, m)
+            keys = deposit_keys(list(cl))[base:base + (1 << n_lo)] - (o_begin & m)
+            cols.append((X[:, base:base + (1 << n_lo)].contiguous(), be.to_device(np.ascontiguousarray(keys))))
+        (A, kA), (B, kB) = cols
+        self.last_kernel = None
+        return be.gemm_keyed(A, B, keyA=kA, keyB=kB, out=self.out)
+
+    def sync_stats(self):
+        """Read back the ranks / acceptances of the steps since the last call (host sync):
+        ``last_rank`` (accepted rank, or None when the last step fell back) and ``rank_fallbacks``."""
+        for r, k in self._pending:
+            rv, kv = int(r.reshape(-1)[0]), int(k.reshape(-1)[0])
+            self.last_rank = kv if kv > 0 else None
+            if rv == 0:  # no factorisation of rank <= 8: exact contraction, not a rejected check
+                self.rank_incompressible += 1
+            elif kv == 0:
+                self.rank_fallbacks += 1
+        self._pending = []
+        return self.last_rank, self.rank_fallbacks
+
     def _rank_compress(self, mats):
         """Two-fragment knit R = A^T B ([K, M], [K, N] operands) rewritten as A''^T B'' with
         r = numerical rank of R rows (engine.data_rank_factors on the two K x K Gram matrices,
@@ -564,9 +789,7 @@ class KnitPipeline:
             lo, hi = self.row_block
             A = A[:, lo:hi].contiguous()
         K = A.shape[0]
-        if self._probe is None or self._probe.shape[0] != B.shape[1]:
-            g = T.Generator().manual_seed(1234)
-            self._probe = T.randn((B.shape[1], 8), generator=g, dtype=T.float64).to(B.device)
+        xt = self._probes(B.shape[1], B.device)
         # Grams first, their readback started at once; the probe reference runs on the GPU while
         # the host factorises (no pageable copies: they would wait for the whole queue)
         G = T.stack([_mm_nt(A, A), _mm_nt(B, B)])
@@ -577,7 +800,7 @@ class KnitPipeline:
         ready = T.cuda.Event() if on_gpu else None
         if on_gpu:
             ready.record()
-        ref = A.T @ _mm_nt(B, self._probe.T)
+        ref = A.T @ _mm_nt(B, xt)
         if on_gpu:
             ready.synchronize()
         Gh = self._pinned.numpy()
@@ -592,7 +815,7 @@ class KnitPipeline:
         tt = tt.to(A.device, non_blocking=on_gpu)
         TA, TB = tt[:r], tt[r:]
         A2, B2 = (TA @ A).contiguous(), (TB @ B).contiguous()
-        err = (A2.T @ _mm_nt(B2, self._probe.T) - ref).norm(dim=0).max()
+        err = (A2.T @ _mm_nt(B2, xt) - ref).norm(dim=0).max()
         self.last_rank = A2.shape[0]
         out = list(mats)
         out[ia], out[ib] = A2, B2
@@ -638,16 +861,18 @@ class KnitPipeline:
 
     def _alloc_out(self, mats):
         T = self.T
+        if self.mode == "slice":
+            return self.be.zeros((self.slice[1],), T.float64)
         if self.mode != "gather":
             return self.be.zeros((1 << self.N,), T.float64)
         lo, hi = self.row_block
         width_b = mats[self.order[-1]].shape[1]
         return self.be.zeros((max(hi - lo, 1) * width_b,), T.float64)
 
-    def _contract(self, mats):
+    def _contract(self, mats, skip=None):
         if self.mode != "gather":
-            return engine.contract(None, mats, self.ops.clbits, self.out, gemm=self.be.gemm_keyed,
-                                   kr=self.be.khatri_rao)
+            gemm = self.be.gemm_keyed if skip is None else (lambda A, B, **kw: self.be.gemm_keyed(A, B, skip=skip, **kw))
+            return engine.contract(None, mats, self.ops.clbits, self.out, gemm=gemm, kr=self.be.khatri_rao)
         # output-sharded: compact [rows, 2^m_B] block in (x_A, x_B) order
         order = self.order
         A = mats[order[0]]

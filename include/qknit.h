@@ -153,6 +153,13 @@ int qk_gemm_keyed(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A,
                   const double* B, int64_t ldb, const int64_t* keyA, int64_t strideA,
                   const int64_t* keyB, int64_t strideB, double* out, int beta);
 
+/* qk_gemm_keyed predicated on a DEVICE flag: nothing is written when *skip > 0 (skip may be NULL).
+ * The exact contraction of a step whose data-rank compression may be rejected on the device
+ * (KnitPipeline: skip = the accepted rank, 0 when rejected), so no host synchronisation decides. */
+int qk_gemm_keyed_pred(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const double* A, int64_t lda,
+                       const double* B, int64_t ldb, const int64_t* keyA, int64_t strideA,
+                       const int64_t* keyB, int64_t strideB, double* out, int beta, const int32_t* skip);
+
 /* Small-K keyed outer product, output-write bound (1 <= K <= 8): the same result as
  * qk_gemm_keyed with beta = 0, for a key table whose column pairs are adjacent outputs:
  * keyB[2i + 1] == keyB[2i] + 1 and keyB[2i] even (the N side holds clbit 0; the caller checks,
@@ -176,8 +183,9 @@ int qk_knit_outer_stream(qk_ctx* ctx, int nbits, int64_t K, const double* A, int
  * out[o - o_begin] (a rank's contiguous slice of the distribution: multi-GPU slice mode). k_dev
  * (DEVICE int32, or NULL) overrides K at run time (min(K, *k_dev)); *k_dev <= 0 makes the call write
  * nothing (a knit predicated on a device-side check, no host sync). Ranges and k_dev need the blocked
- * kernel: o_begin and o_count multiples of its task size 2^TB (TB <= 16, chosen so the K x (2^a + 2^b)
- * staged operand values fit 24 KiB of LDS; 2^16 for syc 32 5 at K <= 8). */
+ * kernel: tasks of 2^TB outputs with 9 <= TB <= 16, TB at most the trailing zero bits of o_begin and
+ * o_count, and the K x (2^a + 2^b) staged operand values within 24 KiB of LDS (2^16 for syc 32 5 at
+ * K <= 8); QK_EARG when no such TB exists. */
 int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* A, int64_t lda, const double* B,
                                int64_t ldb, uint64_t maskA, uint64_t maskB, int64_t o_begin, int64_t o_count,
                                const int32_t* k_dev, double* out);

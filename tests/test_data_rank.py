@@ -63,12 +63,22 @@ def test_pipeline_data_rank_matches_oracle(case, force_fallback):
     if force_fallback:
         pipe.rank_tol = -1.0  # every probe check fails
     ref = dense.run_dense(cut)
-    for _ in range(2):  # second step: after a fallback the exact path stays on
+    for _ in range(2):  # host path: after a fallback the exact path stays on; device path: per step
         res = pipe.step().numpy().copy()
         np.testing.assert_allclose(res, ref, atol=1e-12, rtol=0)
+    pipe.sync_stats()
     K_terms = pipe.ops.num_terms
     compresses = case != "hwe_p2"  # hwe 16 1: one cut, the factored terms are already minimal
-    if force_fallback:
+    if pipe.dev_rank:  # device factors + probe check decide every step (no permanent switch)
+        if force_fallback:
+            assert pipe.rank_fallbacks + pipe.rank_incompressible == 2 and pipe.last_rank is None
+            assert pipe.data_rank
+        elif case == "syc_16":  # rank of R above 8: the exact contraction, every step
+            assert pipe.rank_incompressible == 2 and pipe.rank_fallbacks == 0 and pipe.last_rank is None
+        else:
+            assert pipe.rank_fallbacks == 0 and pipe.last_rank is not None
+            assert (pipe.last_rank < K_terms) == compresses, (pipe.last_rank, K_terms)
+    elif force_fallback:
         assert pipe.rank_fallbacks == (1 if compresses else 0)
         assert pipe.data_rank == (not compresses)
     else:

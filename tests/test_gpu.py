@@ -581,8 +581,10 @@ def test_syc_32_5_data_rank_step_matches_exact_step(T):
     pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
     assert pipe.data_rank
     got = pipe.step()
-    T.cuda.synchronize()
-    assert pipe.rank_fallbacks == 0 and pipe.last_rank is not None and pipe.last_rank <= 8
+    pipe.sync_stats()
+    assert pipe.dev_rank and pipe.last_kernel == "qk_knit_outer_blocked_kernel"
+    assert pipe.rank_fallbacks == 0 and pipe.rank_incompressible == 0
+    assert pipe.last_rank is not None and pipe.last_rank <= 8
     exact = KnitPipeline(VirtualCircuit(cut), factored=True, data_rank=False)
     ref = exact.step()
     T.cuda.synchronize()
