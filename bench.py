@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--no-north-star", action="store_true",
                     help="skip the syc 32 1 sweep-only measurement (north_star_sweep)")
     ap.add_argument("--cpu-sample-labels", type=int, default=12)
+    ap.add_argument("--no-npd", action="store_true", help="skip the NPD timing on the 2^N output")
+    ap.add_argument("--no-general", action="store_true",
+                    help="skip knit_general (the same step without data-rank compression)")
     return ap.parse_args()
 
 
@@ -149,6 +152,133 @@ def cpu_baseline_qvm(cut, processes: int = 8, accuracy: float = 1e-5, return_res
     if return_result:
         out["result"] = dict(npd)
     return out
+
+
+def cpu_baseline_same(pipe, cut, qs_host, n_inst_sample: int = 8, out_block_bits: int = 24) -> dict:
+    """The builder's algorithm on the host cores (numpy + BLAS threads), timed on a bounded sample of
+    the syc 32 5 step and extrapolated (factors stated): exact instances (oracle statevector, a
+    sample of ``n_inst_sample`` reference instances, scaled to the swept instance count), then on the
+    real swept rows (copied from the GPU run): operand transforms, Grams, data-rank factors
+    (data_rank.rank_factors, the host form of qk_rank_factors), compressed operands, the 16-probe
+    check, and the streaming knit of one contiguous block of 2^out_block_bits outputs (pext index
+    gathers), scaled to 2^N."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import dense, qvm
+    from oracle.statevector import simulate
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import data_rank
+
+    try:
+        from threadpoolctl import threadpool_info
+
+        threads = max([t.get("num_threads", 1) for t in threadpool_info()] + [1])
+    except Exception:
+        threads = os.cpu_count() or 1
+    view = qvm.CutView(cut)
+    frags = [list(r) for r in view.qregs if len(r)]
+    t0 = time.perf_counter()
+    done = 0
+    for f in frags:
+        cl = dense.fragment_clbits(view, f)
+        for label in view.labels(f)[: max(1, n_inst_sample // len(frags))]:
+            dense.fold(simulate(view.instance_ops(f, label), len(f)), view.num_clbits, cl)
+            done += 1
+    t_inst = (time.perf_counter() - t0) / done
+    swept = pipe.instance_counts()["instances_swept"]
+    t_sweep = t_inst * swept
+    ia, ib = pipe.order[0], pipe.order[-1]
+    t1 = time.perf_counter()
+    A = pipe.ops.transforms[ia] @ qs_host[ia]
+    B = pipe.ops.transforms[ib] @ qs_host[ib]
+    f = data_rank.rank_factors(A @ A.T, B @ B.T)
+    TA, TB = f
+    A2, B2 = TA @ A, TB @ B
+    x = np.random.default_rng(1234).standard_normal((B.shape[1], 16))
+    err = np.linalg.norm(A.T @ (B @ x) - A2.T @ (B2 @ x), axis=0).max()
+    t_prep = time.perf_counter() - t1
+    import torch
+
+    cA, cB = pipe.ops.clbits[ia], pipe.ops.clbits[ib]
+    nblk = 1 << out_block_bits
+    torch.set_num_threads(threads)  # the write runs on torch's CPU kernels: every BLAS thread
+    At, Bt = torch.from_numpy(A2), torch.from_numpy(B2)
+    t2 = time.perf_counter()
+    o = torch.arange(nblk, dtype=torch.int64)
+    ia_idx = torch.zeros(nblk, dtype=torch.int64)
+    ib_idx = torch.zeros(nblk, dtype=torch.int64)
+    for j, c in enumerate(cA):
+        ia_idx |= ((o >> c) & 1) << j
+    for j, c in enumerate(cB):
+        ib_idx |= ((o >> c) & 1) << j
+    out = (At.index_select(1, ia_idx) * Bt.index_select(1, ib_idx)).sum(0)
+    t_blk = time.perf_counter() - t2
+    scale = (1 << pipe.N) // nblk
+    total = t_sweep + t_prep + t_blk * scale
+    del out
+    return {
+        "value": pipe.instance_counts()["instances_ref"] / total,
+        "unit": "instances/s",
+        "cores": int(threads),
+        "kind": "port",
+        "algorithm": "same as the GPU step (basis-reduced exact instances, factored light-cone knit, "
+                     "data-rank compression, output-order write)",
+        **host_info(),
+        "sample": (f"{done} exact instances at {t_inst * 1e3:.1f} ms each (x{swept / done:.0f} to the "
+                   f"{swept} swept); transforms + Grams + factors + probes on the real swept rows "
+                   f"{t_prep * 1e3:.0f} ms (rank {A2.shape[0]}, probe err {err:.1e}); knit of 2^{out_block_bits} "
+                   f"outputs {t_blk * 1e3:.0f} ms (x{scale} to 2^{pipe.N}): {total:.1f} s per full knit"),
+        "full_knit_s": total,
+    }
+
+
+def knit_general(pipe_kw: dict, steps: int) -> dict:
+    """The same workload without the per-step data-rank compression: the K = 64 light-cone
+    contraction on the MFMA kernel (qk_gemm_glds_kernel), its own timing and roofline."""
+    import torch
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    pipe = KnitPipeline(data_rank=False, **pipe_kw)
+    for _ in range(2):
+        pipe.step()
+    torch.cuda.synchronize()
+    pipe.record_events = True
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        pipe.step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    gemm_ms = sum(s.elapsed_time(e) for s, e in pipe.events) / max(len(pipe.events), 1)
+    M, N, K = pipe.gemm_shape()
+    flops = 2.0 * M * N * K
+    out = {"ms_per_step": ms, "kernel": "qk_gemm_glds_kernel (K = %d light-cone terms, fp64 MFMA)" % K,
+           "gemm_mnk": [M, N, K], "avg_launch_ms": gemm_ms, "achieved_TFs": flops / (gemm_ms * 1e-3) / 1e12,
+           "peak_TFs": FP64_MFMA_PEAK_TFLOPS, "frac": flops / (gemm_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+           "traffic": traffic_per_launch(M, N, K)}
+    del pipe
+    torch.cuda.empty_cache()
+    return out
+
+
+def npd_timing(dense, accuracy: float) -> dict:
+    """``QuasiDistr`` truncation + ``nearest_probability_distribution`` (quasi_distr.py:7-10,28-43,
+    run.py:71) on the GPU over the step's 2^N output: qk_threshold_count then qk_npd, timed apart
+    from the knit."""
+    import torch
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import engine
+
+    ctx = engine.get_context(dense.device.index or 0)
+    engine.nearest_probability_distribution(ctx, dense, accuracy)  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    keys, vals = engine.nearest_probability_distribution(ctx, dense, accuracy)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    return {"ms": ms, "accuracy": accuracy, "kept_entries": int(len(keys)), "entries": int(dense.numel()),
+            "sum_kept": float(vals.sum()) if len(vals) else 0.0}
 
 
 def north_star_sweep(steps: int) -> dict:
@@ -361,10 +491,28 @@ def main():
             "fp64_valu_frac": traffic["flops"] / (sweep_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
         },
     }
+    prep = [s.elapsed_time(e) for s, e in pipe.prep_events]
+    if prep:
+        line["rank_compress_ms"] = sum(prep) / len(prep)  # sweep end -> knit start (transforms, factors, probes)
+    if world == 1 and not args.no_npd:
+        from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import quasi_distr
+
+        line["npd"] = npd_timing(pipe.out, quasi_distr.ACCURACY)
+    qs_host = None
+    if world == 1 and not args.no_cpu_baseline and pipe.dev_rank:
+        qs_host = [q.contiguous().cpu().numpy() for q in pipe.sweep()]
+    if world == 1 and not args.no_general and pipe.data_rank:
+        line["knit_general"] = knit_general(dict(virt=virt, device=local, factored=not args.direct,
+                                                 light_cone=not args.no_light_cone), max(2, args.steps // 4))
     if world == 1 and not args.no_north_star:
         line["north_star_sweep"] = north_star_sweep(args.steps)
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(cut, args.cpu_sample_labels)
+        if qs_host is not None:
+            line["cpu_baseline"] = cpu_baseline_same(pipe, cut, qs_host)
+            line["cpu_baseline"]["naive"] = cpu_baseline(cut, args.cpu_sample_labels)
+        else:
+            line["cpu_baseline"] = cpu_baseline(cut, args.cpu_sample_labels)
+        line["cpu_baseline"]["qvm_literal"] = cpu_baseline_qvm(cut)
     print(json.dumps(line), flush=True)
 
 

@@ -302,6 +302,7 @@ class KnitPipeline:
         self._pinned_k = None  # host staging of a slice step's accepted rank
         self.events = []  # (start, end) events around the main contraction GEMM
         self.sweep_events = []  # (start, end) events around each step's sweep (all fragments)
+        self.prep_events = []  # (sweep end, knit start): operand transforms + data-rank compression
         self.record_events = False
         self._plan()
 
@@ -894,7 +895,11 @@ class KnitPipeline:
         qs = self.sweep()
         end.record()
         self.sweep_events.append((start, end))
-        return self.knit(qs)
+        n = len(self.events)
+        out = self.knit(qs)
+        if len(self.events) > n:  # operand transforms + data-rank step: sweep end -> knit start
+            self.prep_events.append((end, self.events[n][0]))
+        return out
 
     # ------------------------------------------------------------------ accounting
     def instance_counts(self) -> dict:
@@ -952,4 +957,6 @@ class KnitPipeline:
             M *= widths[i]
         if self.row_block is not None:
             M = self.row_block[1] - self.row_block[0]
+        if self.slice is not None:  # this rank's outputs: 1/world of the rows
+            M //= self.world
         return M, widths[self.order[-1]], K
