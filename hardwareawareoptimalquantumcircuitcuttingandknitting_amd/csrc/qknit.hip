@@ -9,6 +9,8 @@
 // Design notes: DESIGN.md §3 (sweep) and §4 (knit).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -1462,7 +1464,10 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
         const size_t stage = 8 * (size_t)K * ((size_t(1) << __builtin_popcountll(maskA & low)) +
                                               (size_t(1) << __builtin_popcountll(maskB & low)));
         const int64_t tasks = o_count >> tb;
-        const int64_t G0 = (int64_t)cus * OB_WG_PER_CU;
+        // workgroups per CU of the grid-stride launch; QKNIT_OB_WG_PER_CU=0: one workgroup per task
+        // (workgroups retire as they finish, so work on other streams can take their slots)
+        static const int wgpc = getenv("QKNIT_OB_WG_PER_CU") ? atoi(getenv("QKNIT_OB_WG_PER_CU")) : OB_WG_PER_CU;
+        const int64_t G0 = wgpc > 0 ? (int64_t)cus * wgpc : tasks;
         OuterBlockedArgs b{(int)K, tb, A, lda, B, ldb, (uint32_t)maskA, (uint32_t)maskB, o_begin >> tb,
                            (o_begin >> tb) + tasks, o_begin, k_dev, out};
         hipLaunchKernelGGL(qk_knit_outer_blocked_kernel, dim3((unsigned)(tasks < G0 ? tasks : G0)), dim3(256), stage,

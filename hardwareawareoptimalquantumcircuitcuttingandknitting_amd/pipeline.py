@@ -299,7 +299,12 @@ class KnitPipeline:
         self.last_kernel = None  # kernel of the last compressed contraction (None: qk_gemm_keyed)
         self._probe = None
         self._pinned = None  # host staging of the two Gram matrices (pinned on a GPU)
-        self._pinned_k = None  # host staging of a slice step's accepted rank
+        self._prep_stream = None
+        # software-pipelined steps (_step_overlapped), off by default: measured on syc 32 5 (one box,
+        # same build) 5.82 ms per step without, 7.20 with (the persistent write grid holds every CU,
+        # so the side stream's sweep waits for it), 6.55 with a one-workgroup-per-task write grid,
+        # 6.06 with 4 write workgroups per CU. QKNIT_OVERLAP=1 turns it on.
+        self.overlap = os.environ.get("QKNIT_OVERLAP", "0") == "1"
         self.events = []  # (start, end) events around the main contraction GEMM
         self.sweep_events = []  # (start, end) events around each step's sweep (all fragments)
         self.prep_events = []  # (sweep end, knit start): operand transforms + data-rank compression
@@ -645,22 +650,29 @@ class KnitPipeline:
         """Single GPU, device data rank: Grams -> qk_rank_factors -> compressed operands -> probe
         check -> streaming knit with the accepted rank (k_eff) and the exact contraction predicated
         on k_eff == 0. Nothing waits for the host; ``sync_stats`` reads ranks / fallbacks later."""
+        return self._launch_dev_rank(self._prep_dev_rank(mats))
+
+    def _prep_dev_rank(self, mats) -> dict:
         ia, ib = self.order[0], self.order[-1]
         A, B = mats[ia], mats[ib]
         G = self.T.stack([_mm_nt(A, A), _mm_nt(B, B)])
         TA, TB, r = self.be.rank_factors(G[0].contiguous(), G[1].contiguous())
         A2, B2 = (TA @ A).contiguous(), (TB @ B).contiguous()
         k_eff, _ = self._accept(A, B, A2, B2, self._probes(B.shape[1], B.device), r)
+        return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
+
+    def _launch_dev_rank(self, p: dict):
+        ia, ib = self.order[0], self.order[-1]
         cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
         if self.record_events:
             start, end = self.be.event(), self.be.event()
             start.record()
         self.last_kernel = "qk_knit_outer_blocked_kernel"
-        self.be.knit_outer_stream(A2, B2, cA, cB, self.N, self.out, k_dev=k_eff)
+        self.be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, self.out, k_dev=p["k_eff"])
         if self.record_events:
             end.record()
             self.events.append((start, end))
-        return self._contract(mats, skip=k_eff)  # exact path: runs only if the check rejected
+        return self._contract(p["mats"], skip=p["k_eff"])  # exact path: runs only if the check rejected
 
     def _knit_slice(self, mats):
         """Slice mode (multi-GPU): this rank writes the contiguous outputs ``self.slice`` of the
@@ -671,16 +683,18 @@ class KnitPipeline:
         column blocks (8 x 2^m per fragment), one all_reduce of the probe errors; the write itself
         is local. A rejected compression (read back after the knit is queued) falls back to the
         exact contraction of the slice from all-gathered operands."""
+        ia, ib = self.order[0], self.order[-1]
+        if not self.dev_rank:
+            return self._slice_exact(mats[ia], mats[ib], self.ops.clbits[ia], self.ops.clbits[ib])
+        return self._launch_slice(self._prep_slice(mats))
+
+    def _prep_slice(self, mats) -> dict:
         import torch.distributed as dist
 
         T, be, P = self.T, self.be, self.world
         ia, ib = self.order[0], self.order[-1]
         XA, XB = mats[ia], mats[ib]  # [K, wA / P], [K, wB / P]
         K = XA.shape[0]
-        cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
-        o_begin, o_count = self.slice
-        if not self.dev_rank:
-            return self._slice_exact(XA, XB, cA, cB)
         bwA, bwB = XA.shape[1], XB.shape[1]
         x_full = self._probes(bwB * P, XB.device)  # [N_PROBES, wB]
         x = x_full[:, self.rank * bwB:(self.rank + 1) * bwB].contiguous()
@@ -713,25 +727,78 @@ class KnitPipeline:
 
         k_eff, _ = self._accept(None, None, None, None, None, r, ref_rows, cmp_rows, reduce_err)
         on_gpu = k_eff.device.type == "cuda"
-        if self._pinned_k is None:
-            self._pinned_k = T.empty(1, dtype=T.int32, pin_memory=on_gpu)
-        self._pinned_k.copy_(k_eff, non_blocking=on_gpu)
+        pinned = T.empty(1, dtype=T.int32, pin_memory=on_gpu)
+        pinned.copy_(k_eff, non_blocking=on_gpu)
         ready = T.cuda.Event() if on_gpu else None
         if on_gpu:
             ready.record()
+        return {"A2": A2, "B2": B2, "k_eff": k_eff, "XA": XA, "XB": XB, "pinned": pinned, "ready": ready,
+                "mats": mats}
+
+    def _launch_slice(self, p: dict):
+        be = self.be
+        ia, ib = self.order[0], self.order[-1]
+        cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
+        o_begin, o_count = self.slice
         if self.record_events:
             start, end = be.event(), be.event()
             start.record()
         self.last_kernel = "qk_knit_outer_blocked_kernel"
-        be.knit_outer_stream(A2, B2, cA, cB, self.N, self.out, o_begin=o_begin, o_count=o_count, k_dev=k_eff)
+        be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, self.out, o_begin=o_begin, o_count=o_count,
+                             k_dev=p["k_eff"])
         if self.record_events:
             end.record()
             self.events.append((start, end))
-        if on_gpu:
-            ready.synchronize()  # the check only, not the knit queued behind it
-        if int(self._pinned_k[0]) == 0:
-            self._slice_exact(XA, XB, cA, cB)
+        if p["ready"] is not None:
+            p["ready"].synchronize()  # the check only, not the knit queued behind it
+        if int(p["pinned"][0]) == 0:
+            self._slice_exact(p["XA"], p["XB"], cA, cB)
         return self.out
+
+    # ------------------------------------------------------------------ overlapped steps
+    def overlap_ok(self) -> bool:
+        """Whether steps can be software-pipelined (``step(overlap=True)``): the device data-rank
+        path (single or slice mode) on a GPU backend, so everything before the write is stream work."""
+        return bool(self.dev_rank and self.mode in ("single", "slice") and getattr(self.be, "dev", None) is not None
+                    and self.be.dev.type == "cuda")
+
+    def _step_overlapped(self):
+        """One step with its sweep + operand transforms + data-rank compression (+ the slice
+        collectives) on a side stream and the write on the caller's stream, so the preparation of
+        this step runs while the previous step's write still streams: the write is HBM-bound, the
+        sweep VALU-bound. Buffers the write reads are tensors of this step, handed to the main
+        stream with record_stream; the sweep buffers are only read on the side stream."""
+        T, be = self.T, self.be
+        main = T.cuda.current_stream()
+        if self._prep_stream is None:
+            self._prep_stream = T.cuda.Stream(device=main.device)
+        S = self._prep_stream
+        with T.cuda.stream(S):
+            be.bind()
+            if self.record_events:
+                s0, s1 = be.event(), be.event()
+                s0.record()
+            qs = self.sweep()
+            if self.record_events:
+                s1.record()
+                self.sweep_events.append((s0, s1))
+            mats = self.operands(qs)
+            if self.out is None:
+                self.out = self._alloc_out(mats)
+            p = self._prep_slice(mats) if self.mode == "slice" else self._prep_dev_rank(mats)
+            done = T.cuda.Event()
+            done.record(S)
+        main.wait_event(done)
+        be.bind()
+        for k in ("A2", "B2", "k_eff"):
+            p[k].record_stream(main)
+        for m in p["mats"]:
+            m.record_stream(main)
+        n = len(self.events)
+        out = self._launch_slice(p) if self.mode == "slice" else self._launch_dev_rank(p)
+        if self.record_events and len(self.events) > n:
+            self.prep_events.append((s1, self.events[n][0]))
+        return out
 
     def _group_rank0(self) -> int:
         import torch.distributed as dist
@@ -888,6 +955,8 @@ class KnitPipeline:
                                   out=self.out)
 
     def step(self):
+        if self.overlap and self.overlap_ok():
+            return self._step_overlapped()
         if not self.record_events:
             return self.knit(self.sweep())
         start, end = self.be.event(), self.be.event()
