@@ -851,15 +851,26 @@ def nearest_probability_distribution(ctx: Context, dense, accuracy: float):
     return keys[:k].cpu().numpy(), vals[:k].cpu().numpy()
 
 
-def hellinger_fidelity(ctx: Context, p, q) -> float:
-    """Hellinger fidelity of two dense distributions (qiskit ``hellinger_fidelity``, as used at
-    ``Utilities.py:222-224``): ``(sum sqrt(p q) / sqrt(sum p sum q))^2`` with negatives clipped."""
+def hellinger_sums(ctx: Context, p, q):
+    """``qk_hellinger``: device [3] = (sum sqrt(p q), sum p, sum q) over non-negative parts; the
+    partial sums of disjoint shards add (multi-GPU fidelity: all_reduce, then the formula)."""
     T = torch()
     assert p.numel() == q.numel()
     acc = T.zeros(3, dtype=T.float64, device=p.device)
-    ctx.check(ctx.lib.qk_hellinger(ctx.handle, p.numel(), p.contiguous().data_ptr(), q.contiguous().data_ptr(),
-                                   acc.data_ptr()), "qk_hellinger")
-    s, sp, sq = acc.cpu().numpy().tolist()
+    if p.numel():
+        ctx.check(ctx.lib.qk_hellinger(ctx.handle, p.numel(), p.contiguous().data_ptr(), q.contiguous().data_ptr(),
+                                       acc.data_ptr()), "qk_hellinger")
+    return acc
+
+
+def fidelity_from_sums(s: float, sp: float, sq: float) -> float:
+    return 0.0 if sp <= 0 or sq <= 0 else float((s / np.sqrt(sp * sq)) ** 2)
+
+
+def hellinger_fidelity(ctx: Context, p, q) -> float:
+    """Hellinger fidelity of two dense distributions (qiskit ``hellinger_fidelity``, as used at
+    ``Utilities.py:222-224``): ``(sum sqrt(p q) / sqrt(sum p sum q))^2`` with negatives clipped."""
+    s, sp, sq = hellinger_sums(ctx, p, q).cpu().numpy().tolist()
     if sp <= 0 or sq <= 0:
         return 0.0
     return float((s / np.sqrt(sp * sq)) ** 2)

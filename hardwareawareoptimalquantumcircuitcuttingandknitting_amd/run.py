@@ -41,6 +41,8 @@ log = logging.getLogger(__name__)
 class RunTimeInfo:
     run_time: float
     knit_time: float
+    # multi-GPU runs: (first output, outputs) of this rank's contiguous share of the distribution
+    shard: tuple | None = None
 
 
 def _sync(device: int) -> None:
@@ -103,11 +105,82 @@ def run_virtual_circuit_dense(virt: VirtualCircuit, shots: int = 20000, *, devic
     return dense, RunTimeInfo(run_time, knit_time)
 
 
+def run_virtual_circuit_sharded(virt: VirtualCircuit, group=None, *, device: int | None = None, backend=None):
+    """Multi-GPU ``run_virtual_circuit`` (one process per GPU, ``torch.distributed`` initialised;
+    ``group``: the process group, None = WORLD). The instance sweep is sharded over the ranks and
+    the distribution assembled by the pipeline's collectives:
+
+    * wide outputs (syc 32: 2^32 fp64 = 34 GB) in ``slice`` mode: rank r returns the contiguous
+      outputs ``[r, r + 1) * 2^N / world`` of the reference-ordered distribution (concatenating the
+      ranks' shards in rank order gives the whole array);
+    * narrow outputs (bv / hwe / qft: at most the instance tensors' size) in ``reduce`` mode: one
+      RCCL reduce; rank 0 holds the whole distribution, the others ``None``.
+
+    Returns ``(tensor or None, RunTimeInfo)`` with ``info.shard = (first output, outputs)`` of the
+    returned tensor. Exact instances only (the reference's ``shots`` sampling: single-GPU
+    ``run_virtual_circuit(sample=True)``)."""
+    import torch.distributed as dist
+
+    from .pipeline import KnitPipeline
+
+    T = engine.torch()
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if device is None:
+        device = T.cuda.current_device() if backend is None else 0
+    log.info("Running virtualizer with %d %s fragments and %d vgates on %d ranks...",
+             len(virt.fragment_circuits), tuple(len(f) for f in virt.fragment_circuits),
+             len(virt.vgate_instructions), world)
+    kw = {"backend": backend} if backend is not None else {}
+    pipe = KnitPipeline(virt, device=device, factored=True, rank=rank, world=world, group=group, **kw)
+    if pipe.mode != "slice":
+        pipe = KnitPipeline(virt, device=device, factored=False, rank=rank, world=world, group=group,
+                            mode="reduce", **kw)
+    on_gpu = backend is None
+    now = perf_counter()
+    qs = pipe.sweep()
+    if on_gpu:
+        _sync(device)
+    run_time = perf_counter() - now
+    now = perf_counter()
+    out = pipe.knit(qs)
+    if on_gpu:
+        _sync(device)
+    knit_time = perf_counter() - now
+    log.info("Knitted in %.2fs.", knit_time)
+    if pipe.mode == "slice":
+        return out, RunTimeInfo(run_time, knit_time, tuple(pipe.slice))
+    n = 1 << pipe.N
+    return (out if rank == 0 else None), RunTimeInfo(run_time, knit_time, (0, n) if rank == 0 else (0, 0))
+
+
 def run_virtual_circuit(virt: VirtualCircuit, shots: int = 20000, *, device: int = 0,
-                        dense: bool = False, factored: bool = False, sample: bool = False, seed: int = 0):
-    """Reference-compatible entry point (``run.py:23-71``)."""
-    out, info = run_virtual_circuit_dense(virt, shots, device=device, factored=factored, sample=sample,
-                                          seed=seed)
+                        dense: bool = False, factored: bool = False, sample: bool = False, seed: int = 0,
+                        group=None):
+    """Reference-compatible entry point (``run.py:23-71``). ``group`` (a ``torch.distributed``
+    process group, e.g. ``dist.group.WORLD``) runs it on every rank of the group
+    (:func:`run_virtual_circuit_sharded`): ``dense=True`` returns the rank's shard, otherwise every
+    rank returns the whole reference-shaped dict (outputs of at most 24 clbits)."""
+    if group is not None:
+        if sample:
+            raise ValueError("multi-GPU runs sweep exact instances (sample=True: single GPU)")
+        out, info = run_virtual_circuit_sharded(virt, group, device=device)
+        if dense:
+            return out, info
+        import torch.distributed as dist
+
+        n_bits = virt.circuit.num_clbits
+        if n_bits > 24:
+            raise ValueError(f"a dict of 2^{n_bits} outcomes: use dense=True (each rank gets its shard)")
+        T = engine.torch()
+        full = T.zeros(1 << n_bits, dtype=T.float64, device=T.device("cuda", device))
+        lo, cnt = info.shard
+        if out is not None and cnt:
+            full[lo:lo + cnt] = out[:cnt]
+        dist.all_reduce(full, group=group)  # shards are disjoint: the sum assembles the distribution
+        out = full
+    else:
+        out, info = run_virtual_circuit_dense(virt, shots, device=device, factored=factored, sample=sample,
+                                              seed=seed)
     if dense:
         return out, info
     from . import quasi_distr

@@ -178,3 +178,60 @@ def test_slice_mode_matches_oracle(case, world, data_rank):
         assert dev and last_rank is not None and incompressible == 0
     if case == "cx_8x8":
         assert incompressible == 2 and last_rank is None
+
+
+def _api_worker(rank, world, port, case, q):
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from cpu_backend import CpuBackend
+
+        from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit
+        from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.run import run_virtual_circuit_sharded
+
+        _, cut = _slice_case(case) if case != "cx_3cuts" else _case(case)
+        out, info = run_virtual_circuit_sharded(VirtualCircuit(cut), backend=CpuBackend())
+        lo, cnt = info.shard
+        n = 1 << len([c for r in cut.cregs for c in r])
+        full = torch.zeros(n, dtype=torch.float64)
+        if out is not None and cnt:
+            full[lo:lo + cnt] = out[:cnt]
+        shards = [None] * world
+        dist.all_gather_object(shards, (lo, cnt))
+        dist.all_reduce(full)
+        if rank == 0:
+            q.put((full.numpy(), shards))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,world", [("hwe_p2", 2), ("cx_3cuts", 2), ("hwe_p2", 4)])
+def test_run_virtual_circuit_sharded_api(case, world):
+    """run_virtual_circuit_sharded (the group= form of run_virtual_circuit, run.py:23-71): slice mode
+    (hwe 16: 2^16 outputs) hands each rank a contiguous shard, in rank order; reduce mode (cx_3cuts:
+    2^6 outputs) the whole distribution on rank 0. Assembled, both equal the oracle's knit."""
+    from oracle import dense
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_api_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    full, shards = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sys.path.insert(0, HERE)
+    _, cut = _slice_case(case) if case != "cx_3cuts" else _case(case)
+    np.testing.assert_allclose(full, dense.run_dense(cut), atol=1e-12, rtol=0)
+    n = full.size
+    if case == "cx_3cuts":
+        assert shards[0] == (0, n) and all(s == (0, 0) for s in shards[1:])
+    else:
+        assert shards == [(r * n // world, n // world) for r in range(world)]

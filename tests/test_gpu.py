@@ -701,3 +701,62 @@ def test_rank_factors_device_degenerate(T):
         T.cuda.synchronize()
         assert int(rd.item()) == 0
         assert float(TA.abs().max()) == 0.0 and float(TB.abs().max()) == 0.0
+
+
+def test_concurrent_runs_from_two_threads(T):
+    """The reference calls run_virtual_circuit from several threads at once (Utilities.py:85-89,
+    132-136, each with its own Pool(8)). Two threads here run different circuits concurrently (one
+    qk context per thread, same device), twice each; every result equals the oracle's knit (1e-12)."""
+    import threading
+
+    from oracle import dense
+
+    import circuits
+
+    cases = {"hwe_16_1_p2": cutting.config_cut_circuit("hwe", 16, 1, 2)[1],
+             "bv_5_1_p2": cutting.config_cut_circuit("bv", 5, 1, 2)[1],
+             "cx_3cuts": circuits.two_fragment("cx", 3, 3, n_cuts=3)[1],
+             "move_gate": circuits.wire_cut(3, 2, extra_gate_cut=True)[1]}
+    refs = {k: dense.run_dense(c) for k, c in cases.items()}
+    plan = [["hwe_16_1_p2", "cx_3cuts", "hwe_16_1_p2", "cx_3cuts"], ["bv_5_1_p2", "move_gate", "move_gate", "bv_5_1_p2"]]
+    errs, failures = {}, []
+
+    def worker(names):
+        try:
+            for k in names:
+                out, _ = run_virtual_circuit(VirtualCircuit(cases[k]), dense=True, factored=(k != "bv_5_1_p2"))
+                T.cuda.current_stream().synchronize()
+                errs.setdefault(k, []).append(float(np.abs(out.cpu().numpy() - refs[k]).max()))
+        except Exception as e:  # surfaced below
+            failures.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(p,)) for p in plan]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not failures, failures
+    assert sorted(errs) == sorted(cases) and all(len(v) == 2 for v in errs.values())
+    assert max(max(v) for v in errs.values()) <= 1e-12, errs
+
+
+def test_npd_on_2_28_entries_known_answer(T):
+    """qk_threshold_count + qk_npd over 2^28 entries (quasi_distr.py:7-10,28-43, run.py:71): sub-
+    threshold noise everywhere plus 2000 planted entries above ACCURACY (a fifth negative); the
+    truncation keeps exactly the planted ones and the projection equals the oracle's NPD of them."""
+    from oracle.quasi import QD
+
+    n = 1 << 28
+    g = T.Generator(device="cuda").manual_seed(11)
+    v = (T.rand(n, dtype=T.float64, device="cuda", generator=g) - 0.5) * 1.8e-5  # |v| < 0.9e-5
+    rng = np.random.default_rng(12)
+    idx = np.unique(rng.integers(0, n, 2000))
+    vals = rng.uniform(2e-5, 1e-3, idx.size)
+    vals[rng.random(idx.size) < 0.2] *= -1.0
+    v[T.from_numpy(idx).cuda()] = T.from_numpy(vals).cuda()
+    keys, got = engine.nearest_probability_distribution(engine.get_context(0), v, 1e-5)
+    ref = QD({int(i): float(x) for i, x in zip(idx, vals)}, 1e-5).npd()
+    assert list(keys) == list(ref.keys())
+    np.testing.assert_allclose(got, list(ref.values()), rtol=0, atol=1e-15)
+    del v
+    T.cuda.empty_cache()
