@@ -28,6 +28,11 @@ class QkProgram(ctypes.Structure):
                 ("ops", c_vp), ("groups", c_vp), ("mats", c_vp)]
 
 
+class QkKnitPlan(ctypes.Structure):
+    _fields_ = [("n_frag", c_i32), ("nbits", c_i32), ("terms", c_i64), ("rows", ctypes.POINTER(c_i64)),
+                ("clbit_masks", ctypes.POINTER(c_u64)), ("transforms", ctypes.POINTER(c_vp))]
+
+
 #: every symbol include/qknit.h declares: name -> (restype, argtypes)
 SIGNATURES = {
     "qk_version": (ctypes.c_char_p, []),
@@ -60,6 +65,8 @@ SIGNATURES = {
                                            ctypes.c_uint64, c_i64, c_i64, c_vp, c_vp]),
     "qk_rank_factors": (c_i32, [c_vp, c_i64, c_vp, c_vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                 ctypes.c_int, c_vp, c_vp, c_vp]),
+    "qk_knit_workspace_bytes": (c_i32, [ctypes.POINTER(QkKnitPlan), ctypes.POINTER(c_i64)]),
+    "qk_knit": (c_i32, [c_vp, ctypes.POINTER(QkKnitPlan), c_vp, c_vp, c_i64, c_vp]),
     "qk_khatri_rao": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "qk_gather_rows": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "qk_npd_workspace_bytes": (c_i32, [c_i64, c_i64, ctypes.POINTER(c_i64)]),

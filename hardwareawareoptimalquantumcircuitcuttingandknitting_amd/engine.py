@@ -716,6 +716,49 @@ def fragment_operands(ctx: Context, ops: KnitOperands, qs: list) -> list:
     return mats
 
 
+def plan_transforms(ops: KnitOperands, frags: list) -> list:
+    """Per fragment the dense transform ``W_f`` ([swept rows, terms]) of the contraction:
+    ``X_f = W_f^T q_f`` (``qk_knit_plan.transforms``). Factored knits carry it already; the direct
+    knit's label gather + coefficients become a 0/coef matrix."""
+    out = []
+    for i, fs in enumerate(frags):
+        if ops.transforms[i] is not None:
+            out.append(np.ascontiguousarray(ops.transforms[i].T))
+            continue
+        W = np.zeros((fs.n_rows if not fs.dropped else 1, ops.num_terms))
+        W[ops.rows[i], np.arange(ops.num_terms)] = ops.coefs[i]
+        out.append(W)
+    return out
+
+
+def knit_plan_c(ctx: Context, virt, frags: list, qs: list, factored: bool = False, out=None):
+    """The whole knit through the plan-level C entry ``qk_knit`` (include/qknit.h): what a
+    non-Python host calls with the planner's transforms and masks. Same result as
+    :func:`knit_dense` (its exact contraction)."""
+    T = torch()
+    dev = T.device("cuda", ctx.device)
+    ops = knit_operands(virt, frags, factored)
+    N = virt.circuit.num_clbits
+    Ws = [T.from_numpy(W).to(dev) for W in plan_transforms(ops, frags)]
+    nf = len(frags)
+    rows = (ctypes.c_int64 * nf)(*[W.shape[0] for W in Ws])
+    masks = (ctypes.c_uint64 * nf)(*[sum(1 << c for c in cl) for cl in ops.clbits])
+    tp = (ctypes.c_void_p * nf)(*[W.data_ptr() for W in Ws])
+    plan = _lib.QkKnitPlan(nf, N, ops.num_terms, ctypes.cast(rows, ctypes.POINTER(ctypes.c_int64)),
+                           ctypes.cast(masks, ctypes.POINTER(ctypes.c_uint64)),
+                           ctypes.cast(tp, ctypes.POINTER(ctypes.c_void_p)))
+    need = ctypes.c_int64()
+    ctx.check(ctx.lib.qk_knit_workspace_bytes(ctypes.byref(plan), ctypes.byref(need)), "qk_knit_workspace_bytes")
+    ws = T.empty(max(need.value, 1), dtype=T.uint8, device=dev)
+    if out is None:
+        out = T.zeros(1 << N, dtype=T.float64, device=dev)
+    qc = [q.contiguous() for q in qs]
+    qp = (ctypes.c_void_p * nf)(*[q.data_ptr() for q in qc])
+    ctx.check(ctx.lib.qk_knit(ctx.handle, ctypes.byref(plan), qp, ws.data_ptr(), ws.numel(), out.data_ptr()), "qk_knit")
+    torch().cuda.current_stream(ctx.device).synchronize()  # Ws / ws / qc die with this frame
+    return out
+
+
 def knit_dense(ctx: Context, virt, frags: list[FragmentState], qs: list, out=None,
                factored: bool = False, num_clbits: int | None = None, row_block=None):
     """Dense knit on the GPU: returns the float64 distribution over all meas clbits.

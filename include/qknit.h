@@ -198,6 +198,29 @@ int qk_khatri_rao(qk_ctx* ctx, int64_t K, int64_t M, int64_t N, const double* A,
 int qk_gather_rows(qk_ctx* ctx, int64_t R, int64_t width, const int64_t* idx, const double* coef,
                    const double* src, double* dst);
 
+/* ---- plan-level knit (qknit_plan.hip) -------------------------------------------------------
+ * The whole knit of virtual_circuit.py:50-68 (merge + per-gate knits, i.e. qd:55-60 and
+ * vg:105-124,179-194,262-286 over every global label) from the swept rows of each fragment:
+ *   X_f = W_f^T q_f,  out[sum_f pdep(x_f, clbit_mask_f)] = sum_k prod_f X_f[k][x_f]
+ * with the transforms W_f ([rows_f][terms], DEVICE, row-major) precomputed by the planner (label
+ * gathers + knit coefficients, or the factored / basis / light-cone transforms: engine.knit_operands)
+ * and q_f = qk_sweep / qk_sweep_compiled_labels output ([rows_f][2^popcount(mask_f)], DEVICE). Writes
+ * every one of the 2^nbits outputs covered by the masks (clbits no fragment measures stay 0: pass a
+ * zeroed out). 1..4 fragments; 3+ are Khatri-Rao folded; the contraction is qk_gemm_keyed (fp64 MFMA).
+ * Replaces KnitPipeline.knit's exact path for non-Python hosts. */
+typedef struct qk_knit_plan {
+    int32_t n_frag;                  /* 1..4 */
+    int32_t nbits;                   /* output clbits N: out has 2^N entries */
+    int64_t terms;                   /* contraction terms K */
+    const int64_t* rows;             /* HOST [n_frag]: swept rows per fragment */
+    const uint64_t* clbit_masks;     /* HOST [n_frag]: global clbits each fragment measures (disjoint) */
+    const double* const* transforms; /* HOST [n_frag] of DEVICE [rows_f][terms] */
+} qk_knit_plan;
+
+int qk_knit_workspace_bytes(const qk_knit_plan* plan, int64_t* bytes);
+int qk_knit(qk_ctx* ctx, const qk_knit_plan* plan, const double* const* q, void* workspace, int64_t workspace_bytes,
+            double* out);
+
 /* ---- data-rank factors (qknit_rank.hip; data_rank.py is the host form) ----------------------
  * Two-fragment knit R = A^T B (A: [K][M], B: [K][N] operands of virtual_circuit.py:50-68's knit)
  * from its Gram matrices GA = A A^T, GB = B B^T ([K][K], DEVICE): pivoted Cholesky of each Gram

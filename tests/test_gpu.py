@@ -760,3 +760,25 @@ def test_npd_on_2_28_entries_known_answer(T):
     np.testing.assert_allclose(got, list(ref.values()), rtol=0, atol=1e-15)
     del v
     T.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("case,factored", [("hwe_16_1_p2", True), ("hwe_16_1_p2", False), ("cx_3cuts", True),
+                                           ("three", False), ("move_gate", True), ("bv_5_1_p2", False),
+                                           ("syc_16", True)])
+def test_plan_level_knit_c_entry(T, case, factored):
+    """qk_knit (include/qknit.h): the whole knit of virtual_circuit.py:50-68 from the swept rows and
+    the planner's transforms / clbit masks in one C call (what a non-Python host binds, see
+    INTEGRATION.md) equals the oracle's dense knit (1e-12): 2 and 3 fragments, direct and factored
+    transforms, wire cuts."""
+    cut = {"hwe_16_1_p2": lambda: cutting.config_cut_circuit("hwe", 16, 1, 2)[1],
+           "bv_5_1_p2": lambda: cutting.config_cut_circuit("bv", 5, 1, 2)[1],
+           "cx_3cuts": lambda: circuits.two_fragment("cx", 3, 3, n_cuts=3)[1],
+           "three": lambda: circuits.three_fragment(seed=9, sizes=(3, 2, 3))[1],
+           "move_gate": lambda: circuits.wire_cut(3, 2, extra_gate_cut=True)[1],
+           "syc_16": lambda: circuits.two_fragment("cx", 8, 8, n_cuts=4)[1]}[case]()
+    virt = VirtualCircuit(cut)
+    ctx = engine.get_context(0)
+    frags = engine.prepare_fragments(virt, 0, basis=factored)
+    qs = [engine.sweep_fragment(ctx, fs) for fs in frags]
+    got = engine.knit_plan_c(ctx, virt, frags, qs, factored=factored).cpu().numpy()
+    assert np.abs(got - dense.run_dense(cut)).max() <= 1e-12
