@@ -23,10 +23,12 @@ def trace(db: str, top: int):
     for name, dur in rows:
         agg[name].append(dur / 1e3)
     total = sum(sum(v) for v in agg.values())
-    print(f"{'kernel':72s} {'calls':>6s} {'total_us':>11s} {'avg_us':>10s} {'min_us':>9s} {'max_us':>9s} {'%':>6s}")
+    lines = [f"{'kernel':72s} {'calls':>6s} {'total_us':>11s} {'avg_us':>10s} {'min_us':>9s} {'max_us':>9s} {'%':>6s}"]
     for name, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:top]:
-        print(f"{name[:72]:72s} {len(v):6d} {sum(v):11.1f} {sum(v) / len(v):10.1f} {min(v):9.1f} {max(v):9.1f} "
-              f"{100 * sum(v) / total:6.2f}")
+        lines.append(f"{name[:72]:72s} {len(v):6d} {sum(v):11.1f} {sum(v) / len(v):10.1f} {min(v):9.1f} "
+                     f"{max(v):9.1f} {100 * sum(v) / total:6.2f}")
+    print("\n".join(lines))
+    return lines
 
 
 def pmc(kern: str, dbs: list, long_only: bool):
@@ -71,11 +73,19 @@ def main():
     p.add_argument("kernel")
     p.add_argument("dbs", nargs="+")
     p.add_argument("--long", action="store_true")
+    for q in (t, p):
+        q.add_argument("--out", default=None, help="also write the result here (trace: text, pmc: JSON)")
     a = ap.parse_args()
     if a.cmd == "trace":
-        trace(a.db, a.top)
+        lines = trace(a.db, a.top)
+        if a.out:
+            open(a.out, "w").write("\n".join(lines) + "\n")
     else:
-        pmc(a.kernel, a.dbs, a.long)
+        import json
+
+        res = pmc(a.kernel, a.dbs, a.long)
+        if a.out:
+            json.dump({"kernel": a.kernel, **res}, open(a.out, "w"), indent=1)
 
 
 if __name__ == "__main__":
