@@ -36,8 +36,9 @@ def pmc(kern: str, dbs: list, long_only: bool):
     durs = {}
     for db in dbs:
         con = sqlite3.connect(db)
+        # instr(): case-sensitive plain substring (LIKE is case-insensitive and '_' is a wildcard)
         rows = con.execute("select dispatch_id, kernel_name, counter_name, value, duration from counters_collection "
-                           "where kernel_name like ?", (f"%{kern}%",)).fetchall()
+                           "where instr(kernel_name, ?) > 0", (kern,)).fetchall()
         per = collections.defaultdict(float)
         dd = {}
         for did, _, cname, v, dur in rows:
