@@ -357,6 +357,24 @@ def traffic_per_launch(M, N, K):
     return None if best is None else best["hbm_bytes_per_launch"]
 
 
+def sweep_counters(workload: str):
+    """Counter-measured sweep bytes / flops per step (profiles/*sweep_pmc.json, written from
+    rocprofv3 --pmc passes over tools/sweep_bench.py): the HBM bytes the sweep kernels really moved
+    (2 x FETCH_SIZE + WRITE_SIZE) and the fp64 flops they executed (SQ_INSTS_VALU_{ADD,MUL,FMA}_F64),
+    per step, for the workload; None without a summary."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*sweep_pmc.json"))):
+        try:
+            rec = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if rec.get("workload", "").startswith(workload):
+            best = (os.path.basename(f), rec["per_step"])
+    return best
+
+
 def main():
     args = parse()
     import torch
@@ -476,21 +494,30 @@ def main():
         },
         "sweep": {
             "kernel": "per-program sweep kernels (sweep_codegen + hiprtc; FINAL pass sums each label's "
-                      "branch jobs) (all fragments, per step, this rank)",
-            "bound": "fp64 VALU / latency: two passes of 13-bit tiles move 0.6 GB per step (modelled "
-                     "hbm_bytes), far below the per-gate algorithmic model",
+                      "branch jobs, labels dispatched heaviest first) (all fragments, per step, this rank)",
+            "bound": "latency / LDS round trips: 1 workgroup (8 waves) per CU at 128 KiB tiles; neither HBM "
+                     "(0.37 GB per step on counters) nor fp64 VALU saturates (profiles/r02_sweep_pmc.json)",
             "ms_per_step": sweep_ms,
             "branch_jobs": counts["branch_jobs"],
-            "hbm_bytes": traffic["hbm"],
-            "hbm_GBs": traffic["hbm"] / (sweep_ms * 1e-3) / 1e9,
-            "hbm_frac": traffic["hbm"] / (sweep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "hbm_bytes_model": traffic["hbm"],
+            "hbm_GBs_model": traffic["hbm"] / (sweep_ms * 1e-3) / 1e9,
             "algorithmic_bytes": traffic["algorithmic"],
             "algorithmic_GBs": traffic["algorithmic"] / (sweep_ms * 1e-3) / 1e9,
-            "fp64_flops": traffic["flops"],
-            "fp64_TFs": traffic["flops"] / (sweep_ms * 1e-3) / 1e12,
-            "fp64_valu_frac": traffic["flops"] / (sweep_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
+            "fp64_flops_model": traffic["flops"],
         },
     }
+    cnt = sweep_counters(line["config"]["workload"])
+    if cnt is not None:  # counter bytes / flops per step, over this run's sweep time
+        src, c = cnt
+        line["sweep"].update({
+            "counters": src,
+            "hbm_bytes": c["hbm_bytes"],
+            "hbm_GBs": c["hbm_bytes"] / (sweep_ms * 1e-3) / 1e9,
+            "hbm_frac": c["hbm_bytes"] / (sweep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "fp64_flops": c["fp64_flops"],
+            "fp64_TFs": c["fp64_flops"] / (sweep_ms * 1e-3) / 1e12,
+            "fp64_valu_frac": c["fp64_flops"] / (sweep_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
+        })
     prep = [s.elapsed_time(e) for s, e in pipe.prep_events]
     if prep:
         line["rank_compress_ms"] = sum(prep) / len(prep)  # sweep end -> knit start (transforms, factors, probes)
