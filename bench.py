@@ -154,14 +154,61 @@ def cpu_baseline_qvm(cut, processes: int = 8, accuracy: float = 1e-5, return_res
     return out
 
 
+_KW = {}
+
+
+def _byte_pext_tables(clbits):
+    import numpy as np
+
+    t = np.zeros((4, 256), dtype=np.int64)
+    for byte in range(4):
+        for v in range(256):
+            x = v << (8 * byte)
+            t[byte, v] = sum(1 << j for j, c in enumerate(clbits) if (x >> c) & 1)
+    return t
+
+
+def _instance_worker(job):
+    """One exact instance (oracle statevector + signed fold) of the cut in _KW (forked worker)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import dense
+    from oracle.statevector import simulate
+
+    fi, li = job
+    view, f = _KW["view"], _KW["frags"][fi]
+    dense.fold(simulate(view.instance_ops(f, view.labels(f)[li]), len(f)), view.num_clbits,
+               dense.fragment_clbits(view, f))
+    return fi
+
+
+def _knit_worker_init(A2, B2, tA, tB):
+    _KW.update(A2=A2, B2=B2, tA=tA, tB=tB)
+
+
+def _knit_worker_chunk(rng):
+    """Outputs [lo, hi) of the compressed two-fragment knit in output order (numpy; one process)."""
+    import numpy as np
+
+    lo, hi = rng
+    A2, B2, tA, tB = _KW["A2"], _KW["B2"], _KW["tA"], _KW["tB"]
+    o = np.arange(lo, hi, dtype=np.int64)
+    ia = tA[0][o & 255] | tA[1][(o >> 8) & 255] | tA[2][(o >> 16) & 255] | tA[3][(o >> 24) & 255]
+    ib = tB[0][o & 255] | tB[1][(o >> 8) & 255] | tB[2][(o >> 16) & 255] | tB[3][(o >> 24) & 255]
+    out = np.take(A2[0], ia) * np.take(B2[0], ib)
+    for k in range(1, A2.shape[0]):
+        out += np.take(A2[k], ia) * np.take(B2[k], ib)
+    return float(out.sum())
+
+
 def cpu_baseline_same(pipe, cut, qs_host, n_inst_sample: int = 8, out_block_bits: int = 24) -> dict:
-    """The builder's algorithm on the host cores (numpy + BLAS threads), timed on a bounded sample of
-    the syc 32 5 step and extrapolated (factors stated): exact instances (oracle statevector, a
-    sample of ``n_inst_sample`` reference instances, scaled to the swept instance count), then on the
+    """The builder's algorithm on the host cores (one process per core; numpy + BLAS threads for
+    the transforms), timed on a bounded sample of the syc 32 5 step and extrapolated (factors
+    stated): exact instances (oracle statevector: one batch of one instance per process, scaled
+    to the swept instance count), then on the
     real swept rows (copied from the GPU run): operand transforms, Grams, data-rank factors
     (data_rank.rank_factors, the host form of qk_rank_factors), compressed operands, the 16-probe
-    check, and the streaming knit of one contiguous block of 2^out_block_bits outputs (pext index
-    gathers), scaled to 2^N."""
+    check, and the streaming knit (byte-table pext index gathers, numpy) of 4 x procs chunks of
+    2^(out_block_bits - 2) outputs spread over one process per host core, scaled to 2^N."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -176,18 +223,23 @@ def cpu_baseline_same(pipe, cut, qs_host, n_inst_sample: int = 8, out_block_bits
         threads = max([t.get("num_threads", 1) for t in threadpool_info()] + [1])
     except Exception:
         threads = os.cpu_count() or 1
+    from multiprocessing import Pool
+
     view = qvm.CutView(cut)
     frags = [list(r) for r in view.qregs if len(r)]
-    t0 = time.perf_counter()
-    done = 0
-    for f in frags:
-        cl = dense.fragment_clbits(view, f)
-        for label in view.labels(f)[: max(1, n_inst_sample // len(frags))]:
-            dense.fold(simulate(view.instance_ops(f, label), len(f)), view.num_clbits, cl)
-            done += 1
-    t_inst = (time.perf_counter() - t0) / done
+    procs = max(1, min(threads, len(os.sched_getaffinity(0))))
+    jobs = []
+    for fi, f in enumerate(frags):
+        jobs += [(fi, li) for li in range(min(len(view.labels(f)), max(1, procs // len(frags))))]
+    _KW.update(view=view, frags=frags)  # inherited by the forked workers
+    with Pool(procs) as pool:
+        t0 = time.perf_counter()
+        pool.map(_instance_worker, jobs)  # one exact instance per process, all at once
+        t_batch = time.perf_counter() - t0
+    done = len(jobs)
+    t_inst = t_batch  # wall time of one concurrent batch of `done` instances
     swept = pipe.instance_counts()["instances_swept"]
-    t_sweep = t_inst * swept
+    t_sweep = t_batch * -(-swept // done)
     ia, ib = pipe.order[0], pipe.order[-1]
     t1 = time.perf_counter()
     A = pipe.ops.transforms[ia] @ qs_host[ia]
@@ -198,37 +250,31 @@ def cpu_baseline_same(pipe, cut, qs_host, n_inst_sample: int = 8, out_block_bits
     x = np.random.default_rng(1234).standard_normal((B.shape[1], 16))
     err = np.linalg.norm(A.T @ (B @ x) - A2.T @ (B2 @ x), axis=0).max()
     t_prep = time.perf_counter() - t1
-    import torch
-
     cA, cB = pipe.ops.clbits[ia], pipe.ops.clbits[ib]
-    nblk = 1 << out_block_bits
-    torch.set_num_threads(threads)  # the write runs on torch's CPU kernels: every BLAS thread
-    At, Bt = torch.from_numpy(A2), torch.from_numpy(B2)
-    t2 = time.perf_counter()
-    o = torch.arange(nblk, dtype=torch.int64)
-    ia_idx = torch.zeros(nblk, dtype=torch.int64)
-    ib_idx = torch.zeros(nblk, dtype=torch.int64)
-    for j, c in enumerate(cA):
-        ia_idx |= ((o >> c) & 1) << j
-    for j, c in enumerate(cB):
-        ib_idx |= ((o >> c) & 1) << j
-    out = (At.index_select(1, ia_idx) * Bt.index_select(1, ib_idx)).sum(0)
-    t_blk = time.perf_counter() - t2
+    chunk = 1 << (out_block_bits - 2)
+    tasks = 4 * procs
+    nblk = chunk * tasks
+    with Pool(procs, initializer=_knit_worker_init, initargs=(A2, B2, _byte_pext_tables(cA),
+                                                                _byte_pext_tables(cB))) as pool:
+        pool.map(_knit_worker_chunk, [(0, 1024)] * procs)  # workers up
+        t2 = time.perf_counter()
+        out = pool.map(_knit_worker_chunk, [(i * chunk, (i + 1) * chunk) for i in range(tasks)])
+        t_blk = time.perf_counter() - t2
     scale = (1 << pipe.N) // nblk
     total = t_sweep + t_prep + t_blk * scale
     del out
     return {
         "value": pipe.instance_counts()["instances_ref"] / total,
         "unit": "instances/s",
-        "cores": int(threads),
+        "cores": int(procs),
         "kind": "port",
         "algorithm": "same as the GPU step (basis-reduced exact instances, factored light-cone knit, "
                      "data-rank compression, output-order write)",
         **host_info(),
-        "sample": (f"{done} exact instances at {t_inst * 1e3:.1f} ms each (x{swept / done:.0f} to the "
-                   f"{swept} swept); transforms + Grams + factors + probes on the real swept rows "
-                   f"{t_prep * 1e3:.0f} ms (rank {A2.shape[0]}, probe err {err:.1e}); knit of 2^{out_block_bits} "
-                   f"outputs {t_blk * 1e3:.0f} ms (x{scale} to 2^{pipe.N}): {total:.1f} s per full knit"),
+        "sample": (f"{done} exact instances at once on {procs} processes in {t_inst * 1e3:.0f} ms "
+                   f"(x{-(-swept // done)} batches to the {swept} swept); transforms + Grams + factors + probes on the real swept rows "
+                   f"{t_prep * 1e3:.0f} ms (rank {A2.shape[0]}, probe err {err:.1e}); knit of {nblk} outputs "
+                   f"on {procs} processes {t_blk * 1e3:.0f} ms (x{scale} to 2^{pipe.N}): {total:.1f} s per full knit"),
         "full_knit_s": total,
     }
 

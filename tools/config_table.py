@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-config results for BASELINE.md §5: every BASELINE.json shape on one MI355X.
 
-  python tools/config_table.py [--steps 5] [--out profiles/r01_configs.json]
+  python tools/config_table.py [--steps 5] [--out profiles/r02_configs.json]
 
 Per config: a KnitPipeline (factored knit where there are cuts, direct otherwise) is planned,
 warmed up and stepped; HIP events on the launch stream time the sweep and the contraction, wall
@@ -50,6 +50,7 @@ def run(key, steps):
         res = pipe.step()
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps
+    pipe.sync_stats()
     knit_ms = sum(s.elapsed_time(e) for s, e in pipe.events) / len(pipe.events)
     sweep_ms = sum(s.elapsed_time(e) for s, e in pipe.sweep_events) / len(pipe.sweep_events)
     M, N, K = pipe.gemm_shape()
