@@ -612,8 +612,10 @@ class KnitPipeline:
             start.record()
         if low is not None:
             res = self._contract_lowrank(low[0])
-        elif self.data_rank and self.mode == "single" and mats[self.order[0]].shape[0] <= 8:
-            res = self._contract_lowrank(mats)  # already small-K (e.g. the light-cone core): write-bound kernels
+        elif self.mode == "single" and len(self.order) == 2 and mats[self.order[0]].shape[0] <= 8:
+            # already small-K (syc 32 1: one label, K = 1; a light-cone core of rank <= 8): the
+            # write-bound kernels (blocked streaming knit when the fragments partition the output)
+            res = self._contract_lowrank(mats)
         else:
             res = self._contract(mats)
         if self.record_events:
