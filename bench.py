@@ -431,8 +431,16 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
+        # QKNIT_DIST_BACKEND=gloo + fewer GPUs than ranks: a rehearsal of the multi-GPU path with
+        # several ranks per device (RCCL refuses that); the default is RCCL, one rank per GPU
+        backend = os.environ.get("QKNIT_DIST_BACKEND", "nccl")
+        if backend != "nccl":
+            local %= torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
 

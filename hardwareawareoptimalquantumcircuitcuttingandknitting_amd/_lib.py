@@ -41,6 +41,9 @@ SIGNATURES = {
     "qk_ctx_set_stream": (c_i32, [c_vp, c_vp]),
     "qk_ctx_synchronize": (c_i32, [c_vp]),
     "qk_last_error": (ctypes.c_char_p, [c_vp]),
+    "qk_stream_create_cu_masked": (c_i32, [ctypes.c_int, ctypes.POINTER(c_u32), ctypes.c_int, ctypes.POINTER(c_vp)]),
+    "qk_stream_destroy": (c_i32, [c_vp]),
+    "qk_stream_cu_count": (c_i32, [ctypes.c_int, c_vp, ctypes.POINTER(ctypes.c_int)]),
     "qk_sweep_workspace_bytes": (c_i32, [ctypes.POINTER(QkProgram), c_i64, ctypes.POINTER(c_i64)]),
     "qk_sweep": (c_i32, [c_vp, ctypes.POINTER(QkProgram), c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "qk_module_compile": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,

@@ -12,6 +12,7 @@ struct qk_ctx {
     int device;
     hipStream_t own;     // created with the context
     hipStream_t stream;  // where launches go (own, or an external stream)
+    int cus;             // compute units the stream may use (its CU mask): persistent grids are sized to it
     std::string err;     // last error message (qk_last_error)
 };
 

@@ -1229,6 +1229,21 @@ extern "C" {
 
 const char* qk_version(void) { return "qknit 0.1 gfx950"; }
 
+// CUs a stream may run on: the popcount of its CU mask (hipExtStreamCreateWithCUMask), or every CU
+// of the device for unmasked streams / the null stream.
+static int stream_cus(hipStream_t s, int device) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1)
+        cus = 1;
+    uint32_t mask[32] = {0};
+    if (s && hipExtStreamGetCUMask(s, 32, mask) == hipSuccess) {
+        int n = 0;
+        for (uint32_t w : mask) n += __builtin_popcount(w);
+        if (n > 0 && n < cus) return n;
+    }
+    return cus;
+}
+
 int qk_ctx_create(int device, qk_ctx** out) {
     if (!out) return QK_EARG;
     *out = nullptr;
@@ -1240,6 +1255,7 @@ int qk_ctx_create(int device, qk_ctx** out) {
         return QK_EHIP;
     }
     c->stream = c->own;
+    c->cus = stream_cus(c->own, device);
     *out = c;
     return QK_OK;
 }
@@ -1255,7 +1271,33 @@ int qk_ctx_destroy(qk_ctx* ctx) {
 
 int qk_ctx_set_stream(qk_ctx* ctx, void* s) {
     if (!ctx) return QK_EARG;
+    if ((hipStream_t)s != ctx->stream || s == nullptr) ctx->cus = stream_cus((hipStream_t)s, ctx->device);
     ctx->stream = (hipStream_t)s;  // NULL = the device's null stream (torch's default stream)
+    return QK_OK;
+}
+
+int qk_stream_create_cu_masked(int device, const uint32_t* cu_mask, int mask_words, void** stream) {
+    if (!stream || !cu_mask || mask_words < 1 || mask_words > 32) return QK_EARG;
+    *stream = nullptr;
+    if (hipSetDevice(device) != hipSuccess) return QK_EHIP;
+    int n = 0;
+    for (int w = 0; w < mask_words; ++w) n += __builtin_popcount(cu_mask[w]);
+    if (n == 0) return QK_EARG;
+    hipStream_t s = nullptr;
+    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask_words, cu_mask) != hipSuccess) return QK_EHIP;
+    *stream = s;
+    return QK_OK;
+}
+
+int qk_stream_destroy(void* stream) {
+    if (!stream) return QK_EARG;
+    (void)hipStreamSynchronize((hipStream_t)stream);
+    return hipStreamDestroy((hipStream_t)stream) == hipSuccess ? QK_OK : QK_EHIP;
+}
+
+int qk_stream_cu_count(int device, void* stream, int* cus) {
+    if (!cus) return QK_EARG;
+    *cus = stream_cus((hipStream_t)stream, device);
     return QK_OK;
 }
 
@@ -1375,16 +1417,14 @@ int qk_gemm_keyed_pred(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const doubl
                            (lda % 2) == 0 && (ldb % 2) == 0;
     if (K >= 1 && K <= SK_MAX && !beta && !keyB && strideB == 1 && N % 2 == 0 && aligned16 &&
         (reinterpret_cast<uintptr_t>(out) & 15) == 0 && M * N >= (int64_t(1) << 16)) {
-        int cus = 0;
-        QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        const int cus = ctx->cus;
         const int64_t G = M < (int64_t)cus * 8 ? M : (int64_t)cus * 8;
         hipLaunchKernelGGL(qk_gemm_smallk_kernel<false>, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
         QK_HIP(ctx, hipGetLastError());
         return QK_OK;
     }
     if (QK_GEMM_GLDS && !beta && M % GT == 0 && N % GT == 0 && K % G2K == 0 && K > 0 && aligned16) {
-        int cus = 0;
-        QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        const int cus = ctx->cus;
         int64_t G = (int64_t)cus * QK_GLDS_WG_PER_CU;
         G = G < 8 ? 8 : G - G % 8;
         if (G > nblk) G = nblk;
@@ -1393,8 +1433,7 @@ int qk_gemm_keyed_pred(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const doubl
         return QK_OK;
     }
 #if QK_GEMM_PERSIST
-    int cus = 0;
-    QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const int cus = ctx->cus;
     int64_t G = (int64_t)cus * QK_GEMM_WG_PER_CU;
     G = G < 8 ? 8 : G - G % 8;
     if (G > nblk) G = nblk;
@@ -1422,8 +1461,7 @@ int qk_gemm_outer_paired(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const dou
         return fail(ctx, QK_EARG, "qk_gemm_outer_paired: N, ldb even and 16-B aligned B/out required%s");
     GemmArgs g{M, N, K, A, lda, B, ldb, keyA, strideA, keyB, 0, out, 0, 0, 0};
     QK_HIP(ctx, hipSetDevice(ctx->device));
-    int cus = 0;
-    QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const int cus = ctx->cus;
     const int64_t G = M < (int64_t)cus * 8 ? M : (int64_t)cus * 8;
     hipLaunchKernelGGL(qk_gemm_smallk_kernel<true>, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
     QK_HIP(ctx, hipGetLastError());
@@ -1455,8 +1493,7 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
         return fail(ctx, QK_EARG, "qk_knit_outer_stream: output range outside 0..2^nbits%s");
     if (o_count == 0) return QK_OK;
     QK_HIP(ctx, hipSetDevice(ctx->device));
-    int cus = 0;
-    QK_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const int cus = ctx->cus;
     const int align = __builtin_ctzll((uint64_t)(o_begin | o_count));
     const int tb = outer_blocked_tile(nbits, K, maskA, maskB, align);
     if (tb) {

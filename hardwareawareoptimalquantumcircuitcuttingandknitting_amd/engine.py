@@ -80,6 +80,50 @@ class Context:
             pass
 
 
+_MASKED_STREAMS: dict = {}
+
+
+def _destroy_masked_streams():
+    """atexit: destroy the CU-masked HIP streams while the runtime is still up."""
+    for key, st in list(_MASKED_STREAMS.items()):
+        try:
+            st.synchronize()
+            _lib.lib().qk_stream_destroy(ctypes.c_void_p(st.cuda_stream))
+        except Exception:
+            pass
+        _MASKED_STREAMS.pop(key, None)
+
+
+def device_cu_count(device: int = 0) -> int:
+    """Compute units of the device (what an unmasked stream may use)."""
+    lib = _lib.lib()
+    n = ctypes.c_int()
+    _lib.check(None, lib.qk_stream_cu_count(device, None, ctypes.byref(n)), "qk_stream_cu_count")
+    return n.value
+
+
+def cu_masked_stream(device: int, cus: tuple):
+    """A torch stream over a HIP stream restricted to the logical CUs ``cus``
+    (``qk_stream_create_cu_masked``), created once per (device, CU set) and kept for the process."""
+    key = (device, tuple(sorted(cus)))
+    with _modules_lock:
+        if key not in _MASKED_STREAMS:
+            lib = _lib.lib()
+            words = (max(key[1]) >> 5) + 1
+            mask = (ctypes.c_uint32 * words)()
+            for c in key[1]:
+                mask[c >> 5] |= 1 << (c & 31)
+            h = ctypes.c_void_p()
+            _lib.check(None, lib.qk_stream_create_cu_masked(device, mask, words, ctypes.byref(h)),
+                       "qk_stream_create_cu_masked")
+            if not _MASKED_STREAMS:
+                import atexit
+
+                atexit.register(_destroy_masked_streams)
+            _MASKED_STREAMS[key] = torch().cuda.ExternalStream(h.value, device=torch().device("cuda", device))
+        return _MASKED_STREAMS[key]
+
+
 _tls = threading.local()
 
 
@@ -202,7 +246,9 @@ def _compile_module(device: int, src: str, names: list):
 def jobs_to_device(jobs: JobTable, device):
     T = torch()
     dev = T.device("cuda", device)
-    slots = np.ascontiguousarray(jobs.slot_mats).view(np.float64).reshape(jobs.n_jobs, -1)
+    # a rank's share of a multi-GPU sweep may hold no jobs at all (more ranks than swept rows)
+    slots = (np.ascontiguousarray(jobs.slot_mats).view(np.float64).reshape(jobs.n_jobs, -1) if jobs.n_jobs
+             else np.zeros((0, 1)))
     slot_t = T.from_numpy(slots.copy()).to(dev) if slots.size else T.zeros(1, dtype=T.float64, device=dev)
     sign_t = T.from_numpy(jobs.sign.copy()).to(dev)
     off_t = T.from_numpy(jobs.label_offsets.copy()).to(dev)

@@ -300,6 +300,8 @@ class KnitPipeline:
         self._probe = None
         self._pinned = None  # host staging of the two Gram matrices (pinned on a GPU)
         self._prep_stream = None
+        self._write_stream = None
+        self.overlap_cus = None  # (prep CUs, write CUs) of pipelined steps
         # software-pipelined steps (_step_overlapped), off by default: measured on syc 32 5 (one box,
         # same build) 5.82 ms per step without, 7.20 with (the persistent write grid holds every CU,
         # so the side stream's sweep waits for it), 6.55 with a one-workgroup-per-task write grid,
@@ -764,17 +766,46 @@ class KnitPipeline:
         return bool(self.dev_rank and self.mode in ("single", "slice") and getattr(self.be, "dev", None) is not None
                     and self.be.dev.type == "cuda")
 
+    PREP_CUS = 32  # CUs of the preparation stream in a pipelined step (QKNIT_PREP_CUS; 0: no CU split)
+
+    def _overlap_streams(self):
+        """(prep stream, write stream) of pipelined steps. With ``QKNIT_PREP_CUS`` = c > 0 (default
+        PREP_CUS) both are CU-masked HIP streams (qk_stream_create_cu_masked): the preparation runs
+        on c CUs (c / 8 of every XCD), the write-bound knit on the rest, so neither waits for the other's workgroups to drain; c = 0: a plain side stream for the
+        preparation and the caller's stream for the write."""
+        if self._prep_stream is None:
+            T = self.T
+            dev = self.be.dev.index or 0
+            c = int(os.environ.get("QKNIT_PREP_CUS", str(self.PREP_CUS)))
+            total = engine.device_cu_count(dev)
+            if 0 < c < total:
+                # the top c logical CUs. The CU-mask bits of a stream are dealt over the XCDs (bit i ->
+                # XCD i % 8, CU i // 8 of it; tools/cu_mask_probe.py): a contiguous block of bits is
+                # the same few CUs of every XCD, while a mask leaving some XCD no CU leaves that XCD
+                # unrestricted (every-8th-bit masks confined nothing)
+                prep = tuple(range(total - c, total))
+                write = tuple(i for i in range(total) if i not in set(prep))
+                self._prep_stream = engine.cu_masked_stream(dev, prep)
+                self._write_stream = engine.cu_masked_stream(dev, write)
+                self.overlap_cus = (len(prep), len(write))
+            else:
+                self._prep_stream = T.cuda.Stream(device=self.be.dev)
+                self._write_stream = None
+                self.overlap_cus = (0, total)
+            self._prep_stream.wait_stream(T.cuda.current_stream())  # plan uploads before the first step
+        return self._prep_stream, self._write_stream
+
     def _step_overlapped(self):
         """One step with its sweep + operand transforms + data-rank compression (+ the slice
-        collectives) on a side stream and the write on the caller's stream, so the preparation of
-        this step runs while the previous step's write still streams: the write is HBM-bound, the
-        sweep VALU-bound. Buffers the write reads are tensors of this step, handed to the main
-        stream with record_stream; the sweep buffers are only read on the side stream."""
+        collectives) on the preparation stream and the write on the write stream (``_overlap_streams``),
+        so the preparation of this step runs while the previous step's write still streams: the write
+        is HBM-bound, the sweep VALU-bound. Buffers the write reads are tensors of this step, handed to
+        the write stream with record_stream; the sweep buffers are only touched on the preparation
+        stream (in order). The caller's stream waits for the write before the step returns."""
         T, be = self.T, self.be
         main = T.cuda.current_stream()
-        if self._prep_stream is None:
-            self._prep_stream = T.cuda.Stream(device=main.device)
-        S = self._prep_stream
+        S, W = self._overlap_streams()
+        W = W if W is not None else main
         with T.cuda.stream(S):
             be.bind()
             if self.record_events:
@@ -788,18 +819,21 @@ class KnitPipeline:
             if self.out is None:
                 self.out = self._alloc_out(mats)
             p = self._prep_slice(mats) if self.mode == "slice" else self._prep_dev_rank(mats)
-            done = T.cuda.Event()
+            done = T.cuda.Event(enable_timing=self.record_events)
             done.record(S)
-        main.wait_event(done)
+        if self.record_events:
+            self.prep_events.append((s1, done))
+        with T.cuda.stream(W):
+            W.wait_event(done)
+            be.bind()
+            for k in ("A2", "B2", "k_eff"):
+                p[k].record_stream(W)
+            for m in p["mats"]:
+                m.record_stream(W)
+            out = self._launch_slice(p) if self.mode == "slice" else self._launch_dev_rank(p)
+        if W is not main:
+            main.wait_stream(W)
         be.bind()
-        for k in ("A2", "B2", "k_eff"):
-            p[k].record_stream(main)
-        for m in p["mats"]:
-            m.record_stream(main)
-        n = len(self.events)
-        out = self._launch_slice(p) if self.mode == "slice" else self._launch_dev_rank(p)
-        if self.record_events and len(self.events) > n:
-            self.prep_events.append((s1, self.events[n][0]))
         return out
 
     def _group_rank0(self) -> int:

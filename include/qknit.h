@@ -93,6 +93,15 @@ int qk_ctx_destroy(qk_ctx* ctx);
 int qk_ctx_set_stream(qk_ctx* ctx, void* hip_stream);
 int qk_ctx_synchronize(qk_ctx* ctx);
 const char* qk_last_error(qk_ctx* ctx);
+
+/* A HIP stream restricted to a set of compute units (hipExtStreamCreateWithCUMask): bit i of
+ * cu_mask (mask_words 32-bit words) enables logical CU i. Kernels launched through a context bound
+ * to such a stream (qk_ctx_set_stream) size their persistent grids to its CU count. The pipelined
+ * step runs the write-bound knit on one CU set and the next step's sweep + data-rank
+ * preparation on the others. qk_stream_cu_count: the CUs a stream may use (all for NULL). */
+int qk_stream_create_cu_masked(int device, const uint32_t* cu_mask, int mask_words, void** stream);
+int qk_stream_destroy(void* stream);
+int qk_stream_cu_count(int device, void* stream, int* cus);
 const char* qk_version(void);
 
 /* Workspace (bytes) qk_sweep needs for n_jobs jobs of prog (0 in PACKED mode). */

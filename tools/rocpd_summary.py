@@ -31,6 +31,24 @@ def trace(db: str, top: int):
     return lines
 
 
+def timeline(db: str, last: int):
+    """The last ``last`` kernels in start order: start / end relative to the first of them (us),
+    duration, queue and stream ids (which kernels overlapped, on which queues)."""
+    con = sqlite3.connect(db)
+    cols = [d[0] for d in con.execute("select * from kernels limit 1").description]
+    extra = [c for c in ("queue_id", "stream_id", "queue", "stream") if c in cols]
+    rows = con.execute(f"select name, start, end{''.join(', ' + c for c in extra)} from kernels "
+                       "order by start").fetchall()[-last:]
+    t0 = rows[0][1] if rows else 0
+    lines = [f"columns: {cols}", f"{'start_us':>10s} {'end_us':>10s} {'dur_us':>9s} " + " ".join(f"{c:>9s}" for c in extra)
+             + "  kernel"]
+    for r in rows:
+        lines.append(f"{(r[1] - t0) / 1e3:10.1f} {(r[2] - t0) / 1e3:10.1f} {(r[2] - r[1]) / 1e3:9.1f} "
+                     + " ".join(f"{str(x):>9s}" for x in r[3:]) + "  " + r[0][:70])
+    print("\n".join(lines))
+    return lines
+
+
 def pmc(kern: str, dbs: list, long_only: bool):
     vals = collections.defaultdict(list)
     durs = {}
@@ -70,15 +88,18 @@ def main():
     t = sub.add_parser("trace")
     t.add_argument("db")
     t.add_argument("--top", type=int, default=30)
+    tl = sub.add_parser("timeline")
+    tl.add_argument("db")
+    tl.add_argument("--last", type=int, default=120)
     p = sub.add_parser("pmc")
     p.add_argument("kernel")
     p.add_argument("dbs", nargs="+")
     p.add_argument("--long", action="store_true")
-    for q in (t, p):
+    for q in (t, tl, p):
         q.add_argument("--out", default=None, help="also write the result here (trace: text, pmc: JSON)")
     a = ap.parse_args()
-    if a.cmd == "trace":
-        lines = trace(a.db, a.top)
+    if a.cmd in ("trace", "timeline"):
+        lines = trace(a.db, a.top) if a.cmd == "trace" else timeline(a.db, a.last)
         if a.out:
             open(a.out, "w").write("\n".join(lines) + "\n")
     else:
