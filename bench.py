@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--no-npd", action="store_true", help="skip the NPD timing on the 2^N output")
     ap.add_argument("--no-general", action="store_true",
                     help="skip knit_general (the same step without data-rank compression)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="plain steps only: no pipelining of the next step's sweep + data-rank preparation "
+                         "(CU-masked stream) under the current step's write")
     return ap.parse_args()
 
 
@@ -448,8 +451,13 @@ def main():
     circ, cut, desc = cutting.config_cut_circuit(name, n, d, p, variant)
     virt = VirtualCircuit(cut)
     torch.cuda.set_device(local)
+    # all work on a non-default stream: pipelined steps keep the legacy null stream idle
+    torch.cuda.set_stream(torch.cuda.Stream())
     pipe = KnitPipeline(virt, device=local, factored=not args.direct, rank=rank, world=world,
                         light_cone=not args.no_light_cone, data_rank=False if args.no_data_rank else None)
+    # pipelined steps (single GPU): step i+1's sweep + data-rank preparation run on a CU-masked stream
+    # while step i's write streams on the other CUs; every step still does all of its work
+    pipe.overlap = bool(world == 1 and not args.no_pipeline and pipe.overlap_ok())
     counts = pipe.instance_counts()
 
     def barrier():
@@ -480,6 +488,26 @@ def main():
         elapsed = float(t.item())
     pipe.sync_stats()  # device data rank: accepted ranks / fallbacks of the timed steps
     gemm_ms = sum(s.elapsed_time(e) for s, e in pipe.events) / max(len(pipe.events), 1)
+    pipelined = None
+    if pipe.overlap:
+        # the latency of one full knit (plain steps: nothing of the next step runs under the write), and
+        # the sweep / preparation times on the whole chip
+        pipelined = {"prep_cus": pipe.overlap_cus[0], "write_cus": pipe.overlap_cus[1],
+                     "ms_per_step_pipelined": elapsed / args.steps * 1e3,
+                     "pipelined_write_ms": gemm_ms}
+        pipe.overlap = False
+        pipe.step()
+        pipe.events.clear()
+        pipe.sweep_events.clear()
+        pipe.prep_events.clear()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            pipe.step()
+        torch.cuda.synchronize()
+        pipelined["full_knit_latency_ms"] = (time.perf_counter() - t1) / args.steps * 1e3
+        pipelined["plain_write_ms"] = sum(s.elapsed_time(e) for s, e in pipe.events) / max(len(pipe.events), 1)
+        pipe.sync_stats()
     sweep_ms = sum(s.elapsed_time(e) for s, e in pipe.sweep_events) / max(len(pipe.sweep_events), 1)
     traffic = pipe.sweep_traffic()
     M, Nn, K = pipe.gemm_shape()
@@ -575,6 +603,12 @@ def main():
     prep = [s.elapsed_time(e) for s, e in pipe.prep_events]
     if prep:
         line["rank_compress_ms"] = sum(prep) / len(prep)  # sweep end -> knit start (transforms, factors, probes)
+    if pipelined is not None:
+        pipelined["note"] = ("value / ms_per_step: pipelined steps (step i+1's sweep + data-rank preparation on "
+                             f"{pipelined['prep_cus']} CUs under step i's write on the other {pipelined['write_cus']}); "
+                             "full_knit_latency_ms: plain steps, one full knit each; roofline: the write launches of "
+                             "the timed (pipelined) steps; sweep / rank_compress_ms: the plain steps (whole chip)")
+        line["pipelined"] = pipelined
     if world == 1 and not args.no_npd:
         from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import quasi_distr
 

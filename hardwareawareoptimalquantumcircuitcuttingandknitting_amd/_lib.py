@@ -68,6 +68,15 @@ SIGNATURES = {
                                            ctypes.c_uint64, c_i64, c_i64, c_vp, c_vp]),
     "qk_rank_factors": (c_i32, [c_vp, c_i64, c_vp, c_vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                 ctypes.c_int, c_vp, c_vp, c_vp]),
+    "qk_prep_workspace_bytes": (c_i32, [c_vp, c_i64, c_i64, ctypes.POINTER(c_i64)]),
+    "qk_prep_operands": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_i64, c_vp, ctypes.c_int,
+                                 c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64]),
+    "qk_compress_operands": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
+                                     c_vp]),
+    "qk_probe_workspace_bytes": (c_i32, [c_vp, c_i64, ctypes.POINTER(c_i64)]),
+    "qk_probe_errors": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64,
+                                c_i64, c_vp, c_i64, c_vp, c_vp, ctypes.c_double, c_vp, c_vp, c_vp, c_i64]),
+    "qk_probe_accept": (c_i32, [c_vp, c_vp, ctypes.c_int, c_vp, ctypes.c_double, c_vp, c_vp]),
     "qk_knit_workspace_bytes": (c_i32, [ctypes.POINTER(QkKnitPlan), ctypes.POINTER(c_i64)]),
     "qk_knit": (c_i32, [c_vp, ctypes.POINTER(QkKnitPlan), c_vp, c_vp, c_i64, c_vp]),
     "qk_khatri_rao": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),

@@ -1,0 +1,468 @@
+// qknit_prep.hip — the data-rank step's operand preparation in three launches.
+//
+// Per step, the two-fragment knit R = A^T B needs, from the swept instance rows q_s [R_s][N_s]:
+//   X_s = W_s^T q_s            [K][N_s]  the light-cone operands (W_s: [R_s][K] transform),
+//   G_s = X_s X_s^T            [K][K]    their Gram matrices (qk_rank_factors' input),
+//   U   = X_B P^T              [K][16]   the B operand against the 16 fixed Gaussian probes P [16][N_B],
+// and, once qk_rank_factors has the factors T_A, T_B ([rmax][K]), the compressed operands
+//   A'' = T_A X_A, B'' = T_B X_B  [rmax][N_s]  the write kernel streams from.
+//
+// qk_prep_operands_kernel does the first three in one pass over q: a workgroup (8 waves) takes
+// 128-column tiles of both sides; each wave forms 16 columns of X with f64 MFMAs (16x16x4, K over
+// the instance rows), the tile goes to LDS once, and the same workgroup adds the tile's Gram block
+// (and, on the B side, its probe products) into register accumulators. Per-workgroup partial sums
+// go to a workspace that qk_prep_reduce_kernel sums in workgroup order (deterministic, no atomics).
+// Bound: fp64 MFMA (syc 32 5: 2.7 GFLOP of transforms + 1.2 of Grams / probes, 0.23 GB of HBM).
+// qk_compress_kernel forms A'' / B'' (one column per thread, T in LDS): HBM-bound on reading X.
+//
+// The acceptance check (qk_probe_errors / qk_probe_accept) runs on the real operands, as the probe
+// products would in torch, but without materialising them: V = B'' P^T ([rmax][16], MFMA, per-
+// workgroup partials), then per column c of A: d_c = X_A[:, c]^T U - A''[:, c]^T V (the row c of
+// (R - A''^T B'') P^T, formed by 16x16x4 MFMAs over K and then rmax) and e_p += d_{c,p}^2; the sums
+// give ||(R - A''^T B'') p_j||^2 per probe. Forming T_A^T T_B first would square the factors'
+// condition (their entries carry L^{-1}); A'' and B'' are balanced, so this keeps the fp64 floor.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "internal.h"
+
+namespace {
+
+typedef double d4_t __attribute__((ext_vector_type(4)));
+typedef double d2_t __attribute__((ext_vector_type(2)));
+
+constexpr int PK = 64;          // largest K (light-cone terms)
+constexpr int PCT = 128;        // columns per tile (8 waves x 16)
+constexpr int PNP = 16;         // probes
+constexpr int PTH = 512;        // threads per workgroup
+constexpr int XLD = PCT + 2;    // X tile row stride (doubles): a Gram k-step's 16 rows x 2 columns hit distinct banks
+constexpr int PPART = PK * PK + PK * PNP;  // doubles of one workgroup's partial sums per side
+
+struct PrepSide {
+    const double* Wt;  // [R][K]
+    const double* q;   // [R][ldq], columns [0, N)
+    int64_t ldq;
+    int64_t N;
+    int R;
+    double* X;         // [K][N]
+    const double* P;   // probes [16][N] (B side) or nullptr
+};
+
+struct PrepArgs {
+    PrepSide s[2];
+    int K;
+    double* part;  // [2][gridDim.x][PPART]
+};
+
+// Stage ring of the transform phase: PRS instance rows of q (128 columns) and of Wt per stage, moved
+// global -> LDS by global_load_lds (16 B per lane, no staging VGPRs); PNS stages in flight per
+// workgroup cover the HBM latency (4 x 28.7 KiB per CU). The ring and the X tile share the LDS.
+constexpr int PRS = 16;          // instance rows per stage (4 MFMA k-steps)
+constexpr int PNS = 4;           // stages in flight
+constexpr int QLD = PCT + 16;    // q stage row stride (doubles): rows 32 banks apart, a k-step's reads conflict-free
+constexpr int WLD = PK + 16;     // Wt stage row stride (same)
+struct PrepStage {
+    double q[PRS][QLD];
+    double w[PRS][WLD];
+};
+union PrepLds {
+    PrepStage st[PNS];
+    double x[PK][XLD];
+};
+
+__device__ __forceinline__ void prep_glds(const double* src, double* lds_row) {
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                     reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                         reinterpret_cast<uintptr_t>(lds_row)),
+                                     16, 0, 0);
+}
+
+// s_waitcnt vmcnt(n) for a run-time n (n > 15 waits for 15: always safe, only later loads in flight)
+__device__ __forceinline__ void prep_vmwait(int n) {
+    switch (n < 15 ? n : 15) {
+#define QK_PW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+        QK_PW(0) QK_PW(1) QK_PW(2) QK_PW(3) QK_PW(4) QK_PW(5) QK_PW(6) QK_PW(7)
+        QK_PW(8) QK_PW(9) QK_PW(10) QK_PW(11) QK_PW(12) QK_PW(13) QK_PW(14) QK_PW(15)
+#undef QK_PW
+    }
+}
+
+__global__ __launch_bounds__(PTH) void qk_prep_operands_kernel(PrepArgs a) {
+    __shared__ __attribute__((aligned(16))) PrepLds L;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l16 = lane & 15, l4 = lane >> 4;
+    const int K = a.K;
+    const int bi = wave & 3, bj0 = (wave >> 2) * 2;  // Gram blocks of this wave: (bi, bj0), (bi, bj0 + 1)
+    const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+    for (int sd = 0; sd < 2; ++sd) {
+        const PrepSide& S = a.s[sd];
+        const int R = S.R;
+        const int nst = (R + PRS - 1) / PRS;
+        const int64_t tiles = S.N / PCT;
+        d4_t g0 = {0, 0, 0, 0}, g1 = {0, 0, 0, 0}, u = {0, 0, 0, 0};
+        for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+            const int64_t c0 = t * PCT;
+            // stage loads: this wave moves q rows 2w, 2w+1 (one 1-KiB wave-instruction each) and Wt
+            // rows 2w, 2w+1 (lanes < K/2: 16 B each); rows >= R are not loaded (masked at use)
+            int nload[PNS];  // loads this wave issued per ring slot (for the vmcnt accounting)
+            auto issue = [&](int st) {
+                PrepStage& P = L.st[st % PNS];
+                int n = 0;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int rl = 2 * wave_s + h, r = st * PRS + rl;
+                    if (r < R) {
+                        prep_glds(S.q + (int64_t)r * S.ldq + c0 + 2 * lane, &P.q[rl][0]);
+                        ++n;
+                        if (2 * lane < K) prep_glds(S.Wt + (int64_t)r * K + 2 * lane, &P.w[rl][0]);
+                        ++n;  // counted for every lane alike (wave-uniform accounting)
+                    }
+                }
+                nload[st % PNS] = n;
+            };
+            __syncthreads();  // the previous tile's X readers are done with the LDS
+            for (int st = 0; st < PNS - 1 && st < nst; ++st) issue(st);
+            d4_t x[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = (d4_t){0, 0, 0, 0};
+            for (int st = 0; st < nst; ++st) {
+                int after = 0;  // loads of this wave issued after stage st's
+                for (int d = st + 1; d < st + PNS - 1 && d < nst; ++d) after += nload[d % PNS];
+                prep_vmwait(after);
+                __syncthreads();  // stage st landed for every wave; stage st - 1 fully read
+                if (st + PNS - 1 < nst) issue(st + PNS - 1);
+                const PrepStage& P = L.st[st % PNS];
+#pragma unroll
+                for (int kk = 0; kk < PRS / 4; ++kk) {
+                    const int rl = 4 * kk + l4;
+                    const bool rv = st * PRS + rl < R;
+                    const double qb = rv ? P.q[rl][16 * wave + l16] : 0.0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int k = 16 * i + l16;
+                        const double wa = (rv && k < K) ? P.w[rl][k] : 0.0;
+                        x[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa, qb, x[i], 0, 0, 0);
+                    }
+                }
+            }
+            __syncthreads();  // every wave is done with the ring: the X tile takes its place
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) L.x[16 * i + l4 + 4 * rr][16 * wave + l16] = x[i][rr];
+            __syncthreads();
+            // ---- Gram blocks and (B side) probe products over the tile's 128 columns
+            const bool probes = S.P != nullptr && wave < 4;
+#pragma unroll 4
+            for (int s4 = 0; s4 < PCT / 4; ++s4) {
+                const int c = 4 * s4 + l4;
+                const double av = L.x[16 * bi + l16][c];
+                const double b0 = L.x[16 * bj0 + l16][c];
+                const double b1 = L.x[16 * (bj0 + 1) + l16][c];
+                g0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0, g0, 0, 0, 0);
+                g1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b1, g1, 0, 0, 0);
+                if (probes) {  // wave-uniform; waves 0-3: bi == wave
+                    const double px = S.P[(int64_t)l16 * S.N + c0 + c];
+                    u = __builtin_amdgcn_mfma_f64_16x16x4f64(av, px, u, 0, 0, 0);
+                }
+            }
+            // ---- X tile to HBM: row tid >> 3, 16 columns per thread (8 x 16-B stores)
+            const int row = tid >> 3, col = (tid & 7) * 16;
+            if (row < K) {
+                double* dst = S.X + (int64_t)row * S.N + c0 + col;
+#pragma unroll
+                for (int v = 0; v < 8; ++v) {
+                    d2_t z;
+                    z.x = L.x[row][col + 2 * v];
+                    z.y = L.x[row][col + 2 * v + 1];
+                    *reinterpret_cast<d2_t*>(dst + 2 * v) = z;
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's load accounting starts at 0
+        }
+        // ---- this workgroup's partial sums (zero if it took no tile)
+        double* p = a.part + ((int64_t)sd * gridDim.x + blockIdx.x) * PPART;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int gr = 16 * bi + l4 + 4 * rr;
+            p[gr * PK + 16 * bj0 + l16] = g0[rr];
+            p[gr * PK + 16 * (bj0 + 1) + l16] = g1[rr];
+            if (wave < 4) p[PK * PK + (16 * wave + l4 + 4 * rr) * PNP + l16] = u[rr];
+        }
+    }
+}
+
+// out (sums in a fixed order): GA [K][K], GB [K][K], U [K][16] (from the B side's partials). A
+// workgroup takes 64 consecutive outputs; its 4 waves sum every 4th partial row (coalesced 512-B row
+// segments, 4 x more loads in flight than one thread per output), then LDS adds the 4 sums.
+__global__ __launch_bounds__(256) void qk_prep_reduce_kernel(const double* __restrict__ part, int nblk, int K,
+                                                             double* __restrict__ GA, double* __restrict__ GB,
+                                                             double* __restrict__ U) {
+    __shared__ double acc[4][64];
+    const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + lane;  // [0, 2 K^2 + 16 K)
+    const int KK = K * K;
+    int sd = -1, off = 0;
+    double* dst = nullptr;
+    if (e < KK) {
+        sd = 0, off = (e / K) * PK + e % K, dst = GA + e;
+    } else if (e < 2 * KK) {
+        sd = 1, off = ((e - KK) / K) * PK + (e - KK) % K, dst = GB + (e - KK);
+    } else if (e < 2 * KK + PNP * K) {
+        const int f = e - 2 * KK;
+        sd = 1, off = PK * PK + f, dst = U + f;  // U rows k < K: [k][16]
+    }
+    double s = 0.0;
+    if (sd >= 0) {
+        const double* p = part + (int64_t)sd * nblk * PPART + off;
+        for (int b = grp; b < nblk; b += 4) s += p[(int64_t)b * PPART];
+    }
+    acc[grp][lane] = s;
+    __syncthreads();
+    if (grp == 0 && dst) *dst = (acc[0][lane] + acc[1][lane]) + (acc[2][lane] + acc[3][lane]);
+}
+
+// out[j][c] = sum_k T[j][k] X[k][c] for j < rmax, both sides (blockIdx.y); columns per thread
+__global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const double* __restrict__ TA,
+                                                          const double* __restrict__ XA, int64_t NA,
+                                                          double* __restrict__ A2, const double* __restrict__ TB,
+                                                          const double* __restrict__ XB, int64_t NB,
+                                                          double* __restrict__ B2) {
+    __shared__ double T[8][PK];
+    const bool bs = blockIdx.y == 1;
+    const double* Tg = bs ? TB : TA;
+    const double* X = bs ? XB : XA;
+    double* out = bs ? B2 : A2;
+    const int64_t N = bs ? NB : NA;
+    for (int e = threadIdx.x; e < rmax * K; e += 256) T[e / K][e % K] = Tg[e];
+    __syncthreads();
+    for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < N; c += (int64_t)gridDim.x * 256) {
+        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < K; ++k) {
+            const double xv = X[(int64_t)k * N + c];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < rmax) acc[j] = fma(T[j][k], xv, acc[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j < rmax) out[(int64_t)j * N + c] = acc[j];
+    }
+}
+
+constexpr int PV_GRID = 64;  // workgroups of the V = B'' P^T partial sums
+
+// V partials: vpart[b][j][p] = sum over this workgroup's columns c of B2[j][c] P[p][c] (j < rmax)
+__global__ __launch_bounds__(256) void qk_probe_v_kernel(int rmax, const double* __restrict__ B2, int64_t ldb2,
+                                                         int64_t NB, const double* __restrict__ P, int64_t ldp,
+                                                         double* __restrict__ vpart) {
+    __shared__ double red[4][256];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, l4 = lane >> 4;
+    d4_t acc = {0, 0, 0, 0};
+    for (int64_t c0 = ((int64_t)blockIdx.x * 4 + wave) * 4; c0 < NB; c0 += (int64_t)gridDim.x * 16) {
+        const int64_t c = c0 + l4;
+        const double av = l16 < rmax ? B2[(int64_t)l16 * ldb2 + c] : 0.0;  // A[j][c]
+        const double bv = P[(int64_t)l16 * ldp + c];                       // B[c][p]
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) red[wave][(l4 + 4 * rr) * 16 + l16] = acc[rr];
+    __syncthreads();
+    vpart[(int64_t)blockIdx.x * 256 + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+}
+
+// e2 partials over 16-column blocks of A: d = X_A^T U - A2^T V, epart[b][p] = sum of d[c][p]^2
+__global__ __launch_bounds__(256) void qk_probe_d_kernel(int K, int rmax, const double* __restrict__ XA, int64_t ldx,
+                                                         int64_t NA, const double* __restrict__ A2, int64_t lda2,
+                                                         const double* __restrict__ U,
+                                                         const double* __restrict__ vpart, int gv,
+                                                         double* __restrict__ epart) {
+    __shared__ double Us[PK][PNP];
+    __shared__ double Vs[16][PNP];
+    __shared__ double ep[4][PNP];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, l4 = lane >> 4;
+    {
+        double v = 0.0;
+        for (int b = 0; b < gv; ++b) v += vpart[(int64_t)b * 256 + tid];
+        Vs[tid / 16][tid % 16] = -v;  // rows >= rmax are zero sums
+    }
+    for (int e = tid; e < PK * PNP; e += 256) Us[e / PNP][e % PNP] = (e / PNP) < K ? U[e] : 0.0;
+    __syncthreads();
+    double e2 = 0.0;
+    const int ksteps = (K + 3) / 4;
+    for (int64_t cb = (int64_t)blockIdx.x * 4 + wave; cb * 16 < NA; cb += (int64_t)gridDim.x * 4) {
+        const int64_t c = cb * 16 + l16;
+        d4_t acc = {0, 0, 0, 0};
+        for (int kk = 0; kk < ksteps; ++kk) {
+            const int k = 4 * kk + l4;
+            const double av = k < K ? XA[(int64_t)k * ldx + c] : 0.0;  // A[c][k]
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Us[k][l16], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int j = 4 * jj + l4;
+            const double av = j < rmax ? A2[(int64_t)j * lda2 + c] : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Vs[j][l16], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) e2 = fma(acc[rr], acc[rr], e2);  // d[cb*16 + l4 + 4rr][l16]
+    }
+    e2 += __shfl_xor(e2, 16, 64);
+    e2 += __shfl_xor(e2, 32, 64);
+    if (l4 == 0) ep[wave][l16] = e2;
+    __syncthreads();
+    if (tid < PNP) epart[(int64_t)blockIdx.x * PNP + tid] = ep[0][tid] + ep[1][tid] + ep[2][tid] + ep[3][tid];
+}
+
+// e2_out[p] = sum_b epart[b][p]; with k_out: *err_out = sqrt(max_p e2), *k_out = (r > 0 && err <= tol) ? r : 0.
+// 256 threads: thread t sums rows b = t / 16, + 16, ... of probe t % 16, then a fixed-order LDS tree.
+__global__ __launch_bounds__(256) void qk_probe_accept_kernel(const double* __restrict__ epart, int n,
+                                                              const int32_t* __restrict__ r_dev, double tol,
+                                                              double* __restrict__ e2_out, int32_t* __restrict__ k_out,
+                                                              double* __restrict__ err_out) {
+    __shared__ double acc[256];
+    const int tid = threadIdx.x, p = tid % PNP;
+    double s = 0.0;
+    for (int b = tid / PNP; b < n; b += 256 / PNP) s += epart[(int64_t)b * PNP + p];
+    acc[tid] = s;
+    __syncthreads();
+    for (int w = 128; w >= PNP; w >>= 1) {
+        if (tid < w) acc[tid] += acc[tid + w];
+        __syncthreads();
+    }
+    if (tid < PNP && e2_out) e2_out[tid] = acc[tid];
+    if (tid == 0 && k_out) {
+        double m = 0.0;
+        for (int q = 0; q < PNP; ++q) m = fmax(m, acc[q]);
+        const double err = sqrt(m);
+        const int r = *r_dev;
+        if (err_out) *err_out = err;
+        *k_out = (r > 0 && err <= tol) ? r : 0;
+    }
+}
+
+int probe_grid_d(qk_ctx* ctx, int64_t NA) {
+    const int64_t blocks = (NA + 63) / 64;  // 4 waves x 16 columns
+    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 2;
+    return (int)(blocks < cap ? (blocks > 0 ? blocks : 1) : cap);
+}
+
+int fail(qk_ctx* ctx, int code, const char* msg) {
+    ctx->err = msg;
+    return code;
+}
+
+int prep_grid(qk_ctx* ctx, int64_t NA, int64_t NB) {
+    const int64_t tiles = (NA > NB ? NA : NB) / PCT;
+    const int64_t g = ctx->cus > 0 ? ctx->cus : 256;  // one 512-thread workgroup per CU
+    return (int)(tiles < g ? (tiles > 0 ? tiles : 1) : g);
+}
+
+}  // namespace
+
+extern "C" {
+
+int qk_prep_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes) {
+    if (!ctx || !bytes) return QK_EARG;
+    *bytes = (int64_t)2 * prep_grid(ctx, NA, NB) * PPART * (int64_t)sizeof(double);
+    return QK_OK;
+}
+
+int qk_prep_operands(qk_ctx* ctx, int K, int RA, const double* WtA, const double* qA, int64_t ldqA, int64_t NA,
+                     double* XA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB, double* XB,
+                     const double* probes, double* GA, double* GB, double* U, double* work, int64_t work_bytes) {
+    if (!ctx) return QK_EARG;
+    if (K < 2 || K > PK || (K & 1) || RA < 1 || RB < 1)
+        return fail(ctx, QK_EARG, "qk_prep_operands: need even 2 <= K <= 64 and R >= 1 on both sides");
+    if (((reinterpret_cast<uintptr_t>(WtA) | reinterpret_cast<uintptr_t>(WtB) | reinterpret_cast<uintptr_t>(qA) |
+          reinterpret_cast<uintptr_t>(qB)) & 15) || (ldqA & 1) || (ldqB & 1))
+        return fail(ctx, QK_EARG, "qk_prep_operands: 16-B aligned Wt / q and even ldq required");
+    if (NA < PCT || NB < PCT || NA % PCT || NB % PCT || ldqA < NA || ldqB < NB)
+        return fail(ctx, QK_EARG, "qk_prep_operands: columns must be a positive multiple of 128 (ldq >= N)");
+    if (!WtA || !qA || !XA || !WtB || !qB || !XB || !probes || !GA || !GB || !U || !work)
+        return fail(ctx, QK_EARG, "qk_prep_operands: null buffer");
+    const int G = prep_grid(ctx, NA, NB);
+    if (work_bytes < (int64_t)2 * G * PPART * (int64_t)sizeof(double))
+        return fail(ctx, QK_EARG, "qk_prep_operands: workspace too small (qk_prep_workspace_bytes)");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_prep_operands: hipSetDevice");
+    PrepArgs args;
+    args.s[0] = PrepSide{WtA, qA, ldqA, NA, RA, XA, nullptr};
+    args.s[1] = PrepSide{WtB, qB, ldqB, NB, RB, XB, probes};
+    args.K = K;
+    args.part = work;
+    hipLaunchKernelGGL(qk_prep_operands_kernel, dim3(G), dim3(PTH), 0, ctx->stream, args);
+    const int outs = 2 * K * K + PNP * K;
+    hipLaunchKernelGGL(qk_prep_reduce_kernel, dim3((outs + 63) / 64), dim3(256), 0, ctx->stream, work, G, K, GA,
+                       GB, U);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_prep_operands: ") + hipGetErrorString(e)).c_str());
+    return QK_OK;
+}
+
+int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, double* A2,
+                         const double* TB, const double* XB, int64_t NB, double* B2) {
+    if (!ctx) return QK_EARG;
+    if (K < 1 || K > PK || rmax < 1 || rmax > 8 || NA < 1 || NB < 1)
+        return fail(ctx, QK_EARG, "qk_compress_operands: need 1 <= K <= 64, 1 <= rmax <= 8, N >= 1");
+    if (!TA || !XA || !A2 || !TB || !XB || !B2) return fail(ctx, QK_EARG, "qk_compress_operands: null buffer");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_compress_operands: hipSetDevice");
+    const int64_t N = NA > NB ? NA : NB;
+    int64_t gx = (N + 255) / 256;
+    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 4;
+    gx = gx < cap ? gx : cap;
+    hipLaunchKernelGGL(qk_compress_kernel, dim3((unsigned)gx, 2), dim3(256), 0, ctx->stream, K, rmax, TA, XA, NA, A2,
+                       TB, XB, NB, B2);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(ctx, QK_EHIP, (std::string("qk_compress_operands: ") + hipGetErrorString(e)).c_str());
+    return QK_OK;
+}
+
+int qk_probe_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t* bytes) {
+    if (!ctx || !bytes) return QK_EARG;
+    *bytes = (int64_t)(PV_GRID * 256 + probe_grid_d(ctx, NA) * PNP) * (int64_t)sizeof(double);
+    return QK_OK;
+}
+
+int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx, int64_t NA, const double* A2,
+                    int64_t lda2, const double* U, const double* B2, int64_t ldb2, int64_t NB, const double* probes,
+                    int64_t ldp, double* e2, const int32_t* r_dev, double tol, int32_t* k_out, double* err_out,
+                    double* work, int64_t work_bytes) {
+    if (!ctx) return QK_EARG;
+    if (K < 1 || K > PK || rmax < 1 || rmax > 8 || NA < 16 || NA % 16 || NB < 4 || NB % 4)
+        return fail(ctx, QK_EARG, "qk_probe_errors: need 1 <= K <= 64, 1 <= rmax <= 8, NA % 16 == 0, NB % 4 == 0");
+    if (!XA || !A2 || !U || !B2 || !probes || !work || (k_out && !r_dev))
+        return fail(ctx, QK_EARG, "qk_probe_errors: null buffer");
+    if (ldx < NA || ldb2 < NB || ldp < NB) return fail(ctx, QK_EARG, "qk_probe_errors: leading dimension");
+    const int gd = probe_grid_d(ctx, NA);
+    if (work_bytes < (int64_t)(PV_GRID * 256 + gd * PNP) * (int64_t)sizeof(double))
+        return fail(ctx, QK_EARG, "qk_probe_errors: workspace too small (qk_probe_workspace_bytes)");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_probe_errors: hipSetDevice");
+    double* vpart = work;
+    double* epart = work + PV_GRID * 256;
+    hipLaunchKernelGGL(qk_probe_v_kernel, dim3(PV_GRID), dim3(256), 0, ctx->stream, rmax, B2, ldb2, NB, probes, ldp,
+                       vpart);
+    hipLaunchKernelGGL(qk_probe_d_kernel, dim3(gd), dim3(256), 0, ctx->stream, K, rmax, XA, ldx, NA, A2, lda2, U, vpart,
+                       PV_GRID, epart);
+    hipLaunchKernelGGL(qk_probe_accept_kernel, dim3(1), dim3(256), 0, ctx->stream, epart, gd, r_dev, tol, e2, k_out,
+                       err_out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_probe_errors: ") + hipGetErrorString(e)).c_str());
+    return QK_OK;
+}
+
+int qk_probe_accept(qk_ctx* ctx, const double* e2, int n, const int32_t* r_dev, double tol, int32_t* k_out,
+                    double* err_out) {
+    if (!ctx) return QK_EARG;
+    if (!e2 || !r_dev || !k_out || n < 1) return fail(ctx, QK_EARG, "qk_probe_accept: null buffer or n < 1");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_probe_accept: hipSetDevice");
+    hipLaunchKernelGGL(qk_probe_accept_kernel, dim3(1), dim3(256), 0, ctx->stream, e2, n, r_dev, tol, nullptr, k_out,
+                       err_out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_probe_accept: ") + hipGetErrorString(e)).c_str());
+    return QK_OK;
+}
+
+}  // extern "C"

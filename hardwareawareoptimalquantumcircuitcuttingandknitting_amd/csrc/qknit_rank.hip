@@ -6,8 +6,8 @@
 // and T_X = S_r^{1/2} V_r^T L_X[P_X]^{-1} in the pivot columns, written as [rmax][K] (rows >= r zero)
 // with r in *r_out. r_out = 0 means "no usable factorisation" (R = 0, no convergence within 32 pivot
 // steps, or r > rmax): the caller's exact contraction then runs (predicated on the same int).
-// The step that consumes these (KnitPipeline) verifies the compressed product with probes on the
-// real operands before trusting it, on the device too.
+// The step that consumes these verifies the compressed product on the real operands
+// (qk_probe_check, csrc/qknit_prep.hip) before trusting it, on the device too.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -45,6 +45,7 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
     __shared__ double Y[2][RK_R][RK_RC];     // triangular-solve results
     __shared__ double sv[RK_RC];
     __shared__ int piv[2][RK_RC], nsteps[2], conv[2], order[RK_RC], rank_s, rotated;
+    __shared__ double Ts[2][RK_R][RK_K];       // T_A, T_B
 
     const int tid = threadIdx.x, lane = tid & 63, side = tid >> 6, K = a.K;
     for (int e = tid; e < 2 * K * K; e += RK_THREADS) {
@@ -211,10 +212,7 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
         }
         rank_s = r;
     }
-    for (int e = tid; e < a.rmax * K; e += RK_THREADS) {
-        a.TA[e] = 0.0;
-        a.TB[e] = 0.0;
-    }
+    for (int e = tid; e < 2 * RK_R * RK_K; e += RK_THREADS) (&Ts[0][0][0])[e] = 0.0;
     __syncthreads();
     const int r = rank_s;
 
@@ -229,9 +227,13 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
             for (int k = i + 1; k < rx; ++k) v -= L[sd][piv[sd][k]][i] * y[k];
             y[i] = v / L[sd][piv[sd][i]][i];
         }
-        double* T = sd ? a.TB : a.TA;
         const double rs = sqrt(sj);
-        for (int i = 0; i < rx; ++i) T[j * K + piv[sd][i]] = rs * y[i];
+        for (int i = 0; i < rx; ++i) Ts[sd][j][piv[sd][i]] = rs * y[i];
+    }
+    __syncthreads();
+    for (int e = tid; e < a.rmax * K; e += RK_THREADS) {
+        a.TA[e] = Ts[0][e / K][e % K];
+        a.TB[e] = Ts[1][e / K][e % K];
     }
     if (tid == 0) *a.r_out = r;
 }

@@ -21,8 +21,8 @@ Steps, on ``GA = A A^T`` and ``GB = B B^T`` ([K, K]):
    ``W``: ``R ~= (T_A A)^T (T_B B)``.
 
 Nothing here is trusted for accuracy: the Grams square the condition number, so the caller verifies
-the compressed product on the real operands with fixed Gaussian probes (``KnitPipeline``) and takes
-the exact contraction when the check fails. Returns None when there is nothing to compress to
+the compressed product on the real operands against fixed Gaussian probes (``qk_probe_errors``,
+``KnitPipeline``) and takes the exact contraction when the check fails. Returns None when there is nothing to compress to
 (``R = 0``, the pivoting did not converge in ``rc_max`` steps, or ``r > rmax``).
 """
 from __future__ import annotations

@@ -722,6 +722,100 @@ def rank_factors_device(ctx: Context, GA, GB, rmax: int = 8, out=None):
     return TA, TB, r
 
 
+PREP_COLS = 128  # qk_prep_operands: column counts must be multiples of this
+N_PROBES = 16    # probes of the data-rank acceptance check (qk_probe_errors)
+_PREP_WORK: dict = {}
+
+
+def prep_ok(K: int, NA: int, NB: int) -> bool:
+    """Whether qk_prep_operands takes these operand shapes (even K <= 64, column counts % 128)."""
+    return 2 <= K <= 64 and K % 2 == 0 and NA >= PREP_COLS and NB >= PREP_COLS and NA % PREP_COLS == 0 and NB % PREP_COLS == 0
+
+
+def prep_operands(ctx: Context, WtA, qA, WtB, qB, probes, out=None):
+    """``qk_prep_operands``: ``(XA, XB, G, U)`` — the two light-cone operands ``X = Wt^T q`` ([K, N]
+    each), their Grams stacked ``G = [XA XA^T, XB XB^T]`` ([2, K, K]) and ``U = XB probes^T`` ([K, 16]),
+    in one pass over the swept rows (plus a fixed-order reduction of per-workgroup partials)."""
+    T = torch()
+    RA, K = WtA.shape
+    RB, K2 = WtB.shape
+    assert K == K2 and qA.shape[0] == RA and qB.shape[0] == RB and probes.shape[0] == N_PROBES
+    NA, NB = qA.shape[1], qB.shape[1]
+    assert probes.shape[1] == NB and all(t.is_contiguous() for t in (WtA, qA, WtB, qB, probes))
+    dev = qA.device
+    if out is None:
+        out = (T.empty((K, NA), dtype=T.float64, device=dev), T.empty((K, NB), dtype=T.float64, device=dev),
+               T.empty((2, K, K), dtype=T.float64, device=dev), T.empty((K, N_PROBES), dtype=T.float64, device=dev))
+    XA, XB, G, U = out
+    need = ctypes.c_int64()
+    ctx.check(ctx.lib.qk_prep_workspace_bytes(ctx.handle, NA, NB, ctypes.byref(need)), "qk_prep_workspace_bytes")
+    key = (str(dev), T.cuda.current_stream(dev).cuda_stream)
+    work = _PREP_WORK.get(key)
+    if work is None or work.numel() * 8 < need.value:
+        work = _PREP_WORK[key] = T.empty(max(need.value // 8, 1), dtype=T.float64, device=dev)
+    ctx.check(ctx.lib.qk_prep_operands(ctx.handle, K, RA, WtA.data_ptr(), qA.data_ptr(), NA, NA, XA.data_ptr(),
+                                       RB, WtB.data_ptr(), qB.data_ptr(), NB, NB, XB.data_ptr(), probes.data_ptr(),
+                                       G[0].data_ptr(), G[1].data_ptr(), U.data_ptr(), work.data_ptr(),
+                                       work.numel() * 8), "qk_prep_operands")
+    return XA, XB, G, U
+
+
+def compress_operands(ctx: Context, TA, XA, TB, XB):
+    """``qk_compress_operands``: ``(TA XA, TB XB)`` ([rmax, N] each) in one launch."""
+    T = torch()
+    rmax, K = TA.shape
+    assert TB.shape == (rmax, K) and XA.shape[0] == K and XB.shape[0] == K
+    A2 = T.empty((rmax, XA.shape[1]), dtype=T.float64, device=XA.device)
+    B2 = T.empty((rmax, XB.shape[1]), dtype=T.float64, device=XB.device)
+    ctx.check(ctx.lib.qk_compress_operands(ctx.handle, K, rmax, TA.data_ptr(), XA.data_ptr(), XA.shape[1],
+                                           A2.data_ptr(), TB.data_ptr(), XB.data_ptr(), XB.shape[1], B2.data_ptr()),
+              "qk_compress_operands")
+    return A2, B2
+
+
+_PROBE_WORK: dict = {}
+
+
+def probe_errors(ctx: Context, XA, A2, U, B2, probes, r=None, tol: float = 0.0, a2_cols: tuple | None = None):
+    """``qk_probe_errors``: squared probe errors ``e2`` ([16]) of the compressed knit over the columns of
+    ``XA`` ([K, NA]); ``A2`` ([rmax, *]) holds those columns at ``a2_cols = (offset, count)`` of its rows
+    (default: all). ``U = XB probes^T`` and ``B2`` / ``probes`` span all of B's columns. With ``r`` (device
+    int32 [1]) also the accepted rank ``k`` and the error: returns ``(e2, k, err)``, else ``(e2, None, None)``."""
+    T = torch()
+    K, NA = XA.shape
+    rmax = A2.shape[0]
+    NB = B2.shape[1]
+    assert U.shape == (K, N_PROBES) and probes.shape == (N_PROBES, NB) and B2.shape[0] == rmax
+    assert all(t.is_contiguous() for t in (XA, A2, U, B2, probes))
+    off = 0 if a2_cols is None else a2_cols[0]
+    assert (a2_cols is None and A2.shape[1] == NA) or (a2_cols is not None and a2_cols[1] == NA)
+    dev = XA.device
+    need = ctypes.c_int64()
+    ctx.check(ctx.lib.qk_probe_workspace_bytes(ctx.handle, NA, ctypes.byref(need)), "qk_probe_workspace_bytes")
+    key = (str(dev), T.cuda.current_stream(dev).cuda_stream)
+    work = _PROBE_WORK.get(key)
+    if work is None or work.numel() * 8 < need.value:
+        work = _PROBE_WORK[key] = T.empty(max(need.value // 8, 1), dtype=T.float64, device=dev)
+    e2 = T.empty(N_PROBES, dtype=T.float64, device=dev)
+    k = T.empty(1, dtype=T.int32, device=dev) if r is not None else None
+    err = T.empty(1, dtype=T.float64, device=dev) if r is not None else None
+    ctx.check(ctx.lib.qk_probe_errors(ctx.handle, K, rmax, XA.data_ptr(), NA, NA, A2.data_ptr() + 8 * off,
+                                      A2.shape[1], U.data_ptr(), B2.data_ptr(), NB, NB, probes.data_ptr(), NB,
+                                      e2.data_ptr(), _ptr(r), tol, _ptr(k), _ptr(err), work.data_ptr(),
+                                      work.numel() * 8), "qk_probe_errors")
+    return e2, k, err
+
+
+def probe_accept(ctx: Context, e2, r, tol: float):
+    """``qk_probe_accept``: ``(k, err)`` from summed squared probe errors ``e2`` ([16])."""
+    T = torch()
+    k = T.empty(1, dtype=T.int32, device=e2.device)
+    err = T.empty(1, dtype=T.float64, device=e2.device)
+    ctx.check(ctx.lib.qk_probe_accept(ctx.handle, e2.data_ptr(), 1, r.data_ptr(), tol, k.data_ptr(), err.data_ptr()),
+              "qk_probe_accept")
+    return k, err
+
+
 def _endpoints(virt, j):
     out = [None, None]
     for instr in virt.circuit:

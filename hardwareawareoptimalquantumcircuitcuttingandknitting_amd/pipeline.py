@@ -227,6 +227,18 @@ class HipBackend:
     def rank_factors(self, GA, GB):
         return engine.rank_factors_device(self.ctx, GA, GB)
 
+    def prep_operands(self, WtA, qA, WtB, qB, probes):
+        return engine.prep_operands(self.ctx, WtA, qA, WtB, qB, probes)
+
+    def probe_errors(self, XA, A2, U, B2, probes, r=None, tol=0.0, a2_cols=None):
+        return engine.probe_errors(self.ctx, XA, A2, U, B2, probes, r=r, tol=tol, a2_cols=a2_cols)
+
+    def probe_accept(self, e2, r, tol):
+        return engine.probe_accept(self.ctx, e2, r, tol)
+
+    def compress(self, TA, XA, TB, XB):
+        return engine.compress_operands(self.ctx, TA, XA, TB, XB)
+
     def event(self):
         return self.T.cuda.Event(enable_timing=True)
 
@@ -297,6 +309,7 @@ class KnitPipeline:
                              and hasattr(self.be, "rank_factors"))
         self._pending = []  # device (rank, accepted) of steps not yet read back
         self.last_kernel = None  # kernel of the last compressed contraction (None: qk_gemm_keyed)
+        self.last_prep = None  # data-rank preparation of the last step: "fused" (qk_prep_operands) or "torch"
         self._probe = None
         self._pinned = None  # host staging of the two Gram matrices (pinned on a GPU)
         self._prep_stream = None
@@ -601,13 +614,18 @@ class KnitPipeline:
         return self._probe
 
     def knit(self, qs: list):
+        if self.dev_rank and self.mode in ("single", "slice"):
+            if self.out is None:
+                self.out = self._alloc_out(None)
+            if self.mode == "slice":
+                return self._launch_slice(self._prep_slice(qs))
+            return self._launch_dev_rank(self._prep_dev_rank(qs))
         mats = self.operands(qs)
         if self.out is None:
             self.out = self._alloc_out(mats)
         if self.mode == "slice":
-            return self._knit_slice(mats)
-        if self.dev_rank and self.mode == "single":
-            return self._knit_dev_rank(mats)
+            ia, ib = self.order[0], self.order[-1]
+            return self._slice_exact(mats[ia], mats[ib], self.ops.clbits[ia], self.ops.clbits[ib])
         low = self._rank_compress(mats) if self.data_rank else None
         if self.record_events:
             start, end = self.be.event(), self.be.event()
@@ -635,6 +653,29 @@ class KnitPipeline:
             dist.reduce(res, dst=0, group=self.group)
         return res
 
+    def _fused_prep(self, qs) -> bool:
+        """Whether the data-rank step takes the fused device preparation (qk_prep_operands ->
+        qk_rank_factors -> qk_compress_operands -> qk_probe_errors): factored transforms on both sides, a backend
+        with those kernels, and operand shapes they take."""
+        ia, ib = self.order[0], self.order[-1]
+        if not hasattr(self.be, "prep_operands") or self.transforms[ia] is None or self.transforms[ib] is None:
+            return False
+        K = self.transforms[ia].shape[1]
+        return (self.transforms[ib].shape[1] == K and self.transforms[ia].shape[0] == qs[ia].shape[0]
+                and self.transforms[ib].shape[0] == qs[ib].shape[0]
+                and engine.prep_ok(K, qs[ia].shape[1], qs[ib].shape[1]))
+
+    def _prep_fused(self, qs, probes):
+        """(mats, G, U): light-cone operands of the two sides, their Grams [2, K, K] and the B side
+        against the probes [K, 16], from one qk_prep_operands call."""
+        ia, ib = self.order[0], self.order[-1]
+        XA, XB, G, U = self.be.prep_operands(self.transforms[ia], qs[ia].contiguous(), self.transforms[ib],
+                                             qs[ib].contiguous(), probes)
+        mats = [None] * len(qs)
+        mats[ia], mats[ib] = XA, XB
+        self.last_prep = "fused"
+        return mats, G, U
+
     def _accept(self, A, B, A2, B2, x, r, ref_rows=None, cmp_rows=None, reduce_err=None):
         """Device-side probe check of a compressed knit: ``(k_eff, err)``, ``k_eff`` = the rank when
         every probe's ``||(A^T B - A2^T B2) x||_2 <= rank_tol`` (see ``__init__``), else 0."""
@@ -650,14 +691,23 @@ class KnitPipeline:
         self._pending.append((r, k_eff))
         return k_eff, err
 
-    def _knit_dev_rank(self, mats):
-        """Single GPU, device data rank: Grams -> qk_rank_factors -> compressed operands -> probe
-        check -> streaming knit with the accepted rank (k_eff) and the exact contraction predicated
-        on k_eff == 0. Nothing waits for the host; ``sync_stats`` reads ranks / fallbacks later."""
-        return self._launch_dev_rank(self._prep_dev_rank(mats))
-
-    def _prep_dev_rank(self, mats) -> dict:
+    def _prep_dev_rank(self, qs) -> dict:
+        """Single GPU, device data rank: operands + Grams + probe products (one fused launch where
+        the shapes allow, else the transforms and torch products), qk_rank_factors with its
+        acceptance check, compressed operands. Nothing waits for the host; ``sync_stats`` reads
+        ranks / fallbacks later. The write (``_launch_dev_rank``) runs with the accepted rank and
+        the exact contraction is predicated on it being 0."""
         ia, ib = self.order[0], self.order[-1]
+        if self._fused_prep(qs):
+            x = self._probes(qs[ib].shape[1], qs[ib].device)
+            mats, G, U = self._prep_fused(qs, x)
+            TA, TB, r = self.be.rank_factors(G[0], G[1])
+            A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib])
+            _, k_eff, _ = self.be.probe_errors(mats[ia], A2, U, B2, x, r=r, tol=self.rank_tol)
+            self._pending.append((r, k_eff))
+            return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
+        mats = self.operands(qs)
+        self.last_prep = "torch"
         A, B = mats[ia], mats[ib]
         G = self.T.stack([_mm_nt(A, A), _mm_nt(B, B)])
         TA, TB, r = self.be.rank_factors(G[0].contiguous(), G[1].contiguous())
@@ -678,58 +728,78 @@ class KnitPipeline:
             self.events.append((start, end))
         return self._contract(p["mats"], skip=p["k_eff"])  # exact path: runs only if the check rejected
 
-    def _knit_slice(self, mats):
-        """Slice mode (multi-GPU): this rank writes the contiguous outputs ``self.slice`` of the
-        reference-ordered distribution. ``mats`` are this rank's column blocks of the two operands
-        (the sweep's all_to_all delivered every instance row of one column block per fragment).
-        Collectives: one all_reduce (the two Grams + B x for the probes), one broadcast of the
-        factors (rank 0's, so every rank knits with the same ones), one all_gather of the compressed
-        column blocks (8 x 2^m per fragment), one all_reduce of the probe errors; the write itself
-        is local. A rejected compression (read back after the knit is queued) falls back to the
-        exact contraction of the slice from all-gathered operands."""
-        ia, ib = self.order[0], self.order[-1]
-        if not self.dev_rank:
-            return self._slice_exact(mats[ia], mats[ib], self.ops.clbits[ia], self.ops.clbits[ib])
-        return self._launch_slice(self._prep_slice(mats))
-
-    def _prep_slice(self, mats) -> dict:
+    def _prep_slice(self, qs) -> dict:
+        """Slice mode (multi-GPU), the preparation of this rank's write: ``qs`` hold every instance
+        row of this rank's column block of each operand (the sweep's all_to_all). Collectives: one
+        all_reduce (the two Grams + the B side against the probes), one broadcast of rank 0's
+        factors and accepted rank (every rank knits with identical ones), one all_gather of the
+        compressed column blocks (rmax x 2^m per fragment); the write itself is local. A rejected
+        compression (read back after the write is queued) falls back to the exact contraction of
+        the slice from all-gathered operands."""
         import torch.distributed as dist
 
         T, be, P = self.T, self.be, self.world
         ia, ib = self.order[0], self.order[-1]
-        XA, XB = mats[ia], mats[ib]  # [K, wA / P], [K, wB / P]
-        K = XA.shape[0]
-        bwA, bwB = XA.shape[1], XB.shape[1]
-        x_full = self._probes(bwB * P, XB.device)  # [N_PROBES, wB]
+        bwA, bwB = qs[ia].shape[1], qs[ib].shape[1]
+        x_full = self._probes(bwB * P, qs[ib].device)  # [N_PROBES, wB]
         x = x_full[:, self.rank * bwB:(self.rank + 1) * bwB].contiguous()
         npr = self.N_PROBES
-        red = T.cat([_mm_nt(XA, XA).reshape(-1), _mm_nt(XB, XB).reshape(-1), _mm_nt(XB, x).reshape(-1)])
-        dist.all_reduce(red, group=self.group)
-        GA = red[:K * K].view(K, K).contiguous()
-        GB = red[K * K:2 * K * K].view(K, K).contiguous()
-        Bx = red[2 * K * K:].view(K, npr)
-        TA, TB, r = be.rank_factors(GA, GB)
-        R8 = TA.shape[0]
-        fac = T.cat([TA.reshape(-1), TB.reshape(-1), r.to(T.float64)])
-        dist.broadcast(fac, src=self._group_rank0(), group=self.group)
-        TA = fac[:R8 * K].view(R8, K)
-        TB = fac[R8 * K:2 * R8 * K].view(R8, K)
-        r = fac[-1:].to(T.int32)
-        loc = T.cat([(TA @ XA).reshape(-1), (TB @ XB).reshape(-1)])
+        if self._fused_prep(qs):
+            mats, G, U = self._prep_fused(qs, x)
+            XA, XB = mats[ia], mats[ib]
+            K = XA.shape[0]
+            red = T.cat([G.reshape(-1), U.reshape(-1)])
+            dist.all_reduce(red, group=self.group)
+            G = red[:2 * K * K].view(2, K, K)
+            U = red[2 * K * K:].view(K, npr).contiguous()
+            TA, TB, r = be.rank_factors(G[0].contiguous(), G[1].contiguous())
+            R8 = TA.shape[0]
+            fac = T.cat([TA.reshape(-1), TB.reshape(-1), r.to(T.float64)])
+            dist.broadcast(fac, src=self._group_rank0(), group=self.group)
+            TA = fac[:R8 * K].view(R8, K)
+            TB = fac[R8 * K:2 * R8 * K].view(R8, K)
+            r = fac[-1:].to(T.int32)
+            A2l, B2l = be.compress(TA.contiguous(), XA, TB.contiguous(), XB)
+            loc = T.cat([A2l.reshape(-1), B2l.reshape(-1)])
+        else:
+            mats = self.operands(qs)
+            self.last_prep = "torch"
+            XA, XB = mats[ia], mats[ib]  # [K, wA / P], [K, wB / P]
+            K = XA.shape[0]
+            red = T.cat([_mm_nt(XA, XA).reshape(-1), _mm_nt(XB, XB).reshape(-1), _mm_nt(XB, x).reshape(-1)])
+            dist.all_reduce(red, group=self.group)
+            GA = red[:K * K].view(K, K).contiguous()
+            GB = red[K * K:2 * K * K].view(K, K).contiguous()
+            Bx = red[2 * K * K:].view(K, npr)
+            TA, TB, r = be.rank_factors(GA, GB)
+            R8 = TA.shape[0]
+            fac = T.cat([TA.reshape(-1), TB.reshape(-1), r.to(T.float64)])
+            dist.broadcast(fac, src=self._group_rank0(), group=self.group)
+            TA = fac[:R8 * K].view(R8, K)
+            TB = fac[R8 * K:2 * R8 * K].view(R8, K)
+            r = fac[-1:].to(T.int32)
+            loc = T.cat([(TA @ XA).reshape(-1), (TB @ XB).reshape(-1)])
         gat = T.empty(P * loc.numel(), dtype=loc.dtype, device=loc.device)
         dist.all_gather_into_tensor(gat, loc, group=self.group)
         gat = gat.view(P, loc.numel())
         A2 = gat[:, :R8 * bwA].view(P, R8, bwA).permute(1, 0, 2).reshape(R8, P * bwA).contiguous()
         B2 = gat[:, R8 * bwA:].view(P, R8, bwB).permute(1, 0, 2).reshape(R8, P * bwB).contiguous()
-        # rows of R in this rank's A column block, against all probes
-        ref_rows = XA.T @ Bx
-        cmp_rows = A2[:, self.rank * bwA:(self.rank + 1) * bwA].T @ _mm_nt(B2, x_full)
-
-        def reduce_err(e2):
+        if self._fused_prep(qs):
+            # this rank's A columns against all probes (B2 / probes: every column), summed over ranks
+            e2, _, _ = be.probe_errors(XA, A2, U, B2, x_full.contiguous(), a2_cols=(self.rank * bwA, bwA))
             dist.all_reduce(e2, group=self.group)
-            return e2
+            k_eff, _ = be.probe_accept(e2, r, self.rank_tol)
+            self._pending.append((r, k_eff))
+        else:
+            # rows of R in this rank's A column block, against all probes
+            ref_rows = XA.T @ Bx
+            cmp_rows = A2[:, self.rank * bwA:(self.rank + 1) * bwA].T @ _mm_nt(B2, x_full)
 
-        k_eff, _ = self._accept(None, None, None, None, None, r, ref_rows, cmp_rows, reduce_err)
+            def reduce_err(e2):
+                dist.all_reduce(e2, group=self.group)
+                return e2
+
+            k_eff, _ = self._accept(None, None, None, None, None, r, ref_rows, cmp_rows, reduce_err)
         on_gpu = k_eff.device.type == "cuda"
         pinned = T.empty(1, dtype=T.int32, pin_memory=on_gpu)
         pinned.copy_(k_eff, non_blocking=on_gpu)
@@ -804,6 +874,11 @@ class KnitPipeline:
         stream (in order). The caller's stream waits for the write before the step returns."""
         T, be = self.T, self.be
         main = T.cuda.current_stream()
+        if main.cuda_stream == 0:
+            # the CU-masked streams are blocking streams: anything queued on the legacy null stream
+            # (here: the caller's wait for the write) would order the next step's preparation behind
+            # this step's write and undo the overlap
+            raise ValueError("pipelined steps need a non-default current stream (torch.cuda.stream(...))")
         S, W = self._overlap_streams()
         W = W if W is not None else main
         with T.cuda.stream(S):
@@ -815,10 +890,9 @@ class KnitPipeline:
             if self.record_events:
                 s1.record()
                 self.sweep_events.append((s0, s1))
-            mats = self.operands(qs)
             if self.out is None:
-                self.out = self._alloc_out(mats)
-            p = self._prep_slice(mats) if self.mode == "slice" else self._prep_dev_rank(mats)
+                self.out = self._alloc_out(None)
+            p = self._prep_slice(qs) if self.mode == "slice" else self._prep_dev_rank(qs)
             done = T.cuda.Event(enable_timing=self.record_events)
             done.record(S)
         if self.record_events:
@@ -829,7 +903,8 @@ class KnitPipeline:
             for k in ("A2", "B2", "k_eff"):
                 p[k].record_stream(W)
             for m in p["mats"]:
-                m.record_stream(W)
+                if m is not None:
+                    m.record_stream(W)
             out = self._launch_slice(p) if self.mode == "slice" else self._launch_dev_rank(p)
         if W is not main:
             main.wait_stream(W)

@@ -241,6 +241,35 @@ int qk_knit(qk_ctx* ctx, const qk_knit_plan* plan, const double* const* q, void*
 int qk_rank_factors(qk_ctx* ctx, int64_t K, const double* GA, const double* GB, double lam_tol, double s_tol,
                     double s_abs, int rmax, double* TA, double* TB, int32_t* r_out);
 
+/* Operand preparation of the data-rank step in one pass over the swept rows (csrc/qknit_prep.hip):
+ *   X_A = Wt_A^T q_A ([K][NA]), X_B = Wt_B^T q_B ([K][NB]) (Wt: [R][K], q: [R][ldq] row-major),
+ *   GA = X_A X_A^T, GB = X_B X_B^T ([K][K]), U = X_B P^T ([K][16], P = probes [16][NB]).
+ * K <= 64; NA, NB positive multiples of 128. work: qk_prep_workspace_bytes (per-workgroup partial
+ * sums, reduced in a fixed order: results are deterministic). All pointers DEVICE. */
+int qk_prep_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes);
+int qk_prep_operands(qk_ctx* ctx, int K, int RA, const double* WtA, const double* qA, int64_t ldqA, int64_t NA,
+                     double* XA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB, double* XB,
+                     const double* probes, double* GA, double* GB, double* U, double* work, int64_t work_bytes);
+
+/* A2 = TA X_A ([rmax][NA]), B2 = TB X_B ([rmax][NB]) for [rmax][K] factors (rmax <= 8), one launch. */
+int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, double* A2,
+                         const double* TB, const double* XB, int64_t NB, double* B2);
+
+/* Acceptance check of a compressed knit on the real operands (the probe products of the torch form,
+ * not materialised): e2[p] = ||(X_A^T X_B - A2^T B2) P_p||^2 summed over the NA columns of X_A given
+ * (X_A: [K][ldx], A2: [rmax][lda2] the same columns; U = X_B P^T [K][16] over ALL columns of X_B; B2:
+ * [rmax][ldb2] and P: [16][ldp] over all NB columns). With k_out: *err_out = sqrt(max_p e2[p]) and
+ * *k_out = (*r_dev > 0 && err <= tol) ? *r_dev : 0 (the accepted rank; 0 = exact contraction).
+ * qk_probe_accept does that last step on e2 rows summed elsewhere (multi-GPU: all-reduced partial
+ * e2 of each rank's columns; n rows of 16). e2 / r_dev / k_out / err_out: DEVICE. */
+int qk_probe_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t* bytes);
+int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx, int64_t NA, const double* A2,
+                    int64_t lda2, const double* U, const double* B2, int64_t ldb2, int64_t NB, const double* probes,
+                    int64_t ldp, double* e2, const int32_t* r_dev, double tol, int32_t* k_out, double* err_out,
+                    double* work, int64_t work_bytes);
+int qk_probe_accept(qk_ctx* ctx, const double* e2, int n, const int32_t* r_dev, double tol, int32_t* k_out,
+                    double* err_out);
+
 /* ---- post-processing (reference-shaped results; quasi_distr.py:3-43, run.py:71) ---------- */
 
 /* Workspace for qk_threshold_count / qk_npd over n dense values with `count` kept entries. */

@@ -111,6 +111,29 @@ class CpuBackend:
             TA[:r], TB[:r] = torch.from_numpy(f[0]), torch.from_numpy(f[1])
         return TA, TB, torch.tensor([r], dtype=torch.int32)
 
+    def prep_operands(self, WtA, qA, WtB, qB, probes):
+        """qk_prep_operands' contract: (XA, XB, [GA, GB], U = XB probes^T)."""
+        XA, XB = WtA.T @ qA, WtB.T @ qB
+        return XA, XB, torch.stack([XA @ XA.T, XB @ XB.T]), XB @ probes.T
+
+    def probe_errors(self, XA, A2, U, B2, probes, r=None, tol=0.0, a2_cols=None):
+        """qk_probe_errors' contract: squared probe errors over XA's columns (+ accepted rank)."""
+        A2c = A2 if a2_cols is None else A2[:, a2_cols[0]:a2_cols[0] + a2_cols[1]]
+        d = XA.T @ U - A2c.T @ (B2 @ probes.T)
+        e2 = (d * d).sum(dim=0)
+        if r is None:
+            return e2, None, None
+        k, err = self.probe_accept(e2, r, tol)
+        return e2, k, err
+
+    def probe_accept(self, e2, r, tol):
+        err = float(e2.max().sqrt())
+        rv = int(r.reshape(-1)[0])
+        return torch.tensor([rv if rv > 0 and err <= tol else 0], dtype=torch.int32), torch.tensor([err])
+
+    def compress(self, TA, XA, TB, XB):
+        return (TA @ XA).contiguous(), (TB @ XB).contiguous()
+
     def khatri_rao(self, A, B):
         K = A.shape[0]
         return torch.stack([torch.outer(B[k], A[k]).reshape(-1) for k in range(K)])

@@ -132,7 +132,8 @@ def _slice_worker(rank, world, port, case, data_rank, q):
             outs.append(torch.cat(parts).numpy())
         pipe.sync_stats()
         if rank == 0:
-            q.put((outs, pipe.slice, pipe.last_rank, pipe.rank_fallbacks, pipe.rank_incompressible, pipe.dev_rank))
+            q.put((outs, pipe.slice, pipe.last_rank, pipe.rank_fallbacks, pipe.rank_incompressible, pipe.dev_rank,
+                   pipe.last_prep))
     finally:
         dist.destroy_process_group()
 
@@ -163,7 +164,7 @@ def test_slice_mode_matches_oracle(case, world, data_rank):
     procs = [ctx.Process(target=_slice_worker, args=(r, world, port, case, data_rank, q)) for r in range(world)]
     for p in procs:
         p.start()
-    outs, sl, last_rank, fallbacks, incompressible, dev = q.get(timeout=300)
+    outs, sl, last_rank, fallbacks, incompressible, dev, prep = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -178,6 +179,8 @@ def test_slice_mode_matches_oracle(case, world, data_rank):
         assert dev and last_rank is not None and incompressible == 0
     if case == "cx_8x8":
         assert incompressible == 2 and last_rank is None
+    if data_rank:  # 128-column blocks take the fused preparation (qk_prep_operands' contract), others torch
+        assert prep == ("fused" if (case, world) in (("hwe_p2", 2), ("cx_8x8", 2)) else "torch")
 
 
 def _api_worker(rank, world, port, case, q):

@@ -690,6 +690,83 @@ def test_rank_factors_device_matches_host(T, K, ra, rb, r):
     assert np.abs(Rh - R).max() <= 1e-9 * scale
 
 
+@pytest.mark.parametrize("K,RA,RB,NA,NB", [(64, 64, 256, 65536, 65536), (64, 37, 130, 1024, 2048), (6, 4, 9, 128, 256),
+                                           (64, 256, 64, 128, 8192)])
+def test_prep_operands_matches_torch(T, K, RA, RB, NA, NB):
+    """qk_prep_operands (one pass: X = Wt^T q on MFMA, per-workgroup Gram / probe partials, fixed-order
+    reduction) against torch fp64: X, the two Grams and U = X_B P^T (relative 1e-13 of the norms).
+    Shapes: syc 32 5's two sides, ragged instance-row counts, K < 16, more tiles on one side; an odd K
+    (rows staged 16 B at a time) is refused."""
+    ctx = engine.get_context(0)
+    g = T.Generator(device="cuda").manual_seed(K + RA + RB)
+    WtA = T.randn(RA, K, dtype=T.float64, device="cuda", generator=g)
+    WtB = T.randn(RB, K, dtype=T.float64, device="cuda", generator=g)
+    qA = T.randn(RA, NA, dtype=T.float64, device="cuda", generator=g)
+    qB = T.randn(RB, NB, dtype=T.float64, device="cuda", generator=g)
+    P = T.randn(16, NB, dtype=T.float64, device="cuda", generator=g)
+    XA, XB, G, U = engine.prep_operands(ctx, WtA, qA, WtB, qB, P)
+    T.cuda.synchronize()
+    rXA, rXB = WtA.T @ qA, WtB.T @ qB
+    close = lambda a, b: float((a - b).abs().max()) <= 1e-13 * max(float(b.abs().max()), 1.0) * 64  # noqa: E731
+    assert close(XA, rXA) and close(XB, rXB)
+    assert close(G[0], rXA @ rXA.T) and close(G[1], rXB @ rXB.T)
+    assert close(U, rXB @ P.T)
+    XA2, XB2, G2, U2 = engine.prep_operands(ctx, WtA, qA, WtB, qB, P)
+    T.cuda.synchronize()
+    assert T.equal(G, G2) and T.equal(U, U2) and T.equal(XB, XB2)  # deterministic
+    if K == 6:
+        assert not engine.prep_ok(5, NA, NB)
+        with pytest.raises(engine._lib.QknitError):
+            engine.prep_operands(ctx, WtA[:, :5].contiguous(), qA, WtB[:, :5].contiguous(), qB, P)
+
+
+@pytest.mark.parametrize("K,ra,rb,r,noise", [(64, 8, 8, 2, 0.0), (64, 5, 12, 4, 0.0), (64, 20, 20, 8, 0.0),
+                                             (64, 8, 8, 2, 1e-9), (24, 3, 3, 3, 0.0)])
+def test_probe_check_and_compress(T, K, ra, rb, r, noise):
+    """qk_compress_operands (A'' = T_A A, B'' = T_B B) and qk_probe_errors / qk_probe_accept (the
+    acceptance check on the real operands without materialising the probe products) against torch:
+    the probe errors ||(A^T B - A''^T B'') p_j|| within the fp64 floor of the two products (1e-13 of
+    their norm),
+    exact low-rank data accepted (k = r), a rank-2 product plus 1e-9 noise rejected (k = 0). Also the
+    column-block form of the multi-GPU path: e2 over two halves of A's columns sums to the whole."""
+    ctx = engine.get_context(0)
+    rng = np.random.default_rng(K + ra + rb + r)
+    M, N = 3072, 2048
+    core = rng.standard_normal((ra, r)) @ rng.standard_normal((r, rb))
+    PA = rng.standard_normal((K, ra))
+    PB = np.linalg.pinv(PA.T) @ core
+    A = PA @ rng.standard_normal((ra, M))
+    B = PB @ rng.standard_normal((rb, N)) + noise * rng.standard_normal((K, N))
+    At, Bt = T.from_numpy(A).cuda(), T.from_numpy(B).cuda()
+    x = T.from_numpy(np.random.default_rng(1234).standard_normal((16, N))).cuda()
+    GA, GB, U = (At @ At.T).contiguous(), (Bt @ Bt.T).contiguous(), (Bt @ x.T).contiguous()
+    TA, TB, rd = engine.rank_factors_device(ctx, GA, GB)
+    A2, B2 = engine.compress_operands(ctx, TA, At, TB, Bt)
+    T.cuda.synchronize()
+    got_r = int(rd.item())
+    assert got_r == r if noise == 0.0 else 0 < got_r <= 8
+    assert float((A2 - TA @ At).abs().max()) <= 1e-12 * float((TA @ At).abs().max())
+    assert float((B2 - TB @ Bt).abs().max()) <= 1e-12 * float((TB @ Bt).abs().max())
+    ref = ((At.T @ U - A2.T @ (B2 @ x.T)) ** 2).sum(dim=0)
+    tol = 1e-12 * float((At.T @ U).norm(dim=0).max())  # exact data: ~1e-15 of it; the noise: ~1e-9
+    e2, k, err = engine.probe_errors(ctx, At, A2, U, B2, x, r=rd, tol=tol)
+    h = M // 2
+    e2a, _, _ = engine.probe_errors(ctx, At[:, :h].contiguous(), A2, U, B2, x, a2_cols=(0, h))
+    e2b, _, _ = engine.probe_errors(ctx, At[:, h:].contiguous(), A2, U, B2, x, a2_cols=(h, h))
+    k2, _ = engine.probe_accept(ctx, (e2a + e2b).contiguous(), rd, tol)
+    T.cuda.synchronize()
+    # the error norms are differences of products of norm ~|A^T U|: both sides carry 1e-16-relative
+    # rounding of those, so they agree to 1e-13 of |A^T U| (exact data: the norms are that noise)
+    floor = 1e-13 * float((At.T @ U).norm(dim=0).max())
+    assert float((e2.sqrt() - ref.sqrt()).abs().max()) <= floor
+    assert float(((e2a + e2b).sqrt() - e2.sqrt()).abs().max()) <= floor
+    assert abs(float(err.item()) - float(e2.max().sqrt())) <= 1e-12 * float(err.item()) + 1e-300
+    if noise == 0.0:
+        assert int(k.item()) == r and int(k2.item()) == r and float(err.item()) <= tol
+    else:
+        assert int(k.item()) == 0 and int(k2.item()) == 0 and float(err.item()) > tol
+
+
 def test_rank_factors_device_degenerate(T):
     """A zero Gram (R = 0) and a non-PSD garbage Gram give r = 0 and zero factors."""
     ctx = engine.get_context(0)

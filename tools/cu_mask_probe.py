@@ -27,7 +27,7 @@ def main():
     pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
     pipe.step()
     qs = pipe.sweep()
-    prep = pipe._prep_dev_rank(pipe.operands(qs))
+    prep = pipe._prep_dev_rank(qs)
     torch.cuda.synchronize()
     total = engine.device_cu_count(0)
 

@@ -20,8 +20,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="syc_32_5_p2")
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--prep-cus", type=int, nargs="*", default=[32, 64, 0])
+    ap.add_argument("--prep-cus", type=int, nargs="*", default=[32, 48, 64, 0])
     ap.add_argument("--layouts", nargs="*", default=["block"])
+    ap.add_argument("--no-final-plain", action="store_true", help="end with the pipelined runs (timelines)")
     args = ap.parse_args()
     import torch
 
@@ -30,6 +31,7 @@ def main():
 
     name, n, d, p, var = cutting.BASELINE_CONFIGS[args.workload]
     _, cut, _ = cutting.config_cut_circuit(name, n, d, p, var)
+    torch.cuda.set_stream(torch.cuda.Stream())  # pipelined steps need a non-default stream
     pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
     host = {}
 
@@ -44,7 +46,7 @@ def main():
 
         setattr(pipe, name, w)
 
-    for nm in ("sweep", "operands", "_prep_dev_rank", "_launch_dev_rank"):
+    for nm in ("sweep", "_prep_dev_rank", "_launch_dev_rank"):
         wrap(nm)
 
     def stats():
@@ -88,8 +90,9 @@ def main():
         print(json.dumps({"setting": "pipelined", "prep_cus": c, "layout": lay, "cus": pipe.overlap_cus, "ms_per_step": ms,
                           "max_abs_diff_vs_plain": diff, "rank_fallbacks": pipe.rank_fallbacks, "host_ms": host_ms, **stats()}),
               flush=True)
-    pipe.overlap = False
-    print(json.dumps({"setting": "plain (again)", "ms_per_step": run(args.steps)}), flush=True)
+    if not args.no_final_plain:
+        pipe.overlap = False
+        print(json.dumps({"setting": "plain (again)", "ms_per_step": run(args.steps)}), flush=True)
 
 
 if __name__ == "__main__":

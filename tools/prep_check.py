@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Fused data-rank preparation (qk_prep_operands + qk_rank_factors + qk_compress_operands + qk_probe_errors)
+against the torch path on a BASELINE workload: operand / Gram / probe-product differences, the rank,
+the accepted rank and the check's error next to the direct probe error on the real operands.
+
+  python tools/prep_check.py [--workload syc_32_5_p2]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="syc_32_5_p2")
+    args = ap.parse_args()
+    import torch
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline, _mm_nt
+
+    name, n, d, p, var = cutting.BASELINE_CONFIGS[args.workload]
+    _, cut, _ = cutting.config_cut_circuit(name, n, d, p, var)
+    pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
+    ia, ib = pipe.order[0], pipe.order[-1]
+    qs = pipe.sweep()
+    x = pipe._probes(qs[ib].shape[1], qs[ib].device)
+    mats_t = pipe.operands(qs)
+    A, B = mats_t[ia], mats_t[ib]
+    GA, GB, Ut = _mm_nt(A, A), _mm_nt(B, B), _mm_nt(B, x)
+    mats_f, G, U = pipe._prep_fused(qs, x)
+    rel = lambda a, b: float((a - b).abs().max()) / max(float(b.abs().max()), 1e-300)  # noqa: E731
+    out = {"K": A.shape[0], "N": [A.shape[1], B.shape[1]], "rows": [qs[ia].shape[0], qs[ib].shape[0]],
+           "XA_rel": rel(mats_f[ia], A), "XB_rel": rel(mats_f[ib], B), "GA_rel": rel(G[0], GA), "GB_rel": rel(G[1], GB),
+           "U_rel": rel(U, Ut)}
+    TA, TB, r = pipe.be.rank_factors(G[0], G[1])
+    TA0, TB0, r0 = pipe.be.rank_factors(GA.contiguous(), GB.contiguous())
+    A2, B2 = pipe.be.compress(TA, mats_f[ia], TB, mats_f[ib])
+    e2, k, err = pipe.be.probe_errors(mats_f[ia], A2, U, B2, x, r=r, tol=pipe.rank_tol)
+    direct = (A.T @ (B @ x.T) - A2.T @ (B2 @ x.T)).norm(dim=0)
+    rv = int(r.item())
+    host = float(e2.max().sqrt())
+    A20, B20 = TA0 @ A, TB0 @ B
+    direct0 = (A.T @ (B @ x.T) - A20.T @ (B20 @ x.T)).norm(dim=0)
+    out.update({"r": rv, "k_eff": int(k.item()), "err_kernel": float(err.item()), "err_kernel_from_e2": host,
+                "err_direct_max": float(direct.max()), "err_direct": direct.tolist(), "r_torch_path": int(r0.item()),
+                "err_direct_torch_path": float(direct0.max()), "tol": pipe.rank_tol,
+                "R_absmax_sample": float((A[:, :256].T @ B[:, :256]).abs().max())})
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
