@@ -47,9 +47,10 @@ def parse():
     ap.add_argument("--no-npd", action="store_true", help="skip the NPD timing on the 2^N output")
     ap.add_argument("--no-general", action="store_true",
                     help="skip knit_general (the same step without data-rank compression)")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="plain steps only: no pipelining of the next step's sweep + data-rank preparation "
-                         "(CU-masked stream) under the current step's write")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="pipelined steps: the next step's sweep + data-rank preparation on a CU-masked stream "
+                         "under the current step's write (DESIGN.md §4; measured box-dependent, off by default)")
+    ap.add_argument("--no-pipeline", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -457,7 +458,7 @@ def main():
                         light_cone=not args.no_light_cone, data_rank=False if args.no_data_rank else None)
     # pipelined steps (single GPU): step i+1's sweep + data-rank preparation run on a CU-masked stream
     # while step i's write streams on the other CUs; every step still does all of its work
-    pipe.overlap = bool(world == 1 and not args.no_pipeline and pipe.overlap_ok())
+    pipe.overlap = bool(world == 1 and args.pipeline and not args.no_pipeline and pipe.overlap_ok())
     counts = pipe.instance_counts()
 
     def barrier():
