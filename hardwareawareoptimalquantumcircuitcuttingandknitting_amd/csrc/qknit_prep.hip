@@ -58,9 +58,18 @@ struct PrepArgs {
 
 // Stage ring of the transform phase: PRS instance rows of q (128 columns) and of Wt per stage, moved
 // global -> LDS by global_load_lds (16 B per lane, no staging VGPRs); PNS stages in flight per
-// workgroup cover the HBM latency (4 x 28.7 KiB per CU). The ring and the X tile share the LDS.
+// workgroup (2 x 28.7 KiB) and two workgroups per CU cover the HBM latency. The ring and the X tile
+// share the LDS (66.5 KiB per workgroup).
 constexpr int PRS = 16;          // instance rows per stage (4 MFMA k-steps)
-constexpr int PNS = 4;           // stages in flight
+// tools/prep_bench.py, syc 32 5 shapes: 2 stages x 2 workgroups per CU 134 us; 1 workgroup per CU with
+// 3 / 4 / 5 stages 167 / 160 / 160 us (the wider ring does not help: latency hiding needs more waves)
+#ifndef QK_PREP_NS
+#define QK_PREP_NS 2
+#endif
+#ifndef QK_PREP_WG_PER_CU
+#define QK_PREP_WG_PER_CU 2  // 512-thread workgroups per CU (2 needs QK_PREP_NS <= 2: the LDS)
+#endif
+constexpr int PNS = QK_PREP_NS;  // stages in flight
 constexpr int QLD = PCT + 16;    // q stage row stride (doubles): rows 32 banks apart, a k-step's reads conflict-free
 constexpr int WLD = PK + 16;     // Wt stage row stride (same)
 struct PrepStage {
@@ -89,7 +98,7 @@ __device__ __forceinline__ void prep_vmwait(int n) {
     }
 }
 
-__global__ __launch_bounds__(PTH) void qk_prep_operands_kernel(PrepArgs a) {
+__global__ __launch_bounds__(PTH, QK_PREP_WG_PER_CU) void qk_prep_operands_kernel(PrepArgs a) {
     __shared__ __attribute__((aligned(16))) PrepLds L;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, l4 = lane >> 4;
@@ -217,7 +226,13 @@ __global__ __launch_bounds__(256) void qk_prep_reduce_kernel(const double* __res
     double s = 0.0;
     if (sd >= 0) {
         const double* p = part + (int64_t)sd * nblk * PPART + off;
-        for (int b = grp; b < nblk; b += 4) s += p[(int64_t)b * PPART];
+        double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // 8 loads in flight per thread, fixed summation order
+        int b = grp;
+        for (; b + 28 < nblk; b += 32)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] += p[(int64_t)(b + 4 * u) * PPART];
+        for (; b < nblk; b += 4) t[0] += p[(int64_t)b * PPART];
+        s = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
     }
     acc[grp][lane] = s;
     __syncthreads();
@@ -240,11 +255,15 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
     __syncthreads();
     for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < N; c += (int64_t)gridDim.x * 256) {
         double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int k = 0; k < K; ++k) {
-            const double xv = X[(int64_t)k * N + c];
+        for (int k0 = 0; k0 < K; k0 += 16) {  // 16 loads in flight per thread
+            double xv[16];
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j < rmax) acc[j] = fma(T[j][k], xv, acc[j]);
+            for (int u = 0; u < 16; ++u) xv[u] = k0 + u < K ? X[(int64_t)(k0 + u) * N + c] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j < rmax && k0 + u < K) acc[j] = fma(T[j][k0 + u], xv[u], acc[j]);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
@@ -252,7 +271,7 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
     }
 }
 
-constexpr int PV_GRID = 64;  // workgroups of the V = B'' P^T partial sums
+constexpr int PV_GRID = 32;  // workgroups of the V = B'' P^T partial sums
 
 // V partials: vpart[b][j][p] = sum over this workgroup's columns c of B2[j][c] P[p][c] (j < rmax)
 __global__ __launch_bounds__(256) void qk_probe_v_kernel(int rmax, const double* __restrict__ B2, int64_t ldb2,
@@ -261,11 +280,21 @@ __global__ __launch_bounds__(256) void qk_probe_v_kernel(int rmax, const double*
     __shared__ double red[4][256];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, l4 = lane >> 4;
     d4_t acc = {0, 0, 0, 0};
-    for (int64_t c0 = ((int64_t)blockIdx.x * 4 + wave) * 4; c0 < NB; c0 += (int64_t)gridDim.x * 16) {
-        const int64_t c = c0 + l4;
-        const double av = l16 < rmax ? B2[(int64_t)l16 * ldb2 + c] : 0.0;  // A[j][c]
-        const double bv = P[(int64_t)l16 * ldp + c];                       // B[c][p]
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    // this wave's contiguous column range, 8 k-steps (32 columns) per batch, loads issued first
+    const int64_t nw = (int64_t)gridDim.x * 4, w = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t per = ((NB / 4 + nw - 1) / nw) * 4;
+    const int64_t cb = w * per, ce = cb + per < NB ? cb + per : NB;
+    for (int64_t c0 = cb; c0 < ce; c0 += 32) {
+        double av[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t c = c0 + 4 * u + l4;
+            const bool cv = c < ce;
+            av[u] = (cv && l16 < rmax) ? B2[(int64_t)l16 * ldb2 + c] : 0.0;  // A[j][c]
+            bv[u] = cv ? P[(int64_t)l16 * ldp + c] : 0.0;                     // B[c][p]
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
     }
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) red[wave][(l4 + 4 * rr) * 16 + l16] = acc[rr];
@@ -284,9 +313,13 @@ __global__ __launch_bounds__(256) void qk_probe_d_kernel(int K, int rmax, const 
     __shared__ double ep[4][PNP];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, l4 = lane >> 4;
     {
-        double v = 0.0;
-        for (int b = 0; b < gv; ++b) v += vpart[(int64_t)b * 256 + tid];
-        Vs[tid / 16][tid % 16] = -v;  // rows >= rmax are zero sums
+        double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int b = 0;
+        for (; b + 8 <= gv; b += 8)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] += vpart[(int64_t)(b + u) * 256 + tid];
+        for (; b < gv; ++b) t[0] += vpart[(int64_t)b * 256 + tid];
+        Vs[tid / 16][tid % 16] = -(((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7])));
     }
     for (int e = tid; e < PK * PNP; e += 256) Us[e / PNP][e % PNP] = (e / PNP) < K ? U[e] : 0.0;
     __syncthreads();
@@ -356,7 +389,7 @@ int fail(qk_ctx* ctx, int code, const char* msg) {
 
 int prep_grid(qk_ctx* ctx, int64_t NA, int64_t NB) {
     const int64_t tiles = (NA > NB ? NA : NB) / PCT;
-    const int64_t g = ctx->cus > 0 ? ctx->cus : 256;  // one 512-thread workgroup per CU
+    const int64_t g = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * QK_PREP_WG_PER_CU;
     return (int)(tiles < g ? (tiles > 0 ? tiles : 1) : g);
 }
 

@@ -22,6 +22,14 @@ constexpr int RK_R = 8;    // largest rank written (rows of TA / TB)
 constexpr int RK_THREADS = 128;
 constexpr int RK_MAX_SWEEPS = 40;
 
+#ifdef QK_RANK_DEBUG  // tuning builds only (tools/build_variants.py): phase clocks + Jacobi sweep count
+__device__ long long qk_rank_dbg[8];
+#define RK_STAMP(i) \
+    if (threadIdx.x == 0) qk_rank_dbg[i] = wall_clock64();
+#else
+#define RK_STAMP(i)
+#endif
+
 struct RankArgs {
     int K, rmax;
     const double* GA;
@@ -32,9 +40,68 @@ struct RankArgs {
     int32_t* r_out;
 };
 
+// Cross-lane reductions with DPP row operations (a few cycles each) and v_readlane across the four
+// 16-lane rows, instead of ds_bpermute shuffles (~100+ cycles of LDS latency per step, serialised by
+// the reduction's dependency chain: those made a Jacobi round cost ~1.5 us).
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+    int2 w = *reinterpret_cast<int2*>(&v);
+    w.x = __builtin_amdgcn_mov_dpp(w.x, CTRL, 0xF, 0xF, false);
+    w.y = __builtin_amdgcn_mov_dpp(w.y, CTRL, 0xF, 0xF, false);
+    return *reinterpret_cast<double*>(&w);
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    int2 w = *reinterpret_cast<int2*>(&v);
+    w.x = __builtin_amdgcn_readlane(w.x, l);
+    w.y = __builtin_amdgcn_readlane(w.y, l);
+    return *reinterpret_cast<double*>(&w);
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+
+// sum over aligned groups of `width` lanes (1, 2, 4, 8, 16, 32, 64); every lane of a group gets it
 __device__ __forceinline__ double wsum(double v, int width = 64) {
-    for (int o = width >> 1; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (width >= 2) v += dppd<DPP_XOR1>(v);
+    if (width >= 4) v += dppd<DPP_XOR2>(v);
+    if (width >= 8) v += dppd<DPP_HALF_MIRROR>(v);
+    if (width >= 16) v += dppd<DPP_MIRROR>(v);
+    if (width == 32) {
+        const double lo = readlane_d(v, 0) + readlane_d(v, 16), hi = readlane_d(v, 32) + readlane_d(v, 48);
+        v = (threadIdx.x & 32) ? hi : lo;
+    } else if (width == 64) {
+        v = (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+    }
     return v;
+}
+
+// wave-wide argmax of v (lowest index on ties); every lane gets (v, idx)
+__device__ __forceinline__ void wargmax(double& v, int& idx) {
+    auto take = [&](double v2, int i2) {
+        if (v2 > v || (v2 == v && i2 < idx)) {
+            v = v2;
+            idx = i2;
+        }
+    };
+    take(dppd<DPP_XOR1>(v), dppi<DPP_XOR1>(idx));
+    take(dppd<DPP_XOR2>(v), dppi<DPP_XOR2>(idx));
+    take(dppd<DPP_HALF_MIRROR>(v), dppi<DPP_HALF_MIRROR>(idx));
+    take(dppd<DPP_MIRROR>(v), dppi<DPP_MIRROR>(idx));
+    double bv = readlane_d(v, 0);
+    int bi = __builtin_amdgcn_readlane(idx, 0);
+#pragma unroll
+    for (int r = 16; r < 64; r += 16) {
+        const double v2 = readlane_d(v, r);
+        const int i2 = __builtin_amdgcn_readlane(idx, r);
+        if (v2 > bv || (v2 == bv && i2 < bi)) {
+            bv = v2;
+            bi = i2;
+        }
+    }
+    v = bv;
+    idx = bi;
 }
 
 __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a) {
@@ -44,22 +111,47 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
     __shared__ double W[RK_RC][RK_RC + 1];   // right rotations
     __shared__ double Y[2][RK_R][RK_RC];     // triangular-solve results
     __shared__ double sv[RK_RC];
-    __shared__ int piv[2][RK_RC], nsteps[2], conv[2], order[RK_RC], rank_s, rotated;
+    __shared__ int piv[2][RK_RC], nsteps[2], conv[2], order[RK_RC], rank_s, chol_live[2][2];
+    __shared__ double cnorm2;
     __shared__ double Ts[2][RK_R][RK_K];       // T_A, T_B
 
     const int tid = threadIdx.x, lane = tid & 63, side = tid >> 6, K = a.K;
-    for (int e = tid; e < 2 * K * K; e += RK_THREADS) {
-        const int s = e / (K * K), i = (e / K) % K, j = e % K;
-        const double* g = s ? a.GB : a.GA;
-        G[s][i][j] = 0.5 * (g[i * K + j] + g[j * K + i]);
+    RK_STAMP(0)
+    {  // raw copy with 16 loads in flight per thread (a serial load chain cost ~20 us), then symmetrise
+        const int n = 2 * K * K;
+        for (int e0 = tid; e0 < n; e0 += RK_THREADS * 16) {
+            double v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int e = e0 + u * RK_THREADS;
+                v[u] = e < n ? (e < K * K ? a.GA[e] : a.GB[e - K * K]) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int e = e0 + u * RK_THREADS;
+                if (e < n) G[e / (K * K)][(e / K) % K][e % K] = v[u];
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < n; e += RK_THREADS) {
+            const int s = e / (K * K), i = (e / K) % K, j = e % K;
+            if (i < j) {
+                const double m = 0.5 * (G[s][i][j] + G[s][j][i]);
+                G[s][i][j] = m;
+                G[s][j][i] = m;
+            }
+        }
+        __syncthreads();
     }
-    __syncthreads();
 
     // ---- 1. pivoted Cholesky, wave `side` on Gram `side`, lane = row
     double d = lane < K ? G[side][lane][lane] : 0.0;
     bool alive = lane < K;
     double dmax = d;
-    for (int o = 32; o >= 1; o >>= 1) dmax = fmax(dmax, __shfl_xor(dmax, o, 64));
+    {
+        int di = lane;
+        wargmax(dmax, di);
+    }
     bool active = dmax > 0.0, converged = !(dmax > 0.0);
     int steps = 0;
     for (int j = 0; j <= RK_RC; ++j) {  // both waves iterate alike: the barrier below is uniform
@@ -73,14 +165,7 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
             } else {
                 double v = alive ? d : -1.0;
                 int idx = lane;
-                for (int o = 32; o >= 1; o >>= 1) {  // argmax, lowest index on ties
-                    const double v2 = __shfl_xor(v, o, 64);
-                    const int i2 = __shfl_xor(idx, o, 64);
-                    if (v2 > v || (v2 == v && i2 < idx)) {
-                        v = v2;
-                        idx = i2;
-                    }
-                }
+                wargmax(v, idx);  // lowest index on ties
                 const int p = idx;
                 const double dp = v;
                 if (!(dp > 0.0)) {
@@ -100,7 +185,10 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
                 }
             }
         }
+        // both waves leave together once neither is active (double-buffered flags: no read/write race)
+        if (lane == 0) chol_live[j & 1][side] = active ? 1 : 0;
         __syncthreads();
+        if (!chol_live[j & 1][0] && !chol_live[j & 1][1]) break;
     }
     if (lane == 0) {
         nsteps[side] = steps;
@@ -109,6 +197,7 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
     __syncthreads();
     const int ra = nsteps[0], rb = nsteps[1];
     bool ok = conv[0] && conv[1] && ra > 0 && rb > 0;
+    RK_STAMP(1)
 
     // ---- 2. core C = L_A^T L_B, W = I
     if (ok) {
@@ -122,18 +211,29 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
     }
     __syncthreads();
 
-    // ---- 3. one-sided Jacobi on C's columns (round-robin pairs, one thread group per pair)
-    if (ok && rb > 1) {
+    // ---- 3. one-sided Jacobi on C's columns (round-robin pairs, one thread group per pair). Pairs of
+    // columns both below 1e-15 of the largest column norm are left alone: their singular values are
+    // far under the rank cut (s_tol = 1e-13), and rotating rounding noise would keep the sweeps going
+    if (ok && tid == 0) {
+        double m = 0.0;
+        for (int j = 0; j < rb; ++j) {
+            double c2 = 0.0;
+            for (int i = 0; i < ra; ++i) c2 += C[i][j] * C[i][j];
+            m = fmax(m, c2);
+        }
+        cnorm2 = m;
+    }
+    __syncthreads();
+    if (ok && rb > 1 && side == 0) {  // wave 0 alone: rounds are ordered by the wave's own LDS traffic
+        const double floor2 = 1e-30 * cnorm2;
         const int n = rb + (rb & 1), npair = n / 2;
-        int tpp = RK_THREADS / npair;
-        tpp = tpp > 64 ? 64 : tpp;
+        int tpp = 64 / npair;
         int pw = 1;
         while (pw * 2 <= tpp) pw *= 2;
-        tpp = pw;  // power of two, within one wave
-        const int g = tid / tpp, t = tid % tpp;
+        tpp = pw;  // power of two lanes per pair
+        const int g = lane / tpp, t = lane % tpp;
         for (int sweep = 0; sweep < RK_MAX_SWEEPS; ++sweep) {
-            if (tid == 0) rotated = 0;
-            __syncthreads();
+            bool rot = false;
             for (int round = 0; round < n - 1; ++round) {
                 int p = -1, q = -1;
                 if (g < npair) {
@@ -162,7 +262,9 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
                 al = wsum(al, tpp);
                 be = wsum(be, tpp);
                 ga = wsum(ga, tpp);
-                if (live && ga != 0.0 && fabs(ga) > 1e-15 * sqrt(al * be)) {
+                // the factors only need to be good enough for the probe check that follows (1e-13
+                // relative orthogonality instead of 1e-15: fewer sweeps chasing rounding)
+                if (live && ga != 0.0 && fabs(ga) > 1e-13 * sqrt(al * be) && fmax(al, be) > floor2) {
                     const double zeta = (be - al) / (2.0 * ga);
                     const double tt = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
                     const double c = 1.0 / sqrt(1.0 + tt * tt), s = c * tt;
@@ -176,16 +278,21 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
                         W[i][p] = c * wp - s * wq;
                         W[i][q] = s * wp + c * wq;
                     }
-                    if (t == 0) rotated = 1;
+                    rot = true;
                 }
-                __syncthreads();
+                // this round's column writes land before the next round's reads (same wave: LDS is in order)
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
             }
-            const int any = rotated;
-            __syncthreads();
-            if (!any) break;
+#ifdef QK_RANK_DEBUG
+            if (lane == 0) qk_rank_dbg[5] = sweep + 1;
+#endif
+            if (!__any(rot)) break;
         }
     }
+    __syncthreads();
 
+    RK_STAMP(2)
     // ---- 4. singular values (column norms), descending order, rank
     if (ok && tid < rb) {
         double s = 0.0;
@@ -236,9 +343,22 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
         a.TB[e] = Ts[1][e / K][e % K];
     }
     if (tid == 0) *a.r_out = r;
+    RK_STAMP(3)
+#ifdef QK_RANK_DEBUG
+    if (tid == 0) {
+        qk_rank_dbg[6] = ra;
+        qk_rank_dbg[7] = rb;
+    }
+#endif
 }
 
 }  // namespace
+
+#ifdef QK_RANK_DEBUG
+extern "C" int qk_rank_debug(long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(qk_rank_dbg), sizeof(long long) * 8) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int qk_rank_factors(qk_ctx* ctx, int64_t K, const double* GA, const double* GB, double lam_tol,
                                double s_tol, double s_abs, int rmax, double* TA, double* TB, int32_t* r_out) {

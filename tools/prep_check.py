@@ -41,6 +41,10 @@ def main():
     A2, B2 = pipe.be.compress(TA, mats_f[ia], TB, mats_f[ib])
     e2, k, err = pipe.be.probe_errors(mats_f[ia], A2, U, B2, x, r=r, tol=pipe.rank_tol)
     direct = (A.T @ (B @ x.T) - A2.T @ (B2 @ x.T)).norm(dim=0)
+    via_tbu = (mats_f[ia].T @ U - A2.T @ (TB @ U)).norm(dim=0)  # V = T_B U instead of B'' P^T
+    out["err_via_TB_U"] = float(via_tbu.max())
+    out["TB_absmax"] = float(TB.abs().max())
+    out["TA_absmax"] = float(TA.abs().max())
     rv = int(r.item())
     host = float(e2.max().sqrt())
     A20, B20 = TA0 @ A, TB0 @ B
@@ -49,6 +53,15 @@ def main():
                 "err_direct_max": float(direct.max()), "err_direct": direct.tolist(), "r_torch_path": int(r0.item()),
                 "err_direct_torch_path": float(direct0.max()), "tol": pipe.rank_tol,
                 "R_absmax_sample": float((A[:, :256].T @ B[:, :256]).abs().max())})
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import data_rank
+
+    import numpy as np
+
+    Gh = G.cpu().numpy()
+    LA, pa, _ = data_rank.pivoted_cholesky(0.5 * (Gh[0] + Gh[0].T))
+    LB, pb, _ = data_rank.pivoted_cholesky(0.5 * (Gh[1] + Gh[1].T))
+    out.update({"cholesky_steps": [len(pa), len(pb)],
+                "core_singular_values": np.linalg.svd(LA.T @ LB, compute_uv=False)[:12].tolist()})
     print(json.dumps(out), flush=True)
 
 

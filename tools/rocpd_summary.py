@@ -31,14 +31,20 @@ def trace(db: str, top: int):
     return lines
 
 
-def timeline(db: str, last: int):
-    """The last ``last`` kernels in start order: start / end relative to the first of them (us),
+def timeline(db: str, last: int, around: str | None = None):
+    """The last ``last`` kernels in start order (with ``around``: the ``last`` kernels up to and
+    including the last one whose name contains it): start / end relative to the first of them (us),
     duration, queue and stream ids (which kernels overlapped, on which queues)."""
     con = sqlite3.connect(db)
     cols = [d[0] for d in con.execute("select * from kernels limit 1").description]
     extra = [c for c in ("queue_id", "stream_id", "queue", "stream") if c in cols]
     rows = con.execute(f"select name, start, end{''.join(', ' + c for c in extra)} from kernels "
-                       "order by start").fetchall()[-last:]
+                       "order by start").fetchall()
+    if around:
+        hits = [i for i, r in enumerate(rows) if around in r[0]]
+        if hits:
+            rows = rows[:hits[-1] + 1]
+    rows = rows[-last:]
     t0 = rows[0][1] if rows else 0
     lines = [f"columns: {cols}", f"{'start_us':>10s} {'end_us':>10s} {'dur_us':>9s} " + " ".join(f"{c:>9s}" for c in extra)
              + "  kernel"]
@@ -91,6 +97,7 @@ def main():
     tl = sub.add_parser("timeline")
     tl.add_argument("db")
     tl.add_argument("--last", type=int, default=120)
+    tl.add_argument("--around", default=None)
     p = sub.add_parser("pmc")
     p.add_argument("kernel")
     p.add_argument("dbs", nargs="+")
@@ -99,7 +106,7 @@ def main():
         q.add_argument("--out", default=None, help="also write the result here (trace: text, pmc: JSON)")
     a = ap.parse_args()
     if a.cmd in ("trace", "timeline"):
-        lines = trace(a.db, a.top) if a.cmd == "trace" else timeline(a.db, a.last)
+        lines = trace(a.db, a.top) if a.cmd == "trace" else timeline(a.db, a.last, a.around)
         if a.out:
             open(a.out, "w").write("\n".join(lines) + "\n")
     else:
