@@ -268,6 +268,17 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str, device_fn: bool = F
     e(f"const unsigned long long lo = {_deposit('(unsigned long long)tid', list(range(TB - 4)), bitpos[:TB - 4])};")
     e("(void)n_jobs; (void)job_slots; (void)lo; (void)label_off;")
     keep = [i for i in range(PER) if not ((NT * i) & traced)]
+    gids = list(range(int(ps["group_begin"]), int(ps["group_end"])))
+    zero_tile = init and not init_sparse and tpj_log > 0
+    if zero_tile and not final:
+        raise ValueError("SPLIT INIT pass that is not FINAL must be sparse")
+    # direct form: the first group's fiber comes straight from HBM (or the |0..0> start) into registers
+    # and the last group's fiber goes straight to HBM (or into the FINAL pass's per-thread probability
+    # sums, at that fiber's positions): two LDS round trips and two barriers fewer per (job, tile) than
+    # staging the whole tile through LDS at both ends. Not for FINAL passes that trace qubits out (the
+    # trace sums amplitudes across threads) or passes without groups.
+    if gids and not (final and traced):
+        return _pass_body_direct(e, enc, ps, gids, TB, NT, n, m, bitpos, init, final, zero_tile, zero_mask)
     if final:
         e("long long j0 = grp, j1 = grp + 1;")
         e("if (label_off) { j0 = label_off[grp]; j1 = label_off[grp + 1]; }")
@@ -278,7 +289,6 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str, device_fn: bool = F
         e("const long long job = grp;")
     e(f"double2* st = state + job * {1 << n}ll;")
     e("(void)st;")
-    zero_tile = init and not init_sparse and tpj_log > 0
     if init:
         e("lds[swz(tid)] = make_double2((tid == 0 && tbase == 0ull) ? 1.0 : 0.0, 0.0);")
         for i in range(1, PER):
@@ -293,32 +303,17 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str, device_fn: bool = F
                 e(f"lds[swz(tid + {NT * i})] = st[{s}];")
     e("__syncthreads();")
     if zero_tile:
-        if not final:
-            raise ValueError("SPLIT INIT pass that is not FINAL must be sparse")
         e("if (tbase == 0ull) {")
-    for gi in range(int(ps["group_begin"]), int(ps["group_end"])):
-        gr = enc.groups[gi]
-        pos = [int(x) for x in gr["pos"]]
-        nonfib = [p for p in range(TB) if p not in pos]
+    for gi in gids:
+        f = _fiber(enc, gi, TB, bitpos)
         e("{")
-        e(f"const unsigned base = {_deposit('tid', list(range(TB - 4)), nonfib)};", 2)
-        cst = [sum(((r >> k) & 1) << pos[k] for k in range(4)) for r in range(PER)]
+        e(f"const unsigned base = {f['base']};", 2)
         e("double2 v[16];", 2)
         for r in range(PER):
-            e(f"v[{r}] = lds[swz(base | {cst[r]}u)];", 2)
-
-        def ext(ebit, nonfib=nonfib):
-            if ebit in bitpos:
-                j = bitpos.index(ebit)
-                if j not in nonfib:  # a fiber position: the base has it cleared
-                    return "false"
-                return f"((tid >> {nonfib.index(j)}) & 1u)"
-            return f"((tbase >> {ebit}) & 1ull)"
-
-        for oi in range(int(gr["op_begin"]), int(gr["op_end"])):
-            _emit_op(e, enc.ops[oi], enc.mats, ext, enc.n_slots)
+            e(f"v[{r}] = lds[swz(base | {f['cst'][r]}u)];", 2)
+        _emit_group_ops(e, enc, gi, f, bitpos)
         for r in range(PER):
-            e(f"lds[swz(base | {cst[r]}u)] = v[{r}];", 2)
+            e(f"lds[swz(base | {f['cst'][r]}u)] = v[{r}];", 2)
         e("__syncthreads();", 2)
         e("}")
     if zero_tile:
@@ -352,6 +347,105 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str, device_fn: bool = F
     else:
         for i in range(PER):
             e(f"st[tbase | lo | 0x{hi[i]:x}ull] = lds[swz(tid + {NT * i})];")
+    e("}", 0)
+    return e.lines
+
+
+def _fiber(enc, gi: int, TB: int, bitpos: list) -> dict:
+    """Layout of group ``gi``'s fiber: tile positions (``pos``), the thread's base tile position
+    (``base`` expression of tid), per-register offsets (``cst``), and the same in state bits:
+    ``lo`` (expression of tid) and ``hi`` (constants), so amplitude r sits at state index
+    ``tbase | lo | hi[r]``."""
+    pos = [int(x) for x in enc.groups[gi]["pos"]]
+    nonfib = [p for p in range(TB) if p not in pos]
+    return {
+        "pos": pos,
+        "nonfib": nonfib,
+        "base": _deposit("tid", list(range(TB - 4)), nonfib),
+        "cst": [sum(((r >> k) & 1) << pos[k] for k in range(4)) for r in range(PER)],
+        "lo": _deposit("(unsigned long long)tid", list(range(TB - 4)), [bitpos[p] for p in nonfib]),
+        "hi": [sum(((r >> k) & 1) << bitpos[pos[k]] for k in range(4)) for r in range(PER)],
+    }
+
+
+def _emit_group_ops(e: _Emitter, enc, gi: int, f: dict, bitpos: list) -> None:
+    nonfib = f["nonfib"]
+
+    def ext(ebit):
+        if ebit in bitpos:
+            j = bitpos.index(ebit)
+            if j not in nonfib:  # a fiber position: the base has it cleared
+                return "false"
+            return f"((tid >> {nonfib.index(j)}) & 1u)"
+        return f"((tbase >> {ebit}) & 1ull)"
+
+    gr = enc.groups[gi]
+    for oi in range(int(gr["op_begin"]), int(gr["op_end"])):
+        _emit_op(e, enc.ops[oi], enc.mats, ext, enc.n_slots)
+
+
+def _pass_body_direct(e: _Emitter, enc, ps, gids: list, TB: int, NT: int, n: int, m: int, bitpos: list,
+                      init: bool, final: bool, zero_tile: bool, zero_mask: int) -> list:
+    """Body of a pass kernel in the direct form (see _pass_kernel)."""
+    first, last = _fiber(enc, gids[0], TB, bitpos), _fiber(enc, gids[-1], TB, bitpos)
+    mmask = (1 << m) - 1
+    if final:
+        e(f"const unsigned long long xlo = (tbase | {last['lo']}) & 0x{mmask:x}ull;")
+        for r in range(PER):
+            e(f"double out{r} = 0.0;")
+        e("long long j0 = grp, j1 = grp + 1;")
+        e("if (label_off) { j0 = label_off[grp]; j1 = label_off[grp + 1]; }")
+        e("for (long long job = j0; job < j1; ++job) {")
+    else:
+        e("const long long job = grp;")
+    e(f"double2* st = state + job * {1 << n}ll;")
+    e("(void)st;")
+    e("double2 v[16];")
+    if init:  # |0..0>: amplitude 1 at tile position 0 = register 0 of thread 0 (of the tbase == 0 tile)
+        e("v[0] = make_double2((tid == 0 && tbase == 0ull) ? 1.0 : 0.0, 0.0);")
+        for r in range(1, PER):
+            e(f"v[{r}] = make_double2(0.0, 0.0);")
+    else:
+        e(f"const unsigned long long slo = tbase | {first['lo']};")
+        for r in range(PER):
+            if zero_mask:
+                e(f"{{ const unsigned long long s = slo | 0x{first['hi'][r]:x}ull; "
+                  f"v[{r}] = (s & 0x{zero_mask:x}ull) ? make_double2(0.0, 0.0) : st[s]; }}")
+            else:
+                e(f"v[{r}] = st[slo | 0x{first['hi'][r]:x}ull];")
+    if zero_tile:
+        e("if (tbase == 0ull) {")
+    for k, gi in enumerate(gids):
+        f = first if k == 0 else (last if k == len(gids) - 1 else _fiber(enc, gi, TB, bitpos))
+        e("{")
+        if k > 0:
+            e(f"const unsigned base = {f['base']};", 2)
+            for r in range(PER):
+                e(f"v[{r}] = lds[swz(base | {f['cst'][r]}u)];", 2)
+        _emit_group_ops(e, enc, gi, f, bitpos)
+        if k < len(gids) - 1:
+            if k == 0:
+                e(f"const unsigned base = {f['base']};", 2)
+            for r in range(PER):
+                e(f"lds[swz(base | {f['cst'][r]}u)] = v[{r}];", 2)
+            e("__syncthreads();", 2)
+        e("}")
+    if zero_tile:
+        e("}")
+    if final:
+        # the ops ran with op_scale divided out: probabilities carry program_scale^2
+        e(f"const double sgn = job_sign[job] * {_lit(program_scale(enc) ** 2)};")
+        for r in range(PER):
+            e(f"out{r} = fma(sgn, fma(v[{r}].x, v[{r}].x, v[{r}].y * v[{r}].y), out{r});")
+        if len(gids) > 1:
+            e("__syncthreads();  // the next branch job's first LDS writes follow this job's last reads")
+        e("}")
+        for r in range(PER):
+            e(f"pjob[(grp << {m}) + (long long)(xlo | 0x{last['hi'][r] & mmask:x}ull)] = out{r};")
+    else:
+        e(f"const unsigned long long slo2 = tbase | {last['lo']};")
+        for r in range(PER):
+            e(f"st[slo2 | 0x{last['hi'][r]:x}ull] = v[{r}];")
     e("}", 0)
     return e.lines
 
