@@ -312,6 +312,34 @@ def _emit(op: HostOp, fib: dict, mats: _Mats) -> list:
     return [rec(K_U2, a=a, b=b, mat=mats.add(mm))]
 
 
+def fiber_groups(ops: list) -> list:
+    """Cut a pass's ops into fiber groups of <= FIBER_BITS non-diagonal qubits, with lookahead: a
+    group takes, in program order, every op whose qubits it can hold and that depends on no op left
+    behind (an op sharing a qubit with a skipped one is skipped too), so independent later ops join
+    an earlier group instead of opening a new one. Each group costs an LDS round trip of the tile in
+    the sweep kernels; ops on disjoint qubits commute, so the result is the same state (fp64
+    rounding aside). Returns [(ops, needed qubits)] in execution order."""
+    remaining = list(ops)
+    out = []
+    while remaining:
+        need_all: set = set()
+        taken, rest, blocked = [], [], set()
+        for op in remaining:
+            qs = set(op.qubits)
+            need = op_need(op)
+            if not (qs & blocked) and len(need_all | need) <= FIBER_BITS:
+                need_all |= need
+                taken.append(op)
+            else:
+                blocked |= qs
+                rest.append(op)
+        if not taken:  # cannot happen (the first remaining op always fits an empty fiber)
+            raise RuntimeError("fiber grouping made no progress")
+        out.append((taken, need_all))
+        remaining = rest
+    return out
+
+
 def encode(prog: FragmentProgram, tile_bits: int = TILE_BITS) -> EncodedProgram:
     """``tile_bits`` (SPLIT programs only; PACKED programs always use 12-bit tiles): 12 for the
     interpreter kernel, 13 for per-program kernels (128 KiB LDS, 512 threads)."""
@@ -328,13 +356,7 @@ def encode(prog: FragmentProgram, tile_bits: int = TILE_BITS) -> EncodedProgram:
         local = {q: i for i, q in enumerate(tile)}  # state bit -> local position
         n_local = n_eff if packed else tile_bits
         g_begin = len(groups_out)
-        # cut the pass into fiber groups
-        cur: list = []
-        cur_need: set = set()
-
-        def close():
-            if not cur:
-                return
+        for cur, cur_need in fiber_groups(p.ops):
             pos = sorted(local[q] for q in cur_need)
             for cand in range(n_local):  # pad the fiber to 4 positions
                 if len(pos) >= FIBER_BITS:
@@ -347,15 +369,6 @@ def encode(prog: FragmentProgram, tile_bits: int = TILE_BITS) -> EncodedProgram:
             for op in cur:
                 ops_out.extend(_emit(op, fib, mats))
             groups_out.append((pos, ob, len(ops_out), (0, 0)))
-
-        for op in p.ops:
-            need = op_need(op)
-            if len(cur_need | need) > FIBER_BITS:
-                close()
-                cur, cur_need = [], set()
-            cur.append(op)
-            cur_need |= need
-        close()
         flags = (PASS_INIT if pi == 0 else 0) | (PASS_FINAL if pi == len(passes) - 1 else 0)
         traced = 0
         if flags & PASS_FINAL:
