@@ -1120,6 +1120,10 @@ struct OuterBlockedArgs {
     double* __restrict__ out;
 };
 
+// BG: the B operand is read from global memory (L2: the task's B indices are one contiguous range
+// of B's rows) instead of an LDS stage, for masks whose B range per task is too large to stage (syc
+// 32 1: B holds all 16 low output bits, 2^16 values per task, A one value per task).
+template <bool BG>
 __global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlockedArgs a) {
     int K = a.K;
     if (a.kdev) {
@@ -1128,7 +1132,7 @@ __global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlocked
         K = kd < K ? kd : K;
     }
     __shared__ uint32_t tab[2][2][256];  // pext of bytes 0 / 1 of a task offset, per side
-    extern __shared__ double stage[];    // [K][na] of A then [K][nb] of B
+    extern __shared__ double stage[];    // [K][na] of A then (LDS mode) [K][nb] of B
     const uint32_t low = (1u << a.TB) - 1u;
     const uint32_t mAl = a.maskA & low, mBl = a.maskB & low;
     const int na = 1 << __builtin_popcount(mAl), nb = 1 << __builtin_popcount(mBl);
@@ -1150,11 +1154,13 @@ __global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlocked
             const int k = i / na;
             sA[i] = a.A[k * a.lda + ah + (i - k * na)];
         }
-        for (int i = threadIdx.x; i < K * nb; i += 256) {
-            const int k = i / nb;
-            sB[i] = a.B[k * a.ldb + bh + (i - k * nb)];
-        }
+        if (!BG)
+            for (int i = threadIdx.x; i < K * nb; i += 256) {
+                const int k = i / nb;
+                sB[i] = a.B[k * a.ldb + bh + (i - k * nb)];
+            }
         __syncthreads();
+        const double* Bg = a.B + bh;
         double* o = a.out + ((int64_t)base - a.o_begin);
 #pragma unroll 4
         for (int it = 0; it < iters; ++it) {
@@ -1165,7 +1171,8 @@ __global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlocked
             for (int k = 0; k < SK_MAX; ++k)
                 if (k < K) {
                     const double av = sA[k * na + row];
-                    const d2_t bv = *reinterpret_cast<const d2_t*>(sB + k * nb + col);
+                    const d2_t bv = BG ? *reinterpret_cast<const d2_t*>(Bg + k * a.ldb + col)
+                                       : *reinterpret_cast<const d2_t*>(sB + k * nb + col);
                     acc.x = fma(av, bv.x, acc.x);
                     acc.y = fma(av, bv.y, acc.y);
                 }
@@ -1179,16 +1186,22 @@ constexpr int OB_WG_PER_CU = 16;
 
 // Widest task (TB <= 16 and <= align_bits, >= 9: one 512-output iteration) whose operand stage fits
 // OB_STAGE_BYTES; 0: none. align_bits = trailing zero bits of the output range's begin and count.
-int outer_blocked_tile(int nbits, int64_t K, uint64_t maskA, uint64_t maskB, int align_bits) {
+// *b_global: stage only A and read B from global memory — taken when that allows a task of >= 2^14
+// outputs while staging both does not (tasks below 2^14 outputs write measurably slower).
+int outer_blocked_tile(int nbits, int64_t K, uint64_t maskA, uint64_t maskB, int align_bits, bool* b_global) {
     int top = nbits < 16 ? nbits : 16;
     top = align_bits < top ? align_bits : top;
+    int both = 0, aonly = 0;
     for (int tb = top; tb >= 9; --tb) {
         const uint64_t low = (uint64_t(1) << tb) - 1;
-        const int64_t bytes = 8 * K * ((int64_t(1) << __builtin_popcountll(maskA & low)) +
-                                       (int64_t(1) << __builtin_popcountll(maskB & low)));
-        if (bytes <= OB_STAGE_BYTES) return tb;
+        const int64_t sa = 8 * K * (int64_t(1) << __builtin_popcountll(maskA & low));
+        const int64_t sb = 8 * K * (int64_t(1) << __builtin_popcountll(maskB & low));
+        // B from global: the lane's 16-B reads need an even B range (bit 0 of the output is B's)
+        if (!aonly && sa <= OB_STAGE_BYTES && (maskB & 1)) aonly = tb;
+        if (!both && sa + sb <= OB_STAGE_BYTES) both = tb;
     }
-    return 0;
+    *b_global = both < 14 && aonly >= 14 && aonly > both;
+    return *b_global ? aonly : both;
 }
 
 __global__ void qk_khatri_rao_kernel(int64_t K, int64_t M, int64_t N, const double* __restrict__ A,
@@ -1495,11 +1508,12 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
     QK_HIP(ctx, hipSetDevice(ctx->device));
     const int cus = ctx->cus;
     const int align = __builtin_ctzll((uint64_t)(o_begin | o_count));
-    const int tb = outer_blocked_tile(nbits, K, maskA, maskB, align);
+    bool bg = false;
+    const int tb = outer_blocked_tile(nbits, K, maskA, maskB, align, &bg);
     if (tb) {
         const uint64_t low = (uint64_t(1) << tb) - 1;
         const size_t stage = 8 * (size_t)K * ((size_t(1) << __builtin_popcountll(maskA & low)) +
-                                              (size_t(1) << __builtin_popcountll(maskB & low)));
+                                              (bg ? 0 : (size_t(1) << __builtin_popcountll(maskB & low))));
         const int64_t tasks = o_count >> tb;
         // workgroups per CU of the grid-stride launch; QKNIT_OB_WG_PER_CU=0: one workgroup per task
         // (workgroups retire as they finish, so work on other streams can take their slots)
@@ -1507,8 +1521,11 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
         const int64_t G0 = wgpc > 0 ? (int64_t)cus * wgpc : tasks;
         OuterBlockedArgs b{(int)K, tb, A, lda, B, ldb, (uint32_t)maskA, (uint32_t)maskB, o_begin >> tb,
                            (o_begin >> tb) + tasks, o_begin, k_dev, out};
-        hipLaunchKernelGGL(qk_knit_outer_blocked_kernel, dim3((unsigned)(tasks < G0 ? tasks : G0)), dim3(256), stage,
-                           ctx->stream, b);
+        const dim3 grid((unsigned)(tasks < G0 ? tasks : G0));
+        if (bg)
+            hipLaunchKernelGGL(qk_knit_outer_blocked_kernel<true>, grid, dim3(256), stage, ctx->stream, b);
+        else
+            hipLaunchKernelGGL(qk_knit_outer_blocked_kernel<false>, grid, dim3(256), stage, ctx->stream, b);
         QK_HIP(ctx, hipGetLastError());
         return QK_OK;
     }

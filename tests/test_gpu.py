@@ -602,8 +602,8 @@ def test_knit_outer_stream_matches_torch(T, K, nbits, bits_b):
     """qk_knit_outer_stream: the small-K two-fragment knit written in output order equals A^T B
     scattered through the deposit keys of the two clbit sets. nbits 3: the per-output kernel on a
     single partial chunk (8 outputs, grid of 1); nbits >= 9: the blocked kernel (tasks of 2^TB
-    outputs, TB <= 16, the operand stage in LDS); nbits 18 / K 8 / 14 low B bits: no task size fits
-    the stage budget, the per-output kernel again."""
+    outputs, TB <= 16, the operand stage in LDS); nbits 18 / K 8 / 14 low B bits: the B range of a
+    task is too large to stage, the blocked kernel reads B from global memory (syc 32 1's layout)."""
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.knit_plan import deposit_keys
 
     ctx = engine.get_context(0)
