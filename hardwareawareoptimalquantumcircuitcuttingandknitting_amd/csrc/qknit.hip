@@ -1200,7 +1200,9 @@ int outer_blocked_tile(int nbits, int64_t K, uint64_t maskA, uint64_t maskB, int
         if (!aonly && sa <= OB_STAGE_BYTES && (maskB & 1)) aonly = tb;
         if (!both && sa + sb <= OB_STAGE_BYTES) both = tb;
     }
-    *b_global = both < 14 && aonly >= 14 && aonly > both;
+    // QKNIT_OB_BGLOBAL=1 forces the B-from-global form wherever it applies (A/B experiments)
+    static const int force = getenv("QKNIT_OB_BGLOBAL") ? atoi(getenv("QKNIT_OB_BGLOBAL")) : -1;
+    *b_global = force >= 0 ? (force > 0 && aonly >= 9) : (both < 14 && aonly >= 14 && aonly > both);
     return *b_global ? aonly : both;
 }
 
