@@ -62,6 +62,16 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 }
 constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
 
+// 1/x and 1/sqrt(x) from the hardware estimates refined by one Newton step
+__device__ __forceinline__ double rcp_d(double x) {
+    const double r = __builtin_amdgcn_rcp(x);
+    return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double rsq_d(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    return fma(y * 0.5, fma(-x * y, y, 1.0), y);
+}
+
 // sum over aligned groups of `width` lanes (1, 2, 4, 8, 16, 32, 64); every lane of a group gets it
 __device__ __forceinline__ double wsum(double v, int width = 64) {
     if (width >= 2) v += dppd<DPP_XOR1>(v);
@@ -133,6 +143,7 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
             }
         }
         __syncthreads();
+        RK_STAMP(4)
         for (int e = tid; e < n; e += RK_THREADS) {
             const int s = e / (K * K), i = (e / K) % K, j = e % K;
             if (i < j) {
@@ -265,9 +276,13 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
                 // the factors only need to be good enough for the probe check that follows (1e-13
                 // relative orthogonality instead of 1e-15: fewer sweeps chasing rounding)
                 if (live && ga != 0.0 && fabs(ga) > 1e-13 * sqrt(al * be) && fmax(al, be) > floor2) {
-                    const double zeta = (be - al) / (2.0 * ga);
-                    const double tt = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-                    const double c = 1.0 / sqrt(1.0 + tt * tt), s = c * tt;
+                    // hardware reciprocal / reciprocal-sqrt seeds + one Newton step each (full double
+                    // precision without the IEEE division / sqrt sequences): this is the serial chain
+                    // of every Jacobi round
+                    const double zeta = (be - al) * 0.5 * rcp_d(ga);
+                    const double w = 1.0 + zeta * zeta;
+                    const double tt = copysign(rcp_d(fabs(zeta) + w * rsq_d(w)), zeta);
+                    const double c = rsq_d(1.0 + tt * tt), s = c * tt;
                     for (int i = t; i < ra; i += tpp) {
                         const double cp = C[i][p], cq = C[i][q];
                         C[i][p] = c * cp - s * cq;
