@@ -55,6 +55,8 @@ SIGNATURES = {
                                          c_vp, c_i64, c_vp]),
     "qk_sweep_compiled_multi": (c_i32, [c_vp, c_vp, ctypes.c_int, ctypes.POINTER(QkProgram), c_lp, c_vp, c_vp, c_lp,
                                         c_vp, c_vp, c_lp, c_vp, c_vp]),
+    "qk_sweep_compiled_multi_shared": (c_i32, [c_vp, c_vp, ctypes.c_int, ctypes.POINTER(QkProgram), c_lp, c_vp, c_vp,
+                                               c_lp, c_vp, c_vp, c_lp, c_vp, c_vp, c_lp, c_vp, c_vp]),
     "qk_reduce_labels": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "qk_gemm_keyed": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                               c_vp, c_i64, c_vp, ctypes.c_int]),

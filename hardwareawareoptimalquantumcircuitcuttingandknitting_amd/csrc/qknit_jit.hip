@@ -45,8 +45,25 @@ int qk_module_compile(qk_ctx* ctx, const char* source, const char* const* names,
     if (hiprtcCreateProgram(&prog, source, "qk_sweep_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
         return jfail(ctx, QK_EHIP, "qk_module_compile: hiprtcCreateProgram failed");
     for (int i = 0; i < n_names; ++i) hiprtcAddNameExpression(prog, names[i]);
-    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    // extra compiler options from a first source line "// qk-options: -fa -fb" (sweep_codegen asks
+    // for -fno-signed-zeros -ffinite-math-only so known-zero amplitudes fold away)
+    std::vector<std::string> extra;
+    const std::string tag = "// qk-options:";
+    const std::string src(source);
+    if (src.compare(0, tag.size(), tag) == 0) {
+        const std::string line = src.substr(tag.size(), src.find('\n') - tag.size());
+        size_t i = 0;
+        while (i < line.size()) {
+            while (i < line.size() && line[i] == ' ') ++i;
+            size_t j = i;
+            while (j < line.size() && line[j] != ' ') ++j;
+            if (j > i) extra.push_back(line.substr(i, j - i));
+            i = j;
+        }
+    }
+    std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    for (const std::string& o : extra) opts.push_back(o.c_str());
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
         hiprtcGetProgramLogSize(prog, &n);
@@ -157,13 +174,19 @@ struct qk_multi_args {
     int64_t begin[QK_MULTI_MAX];
     int64_t end[QK_MULTI_MAX];
     const uint64_t* map;  // block -> (program << 56 | block within its range), or NULL: ranges in order
+    const double* islots[QK_MULTI_MAX];  // INIT round with shared prefixes: slot rows of the prefixes
+    const int* pfx[QK_MULTI_MAX];        // FINAL round of a shared two-pass program: job -> prefix slot
 };
 
-int qk_sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, const qk_program* progs,
-                            const int64_t* n_jobs, const double* const* job_slots, const double* const* job_sign,
-                            const int64_t* n_labels, const int64_t* const* label_offsets, void* const* workspaces,
-                            const int64_t* workspace_bytes, double* const* outs,
-                            const uint64_t* const* block_maps) {
+}  // extern "C"
+
+namespace {
+
+int sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, const qk_program* progs,
+                         const int64_t* n_jobs, const double* const* job_slots, const double* const* job_sign,
+                         const int64_t* n_labels, const int64_t* const* label_offsets, void* const* workspaces,
+                         const int64_t* workspace_bytes, double* const* outs, const uint64_t* const* block_maps,
+                         const int64_t* n_init, const double* const* init_slots, const int32_t* const* prefix_of) {
     if (!ctx) return QK_EARG;
     if (!module || !progs || n_prog < 1 || n_prog > QK_MULTI_MAX || !n_jobs || !job_slots || !job_sign ||
         !n_labels || !label_offsets || !workspaces || !workspace_bytes || !outs)
@@ -184,6 +207,13 @@ int qk_sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, co
         const int64_t need = n_jobs[f] * ((int64_t)1 << p.n) * (int64_t)(2 * sizeof(double));
         if (!workspaces[f] || workspace_bytes[f] < need)
             return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: workspace too small");
+        if (prefix_of && prefix_of[f]) {
+            // shared INIT prefixes: two-pass programs only (a middle pass would write per-job state
+            // over the prefix slots); the prefixes' slot rows and count come with the map
+            if (p.n_passes != 2 || !n_init || n_init[f] < 1 || n_init[f] > n_jobs[f] ||
+                !init_slots || (p.n_slots > 0 && !init_slots[f]))
+                return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi_shared: bad shared-prefix arguments");
+        }
         if (p.n_passes > rounds) rounds = p.n_passes;
     }
     if ((int)module->fns.size() != rounds)
@@ -200,10 +230,13 @@ int qk_sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, co
                 return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: tile width changes between passes");
             const bool sparse_init = r == 0 && p.n_passes > 1;
             const bool fin = r == p.n_passes - 1;
+            const bool shared = prefix_of && prefix_of[f];
             const int64_t units = (fin && label_offsets[f]) ? n_labels[f] : n_jobs[f];
-            total += sparse_init ? n_jobs[f] : (units << (p.n - tb));
+            total += sparse_init ? (shared ? n_init[f] : n_jobs[f]) : (units << (p.n - tb));
             a.end[f] = total;
             a.slots[f] = job_slots[f];
+            a.islots[f] = (shared && sparse_init) ? init_slots[f] : nullptr;
+            a.pfx[f] = (shared && fin) ? prefix_of[f] : nullptr;
             a.sign[f] = job_sign[f];
             a.state[f] = workspaces[f];
             a.out[f] = outs[f];
@@ -220,6 +253,32 @@ int qk_sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, co
             return jfail(ctx, QK_EHIP, std::string("qk_sweep_compiled_multi: ") + hipGetErrorString(e));
     }
     return QK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qk_sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, const qk_program* progs,
+                            const int64_t* n_jobs, const double* const* job_slots, const double* const* job_sign,
+                            const int64_t* n_labels, const int64_t* const* label_offsets, void* const* workspaces,
+                            const int64_t* workspace_bytes, double* const* outs,
+                            const uint64_t* const* block_maps) {
+    return sweep_compiled_multi(ctx, module, n_prog, progs, n_jobs, job_slots, job_sign, n_labels, label_offsets,
+                                workspaces, workspace_bytes, outs, block_maps, nullptr, nullptr, nullptr);
+}
+
+int qk_sweep_compiled_multi_shared(qk_ctx* ctx, const qk_module* module, int n_prog, const qk_program* progs,
+                                   const int64_t* n_jobs, const double* const* job_slots,
+                                   const double* const* job_sign, const int64_t* n_labels,
+                                   const int64_t* const* label_offsets, void* const* workspaces,
+                                   const int64_t* workspace_bytes, double* const* outs,
+                                   const uint64_t* const* block_maps, const int64_t* n_init,
+                                   const double* const* init_slots, const int32_t* const* prefix_of) {
+    if (!prefix_of || !n_init || !init_slots)
+        return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi_shared: null shared-prefix arrays");
+    return sweep_compiled_multi(ctx, module, n_prog, progs, n_jobs, job_slots, job_sign, n_labels, label_offsets,
+                                workspaces, workspace_bytes, outs, block_maps, n_init, init_slots, prefix_of);
 }
 
 int qk_sweep_compiled_labels(qk_ctx* ctx, const qk_module* module, const qk_program* p, int64_t n_jobs,

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes
 import dataclasses
+import hashlib
 import os
 import threading
 from dataclasses import dataclass, field
@@ -29,7 +30,7 @@ from . import _lib
 from .fragment_program import (FragmentProgram, JobTable, basis_reduce, build_jobs, compile_fragment,
                                dedup_labels)
 from .knit_plan import LabelSpace, deposit_keys, factor_vgate
-from .sweep_plan import EncodedProgram, encode
+from .sweep_plan import K_SLOT, EncodedProgram, encode
 
 _torch = None
 
@@ -231,7 +232,7 @@ def compiled_multi_module(device: int, encs: list):
 
 
 def _compile_module(device: int, src: str, names: list):
-    key = (device, names[0])
+    key = (device, names[0], hashlib.sha1(src.encode()).hexdigest())
     with _modules_lock:
         if key not in _MODULES:
             ctx = get_context(device)
@@ -241,6 +242,40 @@ def _compile_module(device: int, src: str, names: list):
                       "qk_module_compile")
             _MODULES[key] = h
         return _MODULES[key]
+
+
+def init_prefixes(enc, jobs: JobTable):
+    """Shared INIT prefixes of a two-pass SPLIT program (``qk_sweep_compiled_multi_shared``).
+
+    The sparse INIT pass starts every branch job from |0..0> and applies the same ops except the
+    slot ops, so its output depends on a job only through the slot matrices of the slots that pass
+    reads. Jobs with equal rows there share one INIT tile: syc 32 5 sweeps 50 INIT tiles for its
+    750 branch jobs (each fragment has 5 channels on each of its 2 INIT slots). Returns
+    ``(reps, prefix_of)`` — one representative job per prefix (first occurrence order) and each
+    job's prefix index — or None when sharing saves nothing (not two passes, no repeated prefix)
+    or ``QKNIT_SWEEP_SHARE=0``."""
+    if os.environ.get("QKNIT_SWEEP_SHARE", "1") == "0" or enc.packed or len(enc.passes) != 2:
+        return None
+    n = jobs.n_jobs
+    if n < 2:
+        return None
+    ps = enc.passes[0]
+    slots = sorted({int(enc.ops[o]["slot"]) for gi in range(int(ps["group_begin"]), int(ps["group_end"]))
+                    for o in range(int(enc.groups[gi]["op_begin"]), int(enc.groups[gi]["op_end"]))
+                    if int(enc.ops[o]["kind"]) == K_SLOT})
+    if slots:
+        rows = np.ascontiguousarray(jobs.slot_mats[:, slots]).reshape(n, -1)
+        keys = rows.view(np.uint8).reshape(n, -1)  # bitwise equality: the kernels read these exact values
+        _, first, inv = np.unique(keys, axis=0, return_index=True, return_inverse=True)
+        order = np.argsort(first, kind="stable")  # prefixes in first-occurrence order
+        rank = np.empty_like(order)
+        rank[order] = np.arange(order.size)
+        reps, prefix_of = first[order].astype(np.int64), rank[inv.reshape(-1)].astype(np.int32)
+    else:  # INIT reads no slot: one prefix for every job
+        reps, prefix_of = np.zeros(1, np.int64), np.zeros(n, np.int32)
+    if reps.size == n:
+        return None
+    return reps, prefix_of
 
 
 def jobs_to_device(jobs: JobTable, device):

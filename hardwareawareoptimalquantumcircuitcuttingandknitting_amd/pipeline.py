@@ -185,16 +185,32 @@ class HipBackend:
         maps = multi_block_maps([fs.dprog.enc for fs in frags], sweeps)
         self._maps = [None if m is None else self.to_device(m.view(np.int64)) for m in maps]  # kept alive
         rounds = len(maps)
-        return (module, (_lib.QkProgram * n)(*[fs.dprog.struct for fs in frags]), i64([sw["n_jobs"] for sw in sweeps]),
+        args = [module, (_lib.QkProgram * n)(*[fs.dprog.struct for fs in frags]), i64([sw["n_jobs"] for sw in sweeps]),
                 vp([sw["slot"].data_ptr() for sw in sweeps]), vp([sw["sign"].data_ptr() for sw in sweeps]),
                 i64([sw["n_local"] for sw in sweeps]),
                 vp([sw["off"].data_ptr() if sw["fused"] else None for sw in sweeps]),
                 vp([sw["ws"].data_ptr() for sw in sweeps]), i64([sw["ws"].numel() for sw in sweeps]),
                 vp([o.data_ptr() for o in outs]),
-                (ctypes.c_void_p * rounds)(*[None if m is None else m.data_ptr() for m in self._maps]))
+                (ctypes.c_void_p * rounds)(*[None if m is None else m.data_ptr() for m in self._maps])]
+        # shared INIT prefixes (engine.init_prefixes): one INIT tile per distinct prefix
+        shared = [engine.init_prefixes(fs.dprog.enc, sw["jobs"]) if sw.get("jobs") is not None else None
+                  for fs, sw in zip(frags, sweeps)]
+        self.shared_init = [None if s is None else int(s[0].size) for s in shared]
+        if any(s is not None for s in shared):
+            self._shared = [None if s is None else (sw["slot"][self.to_device(s[0])].contiguous(),
+                                                    self.to_device(s[1]))
+                            for s, sw in zip(shared, sweeps)]  # kept alive
+            args += [i64([0 if s is None else int(s[0].size) for s in shared]),
+                     vp([None if s is None else s[0].data_ptr() for s in self._shared]),
+                     vp([None if s is None else s[1].data_ptr() for s in self._shared])]
+        return tuple(args)
 
     def sweep_multi(self, plan):
         module, progs, *rest = plan
+        if len(rest) == 12:
+            self.ctx.check(self.ctx.lib.qk_sweep_compiled_multi_shared(self.ctx.handle, module, len(progs), progs,
+                                                                       *rest), "qk_sweep_compiled_multi_shared")
+            return
         self.ctx.check(self.ctx.lib.qk_sweep_compiled_multi(self.ctx.handle, module, len(progs), progs, *rest),
                        "qk_sweep_compiled_multi")
 
@@ -395,7 +411,7 @@ class KnitPipeline:
                           for l0, l1, j0, j1 in engine.label_chunks(offs, self.chunk_jobs)]
                 need = be.workspace_bytes(fs, max(c[3] - c[2] for c in chunks))
             self.sweeps.append(dict(lo=lo, n_local=n_local, slot=slot_t, sign=sign_t, off=off_t, n_jobs=n_jobs,
-                                    fused=fused, chunks=chunks, label_offsets=sub.label_offsets,
+                                    fused=fused, chunks=chunks, label_offsets=sub.label_offsets, jobs=sub,
                                     pjob=(None if fused else
                                           be.empty((max(n_jobs, 1), width), T.float64) if branching
                                           else alloc((max(rows, 1), width), T.float64)),

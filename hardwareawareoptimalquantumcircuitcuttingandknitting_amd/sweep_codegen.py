@@ -26,6 +26,20 @@ OPS_HEADER = os.path.join(_HERE, "csrc", "sweep_ops.h")
 PER = 16  # amplitudes per thread (4 fiber bits); threads per workgroup = 2^(tile_bits - 4)
 
 
+def _prologue() -> str:
+    """Compiler options line (qk_module_compile) and defines ahead of the inlined sweep_ops.h.
+
+    The kernels only ever hold finite amplitudes and the sign of a zero never reaches a result
+    (probabilities are |z|^2), so they are compiled with -fno-signed-zeros -ffinite-math-only:
+    with those, 0 * x, x + 0 and fma(x, 0, y) fold, and the FINAL pass's first fiber — 14 of its
+    16 amplitudes are known zeros of the sparse INIT tile on syc 32 5 — skips the ops on zeros
+    (tools/sweep_isa.py). QKNIT_SWEEP_FOLD_ZEROS=0 compiles without (same results up to signed
+    zeros)."""
+    if os.environ.get("QKNIT_SWEEP_FOLD_ZEROS", "1") == "0":
+        return ""
+    return "// qk-options: -fno-signed-zeros -ffinite-math-only\n"
+
+
 def _lit(x: float) -> str:
     x = float(x)
     return x.hex() if x != 0.0 else ("-0.0" if str(x).startswith("-") else "0.0")
@@ -251,9 +265,10 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str, device_fn: bool = F
         e(f'extern "C" __global__ __launch_bounds__({NT}) void {name}(', 0)
     e("const double* __restrict__ job_slots, const double* __restrict__ job_sign,", 2)
     e("double2* __restrict__ state, double* __restrict__ pjob, long long n_jobs,", 2)
-    e("const long long* __restrict__ label_off) {", 2)
+    e("const long long* __restrict__ label_off" + (", const int* __restrict__ pfx) {" if device_fn else ") {"), 2)
     e("using namespace qk_sweep_ops;")
     if not device_fn:
+        e("const int* pfx = nullptr;")
         e(f"__shared__ double2 lds[{1 << TB}];")
         e("const unsigned blk = blockIdx.x;")
     e("const unsigned tid = threadIdx.x;")
@@ -266,7 +281,7 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str, device_fn: bool = F
     else:
         e("const unsigned long long tbase = 0ull;")
     e(f"const unsigned long long lo = {_deposit('(unsigned long long)tid', list(range(TB - 4)), bitpos[:TB - 4])};")
-    e("(void)n_jobs; (void)job_slots; (void)lo; (void)label_off;")
+    e("(void)n_jobs; (void)job_slots; (void)lo; (void)label_off; (void)pfx;")
     keep = [i for i in range(PER) if not ((NT * i) & traced)]
     gids = list(range(int(ps["group_begin"]), int(ps["group_end"])))
     zero_tile = init and not init_sparse and tpj_log > 0
@@ -287,7 +302,7 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str, device_fn: bool = F
         e("for (long long job = j0; job < j1; ++job) {")
     else:
         e("const long long job = grp;")
-    e(f"double2* st = state + job * {1 << n}ll;")
+    e(_state_ptr(enc, ps))
     e("(void)st;")
     if init:
         e("lds[swz(tid)] = make_double2((tid == 0 && tbase == 0ull) ? 1.0 : 0.0, 0.0);")
@@ -351,6 +366,15 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str, device_fn: bool = F
     return e.lines
 
 
+def _state_ptr(enc, ps) -> str:
+    """Job state of a pass: the FINAL pass of a two-pass program may start from a shared INIT
+    prefix's state (``pfx``: job -> prefix slot, qk_sweep_compiled_multi_shared)."""
+    n = enc.n
+    if len(enc.passes) == 2 and bool(int(ps["flags"]) & sp.PASS_FINAL):
+        return f"double2* st = state + (pfx ? (long long)pfx[job] : job) * {1 << n}ll;"
+    return f"double2* st = state + job * {1 << n}ll;"
+
+
 def _fiber(enc, gi: int, TB: int, bitpos: list) -> dict:
     """Layout of group ``gi``'s fiber: tile positions (``pos``), the thread's base tile position
     (``base`` expression of tid), per-register offsets (``cst``), and the same in state bits:
@@ -398,7 +422,7 @@ def _pass_body_direct(e: _Emitter, enc, ps, gids: list, TB: int, NT: int, n: int
         e("for (long long job = j0; job < j1; ++job) {")
     else:
         e("const long long job = grp;")
-    e(f"double2* st = state + job * {1 << n}ll;")
+    e(_state_ptr(enc, ps))
     e("(void)st;")
     e("double2 v[16];")
     if init:  # |0..0>: amplitude 1 at tile position 0 = register 0 of thread 0 (of the tbase == 0 tile)
@@ -462,7 +486,7 @@ def generate(enc: sp.EncodedProgram) -> tuple[str, list]:
         name = f"qk_sweep_{key}_p{ip}"
         names.append(name)
         body += _pass_kernel(enc, ip, name) + [""]
-    src = open(OPS_HEADER).read() + "\n" + "\n".join(body) + "\n"
+    src = _prologue() + open(OPS_HEADER).read() + "\n" + "\n".join(body) + "\n"
     return src, names
 
 
@@ -477,6 +501,8 @@ _MULTI_STRUCT = """struct qk_multi_args {
     long long begin[4];
     long long end[4];
     const unsigned long long* map;
+    const double* islots[4];
+    const int* pfx[4];
 };
 """
 
@@ -497,6 +523,7 @@ def generate_multi(encs: list) -> tuple[str, list]:
                  + bytes([e.n, e.m, e.n_slots]))
     key = h.hexdigest()[:12]
     body, names = [_MULTI_STRUCT], []
+    shares = [len(e.passes) == 2 for e in encs]
     for r in range(max(len(e.passes) for e in encs)):
         members = [f for f, e in enumerate(encs) if len(e.passes) > r]
         for f in members:
@@ -520,11 +547,15 @@ def generate_multi(encs: list) -> tuple[str, list]:
         body.append("    }")
         for f in members:
             body.append(f"    if (f == {f} && lb >= 0 && lb < a.end[{f}] - a.begin[{f}]) {{")
-            body.append(f"        qk_mb_{key}_f{f}_p{r}(lds, (unsigned)lb, a.slots[{f}], a.sign[{f}],")
-            body.append(f"            (double2*)a.state[{f}], a.out[{f}], a.n_jobs[{f}], a.label_off[{f}]);")
+            # shared INIT prefixes (qk_sweep_compiled_multi_shared): the INIT round reads the prefixes'
+            # slot rows, the FINAL round of a two-pass program maps each job to its prefix's state
+            slots = f"(a.islots[{f}] ? a.islots[{f}] : a.slots[{f}])" if (r == 0 and shares[f]) else f"a.slots[{f}]"
+            pfx = f"a.pfx[{f}]" if (r == 1 and shares[f]) else "nullptr"
+            body.append(f"        qk_mb_{key}_f{f}_p{r}(lds, (unsigned)lb, {slots}, a.sign[{f}],")
+            body.append(f"            (double2*)a.state[{f}], a.out[{f}], a.n_jobs[{f}], a.label_off[{f}], {pfx});")
             body.append("        return;")
             body.append("    }")
         body.append("}")
         body.append("")
-    src = open(OPS_HEADER).read() + "\n" + "\n".join(body) + "\n"
+    src = _prologue() + open(OPS_HEADER).read() + "\n" + "\n".join(body) + "\n"
     return src, names

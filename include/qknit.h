@@ -151,6 +151,21 @@ int qk_sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, co
                             const int64_t* n_labels, const int64_t* const* label_offsets, void* const* workspaces,
                             const int64_t* workspace_bytes, double* const* outs, const uint64_t* const* block_maps);
 
+/* qk_sweep_compiled_multi with shared INIT tiles. The sparse INIT pass of a two-pass program depends
+ * on a job only through the slot matrices its ops read (syc 32 5: 750 branch jobs, 50 distinct
+ * prefixes). For program f with prefix_of[f] non-NULL (DEVICE, int32 per job), the INIT round runs
+ * n_init[f] units whose slot rows are init_slots[f] (DEVICE, n_init x n_slots x 8 doubles) into
+ * workspace state slots [0, n_init), and the FINAL pass of job j starts from slot prefix_of[f][j].
+ * prefix_of[f] NULL: that program runs as in qk_sweep_compiled_multi. Results are bitwise those of
+ * qk_sweep_compiled_multi when every job's INIT slot rows equal its prefix's. */
+int qk_sweep_compiled_multi_shared(qk_ctx* ctx, const qk_module* module, int n_prog, const qk_program* progs,
+                                   const int64_t* n_jobs, const double* const* job_slots,
+                                   const double* const* job_sign, const int64_t* n_labels,
+                                   const int64_t* const* label_offsets, void* const* workspaces,
+                                   const int64_t* workspace_bytes, double* const* outs,
+                                   const uint64_t* const* block_maps, const int64_t* n_init,
+                                   const double* const* init_slots, const int32_t* const* prefix_of);
+
 /* q[l][x] = sum_{j in [offsets[l], offsets[l+1])} pjob[j][x]   (offsets: DEVICE, n_labels+1) */
 int qk_reduce_labels(qk_ctx* ctx, int64_t n_labels, const int64_t* offsets, int64_t width,
                      const double* pjob, double* q);

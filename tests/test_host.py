@@ -344,3 +344,31 @@ def test_generated_multi_fragment_kernels_compile_for_gfx950(tmp_path):
     r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-c",
                         str(f), "-o", str(tmp_path / "m.o")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_init_prefixes_share_init_tiles():
+    """engine.init_prefixes: on syc 32 5 both fragments' 2-pass programs have 25 distinct INIT
+    prefixes (5 channels on each of 2 INIT slots); every job's INIT slot rows equal its prefix
+    representative's bitwise, representatives map to themselves, and single-pass programs opt out."""
+    _, cut, _ = cutting.config_cut_circuit("syc", 32, 5, 2)
+    frags = engine.prepare_fragments(VirtualCircuit(cut), upload=False, basis=True)
+    for fs in frags:
+        enc = sweep_plan.encode(fs.prog, tile_bits=13)
+        reps, prefix_of = engine.init_prefixes(enc, fs.jobs)
+        assert reps.size == 25 and prefix_of.shape == (fs.jobs.n_jobs,)
+        assert prefix_of[reps].tolist() == list(range(reps.size))
+        assert sorted(set(prefix_of.tolist())) == list(range(reps.size))
+        ps = enc.passes[0]
+        slots = sorted({int(enc.ops[o]["slot"]) for gi in range(int(ps["group_begin"]), int(ps["group_end"]))
+                        for o in range(int(enc.groups[gi]["op_begin"]), int(enc.groups[gi]["op_end"]))
+                        if int(enc.ops[o]["kind"]) == sweep_plan.K_SLOT})
+        rows = fs.jobs.slot_mats[:, slots]
+        assert np.array_equal(rows, rows[reps[prefix_of]])
+        # jobs of different prefixes differ somewhere in the INIT slots
+        firsts = rows[reps].reshape(reps.size, -1)
+        assert len({r.tobytes() for r in firsts}) == reps.size
+    small = engine.prepare_fragments(VirtualCircuit(cutting.config_cut_circuit("bv", 5, 1, 2)[1]), upload=False)
+    for fs in small:
+        enc = sweep_plan.encode(fs.prog, tile_bits=12)
+        if enc.packed or len(enc.passes) != 2:
+            assert engine.init_prefixes(enc, fs.jobs) is None
