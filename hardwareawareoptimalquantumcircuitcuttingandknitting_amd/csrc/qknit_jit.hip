@@ -222,12 +222,18 @@ int sweep_compiled_multi(qk_ctx* ctx, const qk_module* module, int n_prog, const
     for (int r = 0; r < rounds; ++r) {
         qk_multi_args a{};
         int64_t total = 0;
+        // one tile width per round (a FINAL pass may be narrower than the INIT pass:
+        // sweep_plan.narrow_final_tile); the round's kernel has 2^(tb - 4) threads
+        tb = 0;
         for (int f = 0; f < n_prog; ++f) {
             const qk_program& p = progs[f];
             a.begin[f] = a.end[f] = total;
             if (p.n_passes <= r) continue;
-            if (__builtin_popcountll(p.passes[r].tile_mask) != tb)
-                return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: tile width changes between passes");
+            const int t = __builtin_popcountll(p.passes[r].tile_mask);
+            if ((tb && t != tb) || t < QK_JIT_TILE_MIN || t > QK_JIT_TILE_MAX || t >= p.n)
+                return jfail(ctx, QK_EARG, "qk_sweep_compiled_multi: programs need one tile width of 10 to 13 "
+                                           "bits per pass round");
+            tb = t;
             const bool sparse_init = r == 0 && p.n_passes > 1;
             const bool fin = r == p.n_passes - 1;
             const bool shared = prefix_of && prefix_of[f];

@@ -152,12 +152,15 @@ class DeviceProgram:
     module: object = None  # qk_module* of the per-program kernels (SPLIT programs), or None
 
     @staticmethod
-    def upload(prog: FragmentProgram, device, jit: bool = True, tile_bits: int | None = None) -> "DeviceProgram":
+    def upload(prog: FragmentProgram, device, jit: bool = True, tile_bits: int | None = None,
+               final_tile_bits: int | None = None) -> "DeviceProgram":
         T = torch()
         # per-program kernels take up to 13-bit tiles (128 KiB LDS: fewer passes, less state
-        # traffic); smaller ones when the batch is too small to fill the chip (jit_tile_bits)
+        # traffic); smaller ones when the batch is too small to fill the chip (jit_tile_bits); the
+        # FINAL pass may run on narrower tiles (final_tile_bits)
         jit = jit and _jit_enabled()
-        enc = encode(prog, tile_bits=(tile_bits or JIT_TILE_BITS_MAX) if jit else 12)
+        enc = encode(prog, tile_bits=(tile_bits or JIT_TILE_BITS_MAX) if jit else 12,
+                     final_tile_bits=final_tile_bits if jit else None)
         dev = T.device("cuda", device)
 
         def to_dev(arr, dtype):
@@ -203,6 +206,23 @@ def jit_tile_bits(sizes: list) -> int:
         if sum(j << max(n - tb, 0) for n, j in sizes) >= JIT_MIN_BLOCKS:
             return tb
     return JIT_TILE_BITS_MIN
+
+
+JIT_FINAL_TILE_BITS = 10  # FINAL-pass tile width to aim for (narrow_final_tile); 0 = the pass width
+
+
+def jit_final_tile_bits(progs: list, tile_bits: int) -> int | None:
+    """FINAL-pass tile width of one sweep's per-program kernels (one launch per pass round, so one
+    width): ``JIT_FINAL_TILE_BITS`` raised to what every FINAL pass needs, None when that is not
+    narrower than ``tile_bits``. ``QKNIT_FINAL_TILE_BITS`` overrides the target (0: off)."""
+    from .sweep_plan import final_need_bits
+
+    target = int(os.environ.get("QKNIT_FINAL_TILE_BITS", JIT_FINAL_TILE_BITS))
+    if not target or not progs:
+        return None
+    need = max(final_need_bits(p, tile_bits) for p in progs)
+    f = max(target, need, JIT_TILE_BITS_MIN)
+    return f if f < tile_bits else None
 
 
 def _jit_enabled() -> bool:
@@ -604,9 +624,11 @@ def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = 
                                  red.expand if red is not None else None))
     split = [(fs.prog.n, fs.jobs.n_jobs) for fs, w in zip(out, want) if w and not fs.dropped and fs.prog.n > 12]
     tb = jit_tile_bits(split) if split else JIT_TILE_BITS_MAX
+    jit_progs = [fs.prog for fs, w in zip(out, want) if w and not fs.dropped and fs.prog.n > 12]
+    ftb = jit_final_tile_bits(jit_progs, tb) if (upload and jit_progs) else None
     for fs, w in zip(out, want):
         if upload and not fs.dropped:
-            fs.dprog = DeviceProgram.upload(fs.prog, device, jit=w, tile_bits=tb)
+            fs.dprog = DeviceProgram.upload(fs.prog, device, jit=w, tile_bits=tb, final_tile_bits=ftb)
     return out
 
 

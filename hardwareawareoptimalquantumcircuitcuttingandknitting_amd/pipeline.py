@@ -113,7 +113,7 @@ def multi_block_maps(encs: list, sweeps: list) -> list:
     rounds = max(len(e.passes) for e in encs)
     out = []
     for r in range(rounds):
-        items, mapped = [], False
+        items, mapped, perms = [], False, {}
         for f, (enc, sw) in enumerate(zip(encs, sweeps)):
             P = len(enc.passes)
             if P <= r:
@@ -124,18 +124,50 @@ def multi_block_maps(encs: list, sweeps: list) -> list:
                 work, bpu = [1] * sw["n_jobs"], 1
             elif fin and sw["fused"]:
                 offs = sw["label_offsets"]
-                work, bpu = list(np.diff(offs)), 1 << (enc.n - enc.tile_bits)
+                work, bpu = list(np.diff(offs)), 1 << (enc.n - enc.pass_tile_bits(r))
                 mapped = True
+                perms[f] = _xcd_tile_order(enc, r)
             else:
-                work, bpu = [1] * sw["n_jobs"], 1 << (enc.n - enc.tile_bits)
+                work, bpu = [1] * sw["n_jobs"], 1 << (enc.n - enc.pass_tile_bits(r))
             items += [(-int(w), f, u, bpu) for u, w in enumerate(work)]
         if not mapped:
             out.append(None)
             continue
         items.sort(key=lambda t: (t[0], t[1], t[2]))
-        m = np.fromiter(((f << 56) | (u * bpu + t) for _, f, u, bpu in items for t in range(bpu)), dtype=np.uint64)
+        ident = {}
+        m = np.fromiter(((f << 56) | (u * bpu + int(perms.get(f, ident.setdefault(bpu, range(bpu)))[t]))
+                         for _, f, u, bpu in items for t in range(bpu)), dtype=np.uint64)
         out.append(m)
     return out
+
+
+XCD_LINE_BITS = 5  # state bits of one 256-B run of fp64 outputs
+
+
+def _xcd_tile_order(enc, r: int) -> np.ndarray:
+    """Order of a (label)'s tiles in a FINAL-pass block map: tiles whose indices differ only in
+    outside bits below ``XCD_LINE_BITS`` write interleaved parts of the same output lines (a
+    narrowed FINAL tile leaves low state bits outside, sweep_plan.narrow_final_tile). Those bits
+    become the slow bits of the block order, so such tiles land 2^(other bits) blocks apart — a
+    multiple of 8 when >= 3 other bits — and blocks b, b + 8, ... share an XCD (dealt round-robin,
+    MI355X_MICROARCH.md), whose L2 then merges the partial lines before they go to HBM.
+    Identity when no outside bit is that low or fewer than 3 others remain."""
+    tm = int(enc.passes[r]["tile_mask"])
+    outside = [q for q in range(enc.n) if not (tm >> q) & 1]
+    low = [i for i, q in enumerate(outside) if q < XCD_LINE_BITS]
+    high = [i for i, q in enumerate(outside) if q >= XCD_LINE_BITS]
+    bpu = 1 << len(outside)
+    if not low or len(high) < 3 or os.environ.get("QKNIT_FINAL_XCD_ORDER", "1") == "0":
+        return np.arange(bpu)
+    perm = np.zeros(bpu, dtype=np.int64)
+    for o in range(bpu):
+        t = 0
+        for k, i in enumerate(high):
+            t |= ((o >> k) & 1) << i
+        for k, i in enumerate(low):
+            t |= ((o >> (len(high) + k)) & 1) << i
+        perm[o] = t
+    return perm
 
 
 class HipBackend:
@@ -437,7 +469,10 @@ class KnitPipeline:
         ok = all(self.sweeps[i]["n_jobs"] and self.sweeps[i]["chunks"] is None
                  and getattr(self.frags[i], "dprog", None) is not None and self.frags[i].dprog.module is not None
                  for i in idx)
-        if not ok or not 2 <= len(idx) <= 4 or len({self.frags[i].dprog.enc.tile_bits for i in idx}) != 1:
+        encs = [self.frags[i].dprog.enc for i in idx] if ok else []
+        rounds = max((len(e.passes) for e in encs), default=0)
+        if not ok or not 2 <= len(idx) <= 4 or any(
+                len({e.pass_tile_bits(r) for e in encs if len(e.passes) > r}) != 1 for r in range(rounds)):
             return
         self._multi = (idx, self.be.plan_multi([self.frags[i] for i in idx], [self.sweeps[i] for i in idx]))
 

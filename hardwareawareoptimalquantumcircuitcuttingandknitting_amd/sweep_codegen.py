@@ -240,7 +240,7 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str, device_fn: bool = F
     """Pass ``ip`` of ``enc`` as an ``extern "C"`` kernel, or (``device_fn``) as a device function
     of the workgroup's block index within the pass and the shared tile (multi-fragment launches)."""
     n, m = enc.n, enc.m
-    TB = enc.tile_bits
+    TB = enc.pass_tile_bits(ip)
     NT = 1 << (TB - 4)
     P = len(enc.passes)
     ps = enc.passes[ip]
@@ -514,9 +514,11 @@ def generate_multi(encs: list) -> tuple[str, list]:
     each launch instead of queueing behind each other."""
     if not 1 <= len(encs) <= MULTI_MAX:
         raise ValueError(f"1..{MULTI_MAX} programs per multi-fragment module")
-    if any(e.packed for e in encs) or len({e.tile_bits for e in encs}) != 1:
-        raise ValueError("multi-fragment kernels need SPLIT programs of one tile width")
-    NT = 1 << (encs[0].tile_bits - 4)
+    if any(e.packed for e in encs):
+        raise ValueError("multi-fragment kernels need SPLIT programs")
+    for r in range(max(len(e.passes) for e in encs)):
+        if len({e.pass_tile_bits(r) for e in encs if len(e.passes) > r}) != 1:
+            raise ValueError("multi-fragment kernels need one tile width per pass round")
     h = hashlib.sha1()
     for e in encs:
         h.update(e.ops.tobytes() + e.groups.tobytes() + e.passes.tobytes() + e.mats.tobytes()
@@ -530,8 +532,9 @@ def generate_multi(encs: list) -> tuple[str, list]:
             body += _pass_kernel(encs[f], r, f"qk_mb_{key}_f{f}_p{r}", device_fn=True) + [""]
         name = f"qk_sweepm_{key}_r{r}"
         names.append(name)
-        body.append(f'extern "C" __global__ __launch_bounds__({NT}) void {name}(qk_multi_args a) {{')
-        body.append(f"    __shared__ double2 lds[{1 << encs[0].tile_bits}];")
+        tb = encs[members[0]].pass_tile_bits(r)
+        body.append(f'extern "C" __global__ __launch_bounds__({1 << (tb - 4)}) void {name}(qk_multi_args a) {{')
+        body.append(f"    __shared__ double2 lds[{1 << tb}];")
         body.append("    const long long b = blockIdx.x;")
         # caller-ordered blocks (qk_sweep_compiled_multi block_maps): program << 56 | block in its range;
         # otherwise the programs' block ranges in order

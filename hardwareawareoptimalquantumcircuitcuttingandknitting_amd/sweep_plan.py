@@ -189,6 +189,10 @@ class EncodedProgram:
     def tiles_per_job(self) -> int:
         return 1 if self.packed else 1 << (self.n - self.tile_bits)
 
+    def pass_tile_bits(self, ip: int) -> int:
+        """State bits of pass ``ip``'s tile (the FINAL pass's may be narrower: narrow_final_tile)."""
+        return self.n_eff if self.packed else bin(int(self.passes[ip]["tile_mask"])).count("1")
+
 
 class _Mats:
     def __init__(self):
@@ -340,21 +344,61 @@ def fiber_groups(ops: list) -> list:
     return out
 
 
-def encode(prog: FragmentProgram, tile_bits: int = TILE_BITS) -> EncodedProgram:
+def narrow_final_tile(prog: FragmentProgram, passes: list, final_tile_bits: int) -> None:
+    """Shrink the FINAL pass's tile (in place) to ``final_tile_bits`` state bits when its
+    non-diagonal and traced qubits fit: those plus the lowest other state bits. The pass then runs
+    on more, smaller workgroups (per-program kernels: 2^(bits - 4) threads, 2^bits x 16 B of LDS),
+    several per CU, so one workgroup's barrier and LDS phases overlap another's arithmetic instead of
+    stalling the CU; its ops are the same (diagonal action on the bits that leave the tile comes from
+    the tile index). syc 32 5: the FINAL passes need 6 and 9 of the 13 tile bits."""
+    if len(passes) < 2 or prog.n <= TILE_BITS:
+        return
+    last = passes[-1]
+    need = set(range(prog.m, prog.n))
+    for op in last.ops:
+        need |= op_need(op)
+    if not (FIBER_BITS + 6 <= final_tile_bits < len(last.tile)) or len(need) > final_tile_bits:
+        return
+    tile = set(need)
+    for q in range(prog.n):
+        if len(tile) >= final_tile_bits:
+            break
+        tile.add(q)
+    last.tile = sorted(tile)
+
+
+def final_need_bits(prog: FragmentProgram, tile_bits: int) -> int:
+    """State bits the FINAL pass's tile must hold (its non-diagonal and traced qubits), or
+    ``tile_bits`` when the program has a single pass."""
+    if prog.n <= TILE_BITS:
+        return tile_bits
+    passes = schedule_passes(prog, tile_bits)
+    if len(passes) < 2:
+        return tile_bits
+    need = set(range(prog.m, prog.n))
+    for op in passes[-1].ops:
+        need |= op_need(op)
+    return len(need)
+
+
+def encode(prog: FragmentProgram, tile_bits: int = TILE_BITS, final_tile_bits: int | None = None) -> EncodedProgram:
     """``tile_bits`` (SPLIT programs only; PACKED programs always use 12-bit tiles): 12 for the
-    interpreter kernel, 13 for per-program kernels (128 KiB LDS, 512 threads)."""
+    interpreter kernel, 13 for per-program kernels (128 KiB LDS, 512 threads). ``final_tile_bits``
+    (per-program kernels only): narrower FINAL-pass tile (:func:`narrow_final_tile`)."""
     n = prog.n
     packed = n <= TILE_BITS
     n_eff = max(n, FIBER_BITS) if packed else n
     if packed or tile_bits >= n:
         tile_bits = TILE_BITS
     passes = schedule_passes(prog, tile_bits)
+    if final_tile_bits and not packed:
+        narrow_final_tile(prog, passes, final_tile_bits)
     mats = _Mats()
     ops_out, groups_out, passes_out = [], [], []
     for pi, p in enumerate(passes):
         tile = list(range(n_eff)) if packed else p.tile
         local = {q: i for i, q in enumerate(tile)}  # state bit -> local position
-        n_local = n_eff if packed else tile_bits
+        n_local = n_eff if packed else len(tile)
         g_begin = len(groups_out)
         for cur, cur_need in fiber_groups(p.ops):
             pos = sorted(local[q] for q in cur_need)
