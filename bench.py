@@ -576,10 +576,13 @@ def main():
             "avg_launch_ms": gemm_ms,
         },
         "sweep": {
-            "kernel": "per-program sweep kernels (sweep_codegen + hiprtc; FINAL pass sums each label's "
-                      "branch jobs, labels dispatched heaviest first) (all fragments, per step, this rank)",
-            "bound": "latency / LDS round trips: 1 workgroup (8 waves) per CU at 128 KiB tiles; neither HBM "
-                     "(0.37 GB per step on counters) nor fp64 VALU saturates (profiles/r02_sweep_pmc.json)",
+            "kernel": "per-program sweep kernels (sweep_codegen + hiprtc): shared INIT tiles (one per distinct "
+                      "INIT-slot prefix), FINAL pass on narrowed single-wave tiles summing each label's branch "
+                      "jobs, labels heaviest first, XCD-grouped tile order (all fragments, per step, this rank)",
+            "bound": "VALU issue: the FINAL pass (89% of the sweep) keeps the VALU busy 69% of its cycles, 49% "
+                     "on f64 instructions (mostly adds: the normalised +-1/+-i gate entries fold multiplies "
+                     "away, so flop rates understate it); HBM moves ~0.2 GB per step (counters, "
+                     "profiles/r02b_sweep_pmc.json)",
             "ms_per_step": sweep_ms,
             "branch_jobs": counts["branch_jobs"],
             "hbm_bytes_model": traffic["hbm"],
@@ -601,6 +604,9 @@ def main():
             "fp64_TFs": c["fp64_flops"] / (sweep_ms * 1e-3) / 1e12,
             "fp64_valu_frac": c["fp64_flops"] / (sweep_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
         })
+        for k in ("f64_issue_frac", "valu_busy_frac"):  # SIMD issue cycles over the counted run's step
+            if k in c:
+                line["sweep"][k] = c[k]
     prep = [s.elapsed_time(e) for s, e in pipe.prep_events]
     if prep:
         line["rank_compress_ms"] = sum(prep) / len(prep)  # sweep end -> knit start (transforms, factors, probes)

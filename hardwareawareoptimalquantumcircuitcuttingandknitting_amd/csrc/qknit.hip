@@ -1101,12 +1101,17 @@ __global__ __launch_bounds__(256) void qk_knit_outer_stream_kernel(OuterStreamAr
 // (2^TB - 1)) values each: syc 32 5, K = 2, TB = 16: 2 x 256 per side, 8 KiB). A workgroup stages
 // them in LDS once per task and then streams the task's 2^TB outputs with LDS reads only; a lane's
 // low-byte pext is hoisted out of the loop (its two output bits 0..7 never change). Each wave's 16-B
-// nontemporal stores cover one 1-KiB run, a task one contiguous 2^(TB+3)-byte block. tools/write_ab:
+// stores cover one 1-KiB run, a task one contiguous 2^(TB+3)-byte block. tools/write_ab:
 // 6.5-6.8 TB/s on syc 32 5 (5.0-5.2 ms per 2^32-entry knit), above a grid-stride fill, where the
 // per-output L2 gathers of qk_knit_outer_stream_kernel reach 5.25 (6.55 ms).
 // Range form: outputs [o_begin, o_begin + o_count) (task-aligned) are written to out[o - o_begin]
 // (a rank's contiguous slice of the distribution); kdev (DEVICE int, or NULL) overrides K at run time,
 // and K <= 0 there skips the launch's work entirely (predicated knit, no host sync).
+// Plain 16-B stores: 4% faster than nontemporal ones for this 34 GB write on the same box (tools/write_ab
+// round 3: 6.01 vs 6.26 ms at 16 workgroups per CU; a plain grid-stride fill 6.41, nontemporal 6.75).
+#ifndef QK_OB_NT
+#define QK_OB_NT 0
+#endif
 struct OuterBlockedArgs {
     int K, TB;
     const double* __restrict__ A;
@@ -1176,7 +1181,11 @@ __global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlocked
                     acc.x = fma(av, bv.x, acc.x);
                     acc.y = fma(av, bv.y, acc.y);
                 }
+#if QK_OB_NT
             __builtin_nontemporal_store(acc, reinterpret_cast<d2_t*>(o + 512 * it + 2 * threadIdx.x));
+#else
+            *reinterpret_cast<d2_t*>(o + 512 * it + 2 * threadIdx.x) = acc;
+#endif
         }
     }
 }

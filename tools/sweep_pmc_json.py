@@ -26,6 +26,7 @@ def derive(raw: dict) -> dict:
         "mean_ms": ms, "hbm_bytes": hbm, "hbm_GBs": hbm / dur / 1e9, "fp64_flops": flops,
         "fp64_TFs": flops / dur / 1e12, "f64_wave_instructions": f64,
         "f64_issue_frac": f64 * 4 / (1024 * dur * clk), "valu_wave_instructions": raw["SQ_INSTS_VALU"],
+        "valu_busy_frac": raw["SQ_INSTS_VALU"] * 4 / (1024 * dur * clk),
         "wait_any_frac": raw["SQ_WAIT_ANY"] / wc, "wait_inst_frac": raw["SQ_WAIT_INST_ANY"] / wc,
         "active_frac": raw["SQ_ACTIVE_INST_ANY"] / wc,
         "lds_bank_conflict_frac": raw["SQ_LDS_BANK_CONFLICT"] / max(raw["SQ_LDS_IDX_ACTIVE"], 1.0),
@@ -44,12 +45,18 @@ def main():
     ms = sum(k["mean_ms"] for k in kernels.values())
     hbm = sum(k["hbm_bytes"] for k in kernels.values())
     flops = sum(k["fp64_flops"] for k in kernels.values())
+    # issue fractions over the step: each kernel's SIMD-cycles of (f64 / all) VALU issue (4 cycles per
+    # wave64 instruction) over the step's SIMD-cycles at that kernel's clock
+    simd_cyc = sum(1024 * k["mean_ms"] * 1e-3 * k["effective_clock_GHz"] * 1e9 for k in kernels.values())
+    f64_issue = sum(4 * k["f64_wave_instructions"] for k in kernels.values()) / simd_cyc
+    valu_busy = sum(4 * k["valu_wave_instructions"] for k in kernels.values()) / simd_cyc
     rec = {
         "workload": workload, "kernels": kernels,
         "note": "rocprofv3 --pmc, four passes (FETCH_SIZE; WRITE_SIZE; 8 SQ; 7 SQ + GRBM) over tools/sweep_bench.py; "
                 "derivations in tools/sweep_pmc_json.py",
         "per_step": {"ms": ms, "hbm_bytes": hbm, "hbm_frac_of_8TBs": hbm / (ms * 1e-3) / 8e12, "fp64_flops": flops,
-                     "fp64_frac_of_78.6TF": flops / (ms * 1e-3) / 78.6e12},
+                     "fp64_frac_of_78.6TF": flops / (ms * 1e-3) / 78.6e12, "f64_issue_frac": f64_issue,
+                     "valu_busy_frac": valu_busy},
     }
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec["per_step"]))

@@ -178,6 +178,126 @@ __global__ __launch_bounds__(256) void k_blocked_dyn(int K, const double* __rest
     }
 }
 
+// round 3: the store flavour (nontemporal vs plain) of the fill and of the blocked kernel, and a fill
+// in 2^28-entry launches (the shape of torch's zeros() over the same buffer)
+template <bool NT>
+__global__ __launch_bounds__(256) void k_fill_st(double* __restrict__ out, int64_t total) {
+    const d2_t v = {1.0, 2.0};
+    for (int64_t o = 2 * ((int64_t)blockIdx.x * 256 + threadIdx.x); o < total; o += 2 * (int64_t)gridDim.x * 256) {
+        if (NT)
+            __builtin_nontemporal_store(v, reinterpret_cast<d2_t*>(out + o));
+        else
+            *reinterpret_cast<d2_t*>(out + o) = v;
+    }
+}
+
+template <int TB, bool NT>
+__global__ __launch_bounds__(256) void k_blocked_st(int K, const double* __restrict__ A, const double* __restrict__ B,
+                                                    int64_t ld, uint32_t mA, uint32_t mB, double* __restrict__ out,
+                                                    int64_t total) {
+    constexpr uint32_t LOW = (1u << TB) - 1;
+    __shared__ uint32_t tab[2][2][256];
+    __shared__ double sA[KMAX * 256];
+    __shared__ double sB[KMAX * 256];
+    const uint32_t mAl = mA & LOW, mBl = mB & LOW;
+    const int na = 1 << __builtin_popcount(mAl), nb = 1 << __builtin_popcount(mBl);
+    for (int i = threadIdx.x; i < 512; i += 256) {
+        const int byte = i >> 8, v = i & 255;
+        tab[0][byte][v] = pext32((uint32_t)v << (8 * byte), mAl);
+        tab[1][byte][v] = pext32((uint32_t)v << (8 * byte), mBl);
+    }
+    __syncthreads();
+    const uint32_t r0 = tab[0][0][(2 * threadIdx.x) & 255], c0 = tab[1][0][(2 * threadIdx.x) & 255];
+    const int64_t tasks = total >> TB;
+    for (int64_t t = blockIdx.x; t < tasks; t += gridDim.x) {
+        const uint32_t base = (uint32_t)(t << TB);
+        const uint32_t ah = pext32(base, mA), bh = pext32(base, mB);
+        __syncthreads();
+        for (int i = threadIdx.x; i < K * na; i += 256) sA[i] = A[(i / na) * ld + ah + (i % na)];
+        for (int i = threadIdx.x; i < K * nb; i += 256) sB[i] = B[(i / nb) * ld + bh + (i % nb)];
+        __syncthreads();
+        double* o = out + base;
+#pragma unroll 4
+        for (int it = 0; it < (1 << TB) / 512; ++it) {
+            const uint32_t hi = (uint32_t)(2 * it + (threadIdx.x >> 7));
+            const uint32_t row = r0 + tab[0][1][hi & 255], col = c0 + tab[1][1][hi & 255];
+            d2_t acc = {0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k)
+                if (k < K) {
+                    const double av = sA[k * na + row];
+                    const d2_t bv = *reinterpret_cast<const d2_t*>(sB + k * nb + col);
+                    acc.x = fma(av, bv.x, acc.x);
+                    acc.y = fma(av, bv.y, acc.y);
+                }
+            if (NT)
+                __builtin_nontemporal_store(acc, reinterpret_cast<d2_t*>(o + 512 * it + 2 * threadIdx.x));
+            else
+                *reinterpret_cast<d2_t*>(o + 512 * it + 2 * threadIdx.x) = acc;
+        }
+    }
+}
+
+// round 4 (plain stores): task order (grid-stride or a contiguous task range per workgroup) and store
+// width (WIDE: each lane writes 4 consecutive outputs, two adjacent 16-B stores: a wave covers 2 KiB)
+template <int TB, bool CONTIG, bool WIDE>
+__global__ __launch_bounds__(256) void k_blocked_v4(int K, const double* __restrict__ A, const double* __restrict__ B,
+                                                    int64_t ld, uint32_t mA, uint32_t mB, double* __restrict__ out,
+                                                    int64_t total) {
+    constexpr uint32_t LOW = (1u << TB) - 1;
+    __shared__ uint32_t tab[2][2][256];
+    __shared__ double sA[KMAX * 256];
+    __shared__ double sB[KMAX * 256];
+    const uint32_t mAl = mA & LOW, mBl = mB & LOW;
+    const int na = 1 << __builtin_popcount(mAl), nb = 1 << __builtin_popcount(mBl);
+    for (int i = threadIdx.x; i < 512; i += 256) {
+        const int byte = i >> 8, v = i & 255;
+        tab[0][byte][v] = pext32((uint32_t)v << (8 * byte), mAl);
+        tab[1][byte][v] = pext32((uint32_t)v << (8 * byte), mBl);
+    }
+    __syncthreads();
+    constexpr int PER = WIDE ? 4 : 2;  // outputs per lane per iteration
+    const uint32_t l0 = (PER * threadIdx.x) & 255;
+    const uint32_t r0 = tab[0][0][l0], c0 = tab[1][0][l0];
+    const uint32_t r1 = tab[0][0][l0 + 2], c1 = tab[1][0][l0 + 2];
+    const int64_t tasks = total >> TB;
+    const int64_t per = (tasks + gridDim.x - 1) / gridDim.x;
+    const int64_t t0 = CONTIG ? blockIdx.x * per : blockIdx.x, t1 = CONTIG ? std::min(tasks, t0 + per) : tasks;
+    const int64_t step = CONTIG ? 1 : gridDim.x;
+    for (int64_t t = t0; t < t1; t += step) {
+        const uint32_t base = (uint32_t)(t << TB);
+        const uint32_t ah = pext32(base, mA), bh = pext32(base, mB);
+        __syncthreads();
+        for (int i = threadIdx.x; i < K * na; i += 256) sA[i] = A[(i / na) * ld + ah + (i % na)];
+        for (int i = threadIdx.x; i < K * nb; i += 256) sB[i] = B[(i / nb) * ld + bh + (i % nb)];
+        __syncthreads();
+        double* o = out + base;
+#pragma unroll 4
+        for (int it = 0; it < (1 << TB) / (256 * PER); ++it) {
+            const uint32_t hi = WIDE ? (uint32_t)(4 * it + (threadIdx.x >> 6)) : (uint32_t)(2 * it + (threadIdx.x >> 7));
+            const uint32_t rh = tab[0][1][hi & 255], ch = tab[1][1][hi & 255];
+            d2_t acc = {0.0, 0.0}, acc2 = {0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k)
+                if (k < K) {
+                    const double av = sA[k * na + r0 + rh];
+                    const d2_t bv = *reinterpret_cast<const d2_t*>(sB + k * nb + c0 + ch);
+                    acc.x = fma(av, bv.x, acc.x);
+                    acc.y = fma(av, bv.y, acc.y);
+                    if (WIDE) {
+                        const double av2 = sA[k * na + r1 + rh];
+                        const d2_t bv2 = *reinterpret_cast<const d2_t*>(sB + k * nb + c1 + ch);
+                        acc2.x = fma(av2, bv2.x, acc2.x);
+                        acc2.y = fma(av2, bv2.y, acc2.y);
+                    }
+                }
+            double* dst = o + (int64_t)(256 * PER) * it + PER * threadIdx.x;
+            *reinterpret_cast<d2_t*>(dst) = acc;
+            if (WIDE) *reinterpret_cast<d2_t*>(dst + 2) = acc2;
+        }
+    }
+}
+
 int main(int argc, char** argv) {
     const int K = argc > 1 ? atoi(argv[1]) : 2;
     const int nbits = 32;
@@ -230,7 +350,51 @@ int main(int argc, char** argv) {
         }
         printf("  %s max |err| on samples %.3e\n", name, err);
     };
-    const bool round2 = argc > 2;
+    const bool round2 = argc > 2 && atoi(argv[2]) == 2;
+    const bool round3 = argc > 2 && atoi(argv[2]) == 3;
+    if (argc > 2 && atoi(argv[2]) == 4) {
+        for (int wpc : {8, 16, 32}) {
+            const int G = cus * wpc;
+            char nm[64];
+            snprintf(nm, sizeof nm, "v4 stride wg/cu=%d", wpc);
+            timeit(nm, [&] { hipLaunchKernelGGL((k_blocked_v4<16, false, false>), dim3(G), dim3(256), 0, 0, K, A, B, N, mA, mB, out, total); });
+            if (wpc == 16) check("v4 stride");
+            snprintf(nm, sizeof nm, "v4 contig wg/cu=%d", wpc);
+            timeit(nm, [&] { hipLaunchKernelGGL((k_blocked_v4<16, true, false>), dim3(G), dim3(256), 0, 0, K, A, B, N, mA, mB, out, total); });
+            snprintf(nm, sizeof nm, "v4 stride wide wg/cu=%d", wpc);
+            timeit(nm, [&] { hipLaunchKernelGGL((k_blocked_v4<16, false, true>), dim3(G), dim3(256), 0, 0, K, A, B, N, mA, mB, out, total); });
+            if (wpc == 16) check("v4 stride wide");
+            snprintf(nm, sizeof nm, "v4 contig wide wg/cu=%d", wpc);
+            timeit(nm, [&] { hipLaunchKernelGGL((k_blocked_v4<16, true, true>), dim3(G), dim3(256), 0, 0, K, A, B, N, mA, mB, out, total); });
+        }
+        return 0;
+    }
+    if (round3) {
+        for (int wpc : {8, 16}) {
+            const int G = cus * wpc;
+            char nm[64];
+            snprintf(nm, sizeof nm, "fill nt wg/cu=%d", wpc);
+            timeit(nm, [&] { hipLaunchKernelGGL(k_fill_st<true>, dim3(G), dim3(256), 0, 0, out, total); });
+            snprintf(nm, sizeof nm, "fill plain wg/cu=%d", wpc);
+            timeit(nm, [&] { hipLaunchKernelGGL(k_fill_st<false>, dim3(G), dim3(256), 0, 0, out, total); });
+            snprintf(nm, sizeof nm, "fill nt 16x2^28 wg/cu=%d", wpc);
+            timeit(nm, [&] {
+                for (int c = 0; c < 16; ++c)
+                    hipLaunchKernelGGL(k_fill_st<true>, dim3(G), dim3(256), 0, 0, out + (int64_t(c) << 28), int64_t(1) << 28);
+            });
+            snprintf(nm, sizeof nm, "fill plain 16x2^28 wg/cu=%d", wpc);
+            timeit(nm, [&] {
+                for (int c = 0; c < 16; ++c)
+                    hipLaunchKernelGGL(k_fill_st<false>, dim3(G), dim3(256), 0, 0, out + (int64_t(c) << 28), int64_t(1) << 28);
+            });
+            snprintf(nm, sizeof nm, "blocked16 nt wg/cu=%d", wpc);
+            timeit(nm, [&] { hipLaunchKernelGGL((k_blocked_st<16, true>), dim3(G), dim3(256), 0, 0, K, A, B, N, mA, mB, out, total); });
+            snprintf(nm, sizeof nm, "blocked16 plain wg/cu=%d", wpc);
+            timeit(nm, [&] { hipLaunchKernelGGL((k_blocked_st<16, false>), dim3(G), dim3(256), 0, 0, K, A, B, N, mA, mB, out, total); });
+            if (wpc == 16) check("blocked16 plain");
+        }
+        return 0;
+    }
     for (int wpc : {4, 8, 16}) {
         if (round2) break;
         const int G = cus * wpc;
