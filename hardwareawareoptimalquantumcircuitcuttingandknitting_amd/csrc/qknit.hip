@@ -485,7 +485,8 @@ __device__ __forceinline__ void gemm_load(d2_t (&r)[4], const double* __restrict
 }
 
 #ifndef QK_GEMM_STORE
-#define QK_GEMM_STORE 1  // 0: per-element stores; 1: paired 16-B nt stores; 2: paired 16-B sc1 stores
+#define QK_GEMM_STORE 1  // 0: per-element stores; 1: paired 16-B nt stores; 2: paired 16-B sc1 stores;
+                         // 3: paired 16-B plain stores
 // (LDS-DMA kernel, syc 32 5 contraction: nt 66.1 TF/s, sc1 65.4)
 #endif
 
@@ -506,6 +507,8 @@ __device__ __forceinline__ void gemm_store_pair(double* p, d2_t v) {
     // s_nop 1: a >8-B store's data VGPRs must not be rewritten in the next cycle (the hazard
     // recogniser does not see inside inline asm)
     asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+#elif QK_GEMM_STORE == 3
+    *reinterpret_cast<d2_t*>(p) = v;
 #else
     __builtin_nontemporal_store(v, reinterpret_cast<d2_t*>(p));
 #endif

@@ -235,7 +235,65 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
         cnorm2 = m;
     }
     __syncthreads();
-    if (ok && rb > 1 && side == 0) {  // wave 0 alone: rounds are ordered by the wave's own LDS traffic
+    if (ok && rb > 1 && ra <= 8 && rb <= 8 && side == 0) {
+        // Register form for cores of at most 8 x 8 (syc 32 5: the common case): lane 8 j + i holds
+        // C[i][j] and W[i][j]; a round's partner column comes by one ds_bpermute per matrix and the
+        // column sums by 3-step DPP reductions over the column's 8 lanes, so a round is a short
+        // register chain instead of LDS round trips (same rotations, same pairing, same stopping rule
+        // as the LDS form below)
+        const int i = lane & 7, j = lane >> 3;
+        const double floor2 = 1e-30 * cnorm2;
+        double c = (i < ra && j < rb) ? C[i][j] : 0.0;
+        double w = (i < rb && j < rb) ? W[i][j] : 0.0;
+        const int n = rb + (rb & 1);
+        auto perm = [](double v, int src_lane) {
+            int2 x = *reinterpret_cast<int2*>(&v);
+            x.x = __builtin_amdgcn_ds_bpermute(src_lane << 2, x.x);
+            x.y = __builtin_amdgcn_ds_bpermute(src_lane << 2, x.y);
+            return *reinterpret_cast<double*>(&x);
+        };
+        for (int sweep = 0; sweep < RK_MAX_SWEEPS; ++sweep) {
+            bool rot = false;
+            for (int round = 0; round < n - 1; ++round) {
+                // partner of column j in this round (the LDS form's round-robin pairs)
+                int pj;
+                if (j == n - 1) pj = round;
+                else if (j == round) pj = n - 1;
+                else pj = (2 * round - j + 2 * (n - 1)) % (n - 1);
+                const bool live = j < n && pj < rb && j < rb;
+                const int src = (pj & 7) * 8 + i;
+                const double cq = perm(c, src), wq = perm(w, src);
+                double own = c * c, oth = cq * cq, cross = c * cq;
+                own += dppd<DPP_XOR1>(own);
+                oth += dppd<DPP_XOR1>(oth);
+                cross += dppd<DPP_XOR1>(cross);
+                own += dppd<DPP_XOR2>(own);
+                oth += dppd<DPP_XOR2>(oth);
+                cross += dppd<DPP_XOR2>(cross);
+                own += dppd<DPP_HALF_MIRROR>(own);
+                oth += dppd<DPP_HALF_MIRROR>(oth);
+                cross += dppd<DPP_HALF_MIRROR>(cross);
+                const bool lo = j < pj;  // column p of the pair (p < q)
+                const double al = lo ? own : oth, be = lo ? oth : own, ga = cross;
+                if (live && ga != 0.0 && fabs(ga) > 1e-13 * sqrt(al * be) && fmax(al, be) > floor2) {
+                    const double zeta = (be - al) * 0.5 * rcp_d(ga);
+                    const double ww = 1.0 + zeta * zeta;
+                    const double tt = copysign(rcp_d(fabs(zeta) + ww * rsq_d(ww)), zeta);
+                    const double cs = rsq_d(1.0 + tt * tt), sn = cs * tt;
+                    // p: c' = cs c_p - sn c_q;  q: c' = sn c_p + cs c_q
+                    c = lo ? cs * c - sn * cq : sn * cq + cs * c;
+                    w = lo ? cs * w - sn * wq : sn * wq + cs * w;
+                    rot = true;
+                }
+            }
+#ifdef QK_RANK_DEBUG
+            if (lane == 0) qk_rank_dbg[5] = sweep + 1;
+#endif
+            if (!__any(rot)) break;
+        }
+        if (i < ra && j < rb) C[i][j] = c;
+        if (i < rb && j < rb) W[i][j] = w;
+    } else if (ok && rb > 1 && side == 0) {  // wave 0 alone: rounds are ordered by the wave's own LDS traffic
         const double floor2 = 1e-30 * cnorm2;
         const int n = rb + (rb & 1), npair = n / 2;
         int tpp = 64 / npair;
