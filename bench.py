@@ -335,9 +335,12 @@ def north_star_sweep(steps: int) -> dict:
     """BASELINE.json north-star target: the batched statevector sweep for syc 32 1 at p=2 on one
     MI355X against the HBM roofline. Per variant (the reference cut: 0 cuts, 2 instances; the
     forced 4-cut variant: the full 4^k instance batch) the sweep of every fragment is timed alone
-    with HIP events on the launch stream; ``roofline_frac`` = SURVEY.md §8d algorithmic bytes (one
-    read + write of the complex128 state per fused op per branch job) / time / 8 TB/s, and
-    ``hbm_frac`` the same for the bytes the kernels actually move (modelled)."""
+    with HIP events on the launch stream. ``hbm_frac``: the bytes the kernels actually move (modelled,
+    DESIGN.md §3) / time / 8 TB/s. ``model_bytes_frac``: SURVEY.md §8d's per-gate algorithmic bytes
+    (one read + write of the complex128 state per fused op per branch job) on the same scale — a
+    model, not a ceiling (a pass touches the state once for all its gates, so it exceeds 1). With
+    one or a few 16-qubit instances the sweep is latency-bound: two dependent launches (INIT, FINAL)
+    of a few microseconds each, ~1 MB of state."""
     import torch
 
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
@@ -380,10 +383,11 @@ def north_star_sweep(steps: int) -> dict:
             "ms_per_sweep": ms,
             "launch": launch,
             "ms_by_launch": ways,
-            "algorithmic_bytes": tr["algorithmic"],
-            "roofline_frac": tr["algorithmic"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "bound": "latency (2 dependent launches, single-instance 16-qubit fragments)",
             "hbm_bytes": tr["hbm"],
             "hbm_frac": tr["hbm"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "algorithmic_bytes_model": tr["algorithmic"],
+            "model_bytes_frac": tr["algorithmic"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
         }
         del pipe
         torch.cuda.empty_cache()

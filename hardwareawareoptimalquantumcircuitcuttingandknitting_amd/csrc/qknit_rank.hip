@@ -127,32 +127,28 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
 
     const int tid = threadIdx.x, lane = tid & 63, side = tid >> 6, K = a.K;
     RK_STAMP(0)
-    {  // raw copy with 16 loads in flight per thread (a serial load chain cost ~20 us), then symmetrise
-        const int n = 2 * K * K;
-        for (int e0 = tid; e0 < n; e0 += RK_THREADS * 16) {
+    {  // raw copy, wave w on rows w*16.. of [GA; GB] (lane = column), 16 loads in flight per lane and no
+       // integer division in the index math (the divide-by-K form cost ~10 us); the symmetrisation
+       // 0.5 (G + G^T) happens where the Cholesky reads a column
+        const int wv = tid >> 6;
+        for (int r0 = wv * 16; r0 < 2 * K; r0 += 32) {
             double v[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-                const int e = e0 + u * RK_THREADS;
-                v[u] = e < n ? (e < K * K ? a.GA[e] : a.GB[e - K * K]) : 0.0;
+                const int rr = r0 + u;
+                v[u] = (rr < 2 * K && lane < K) ? (rr < K ? a.GA[rr * K + lane] : a.GB[(rr - K) * K + lane]) : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-                const int e = e0 + u * RK_THREADS;
-                if (e < n) G[e / (K * K)][(e / K) % K][e % K] = v[u];
+                const int rr = r0 + u;
+                if (rr < 2 * K && lane < K) {
+                    const int s = rr >= K ? 1 : 0;
+                    G[s][rr - s * K][lane] = v[u];
+                }
             }
         }
         __syncthreads();
         RK_STAMP(4)
-        for (int e = tid; e < n; e += RK_THREADS) {
-            const int s = e / (K * K), i = (e / K) % K, j = e % K;
-            if (i < j) {
-                const double m = 0.5 * (G[s][i][j] + G[s][j][i]);
-                G[s][i][j] = m;
-                G[s][j][i] = m;
-            }
-        }
-        __syncthreads();
     }
 
     // ---- 1. pivoted Cholesky, wave `side` on Gram `side`, lane = row
@@ -182,7 +178,7 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
                 if (!(dp > 0.0)) {
                     active = false;
                 } else {
-                    double s = lane < K ? G[side][lane][p] : 0.0;
+                    double s = lane < K ? 0.5 * (G[side][lane][p] + G[side][p][lane]) : 0.0;
                     for (int i = 0; i < j; ++i) s -= L[side][lane][i] * L[side][p][i];
                     const double col = lane < K ? s / sqrt(dp) : 0.0;
                     if (lane < K) L[side][lane][j] = col;

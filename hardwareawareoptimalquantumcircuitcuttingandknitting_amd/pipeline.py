@@ -1157,7 +1157,9 @@ class KnitPipeline:
         from . import sweep_plan
 
         hbm = alg = flops = 0
-        for fs, sw in zip(self.frags, self.sweeps):
+        shared = dict(zip(getattr(self, "_multi", None)[0], getattr(self.be, "shared_init", None) or [])) \
+            if getattr(self, "_multi", None) is not None else {}
+        for i, (fs, sw) in enumerate(zip(self.frags, self.sweeps)):
             if sw is None or not sw["n_jobs"]:
                 continue
             enc = fs.dprog.enc if getattr(fs, "dprog", None) is not None else sweep_plan.encode(fs.prog)
@@ -1166,7 +1168,9 @@ class KnitPipeline:
             if enc.packed or P == 1:
                 per_job = out
             elif P == 2:
-                per_job = 2 * tile + out
+                # shared INIT prefixes: the INIT tiles are written once per prefix, each job's FINAL
+                # pass reads its prefix's tile (L2 / MALL re-reads counted as HBM here)
+                per_job = tile + out + (tile * shared[i] // J if shared.get(i) else tile)
             else:
                 per_job = 2 * tile + S + (P - 3) * 2 * S + S + out
             if sw.get("fused"):  # FINAL pass sums a label's jobs: one row per label, no reduction
