@@ -239,49 +239,64 @@ __global__ __launch_bounds__(256) void qk_prep_reduce_kernel(const double* __res
     if (grp == 0 && dst) *dst = (acc[0][lane] + acc[1][lane]) + (acc[2][lane] + acc[3][lane]);
 }
 
-// out[j][c] = sum_k T[j][k] X[k][c] for j < rmax, both sides (blockIdx.y); columns per thread
+// out[j][c] = sum_k T[j][k] X[k][c] for j < rmax, both sides (blockIdx.y). A workgroup takes 64 columns;
+// its four waves split K in quarters (16 rows each: every load of a thread in flight at once) and sum
+// their partial products through LDS in a fixed order: one memory latency per column block instead of
+// K / 16 in a row (32 -> ~10 us on syc 32 5; the 1/8-width blocks of an 8-rank slice were as slow)
 __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const double* __restrict__ TA,
                                                           const double* __restrict__ XA, int64_t NA,
                                                           double* __restrict__ A2, const double* __restrict__ TB,
                                                           const double* __restrict__ XB, int64_t NB,
                                                           double* __restrict__ B2) {
     __shared__ double T[8][PK];
+    __shared__ double part[4][8][64];
     const bool bs = blockIdx.y == 1;
     const double* Tg = bs ? TB : TA;
     const double* X = bs ? XB : XA;
     double* out = bs ? B2 : A2;
     const int64_t N = bs ? NB : NA;
+    const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
     for (int e = threadIdx.x; e < rmax * K; e += 256) T[e / K][e % K] = Tg[e];
     __syncthreads();
-    for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < N; c += (int64_t)gridDim.x * 256) {
-        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int k0 = 0; k0 < K; k0 += 16) {  // 16 loads in flight per thread
-            double xv[16];
+    for (int64_t c0 = (int64_t)blockIdx.x * 64; c0 < N; c0 += (int64_t)gridDim.x * 64) {
+        const int64_t c = c0 + l;
+        double xv[16];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) xv[u] = k0 + u < K ? X[(int64_t)(k0 + u) * N + c] : 0.0;
-#pragma unroll
-            for (int u = 0; u < 16; ++u)
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (j < rmax && k0 + u < K) acc[j] = fma(T[j][k0 + u], xv[u], acc[j]);
+        for (int u = 0; u < 16; ++u) {
+            const int k = 16 * q + u;
+            xv[u] = (k < K && c < N) ? X[(int64_t)k * N + c] : 0.0;
         }
+        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (j < rmax) out[(int64_t)j * N + c] = acc[j];
+        for (int u = 0; u < 16; ++u)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < rmax && 16 * q + u < K) acc[j] = fma(T[j][16 * q + u], xv[u], acc[j]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part[q][j][l] = acc[j];
+        __syncthreads();
+        for (int e = threadIdx.x; e < 8 * 64; e += 256) {
+            const int j = e >> 6, cc = e & 63;
+            if (j < rmax && c0 + cc < N)
+                out[(int64_t)j * N + c0 + cc] = (part[0][j][cc] + part[1][j][cc]) + (part[2][j][cc] + part[3][j][cc]);
+        }
+        __syncthreads();
     }
 }
 
-constexpr int PV_GRID = 32;  // workgroups of the V = B'' P^T partial sums
+constexpr int PV_GRID = 32;   // workgroups of the V = B'' P^T partial sums (probe_d sums their partials)
+constexpr int PV_WAVES = 16;  // waves per workgroup: 512 column ranges in flight (4 waves: 27 us, latency)
 
 // V partials: vpart[b][j][p] = sum over this workgroup's columns c of B2[j][c] P[p][c] (j < rmax)
-__global__ __launch_bounds__(256) void qk_probe_v_kernel(int rmax, const double* __restrict__ B2, int64_t ldb2,
-                                                         int64_t NB, const double* __restrict__ P, int64_t ldp,
-                                                         double* __restrict__ vpart) {
-    __shared__ double red[4][256];
+__global__ __launch_bounds__(64 * PV_WAVES) void qk_probe_v_kernel(int rmax, const double* __restrict__ B2,
+                                                                  int64_t ldb2, int64_t NB,
+                                                                  const double* __restrict__ P, int64_t ldp,
+                                                                  double* __restrict__ vpart) {
+    __shared__ double red[PV_WAVES][256];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, l4 = lane >> 4;
     d4_t acc = {0, 0, 0, 0};
     // this wave's contiguous column range, 8 k-steps (32 columns) per batch, loads issued first
-    const int64_t nw = (int64_t)gridDim.x * 4, w = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t nw = (int64_t)gridDim.x * PV_WAVES, w = (int64_t)blockIdx.x * PV_WAVES + wave;
     const int64_t per = ((NB / 4 + nw - 1) / nw) * 4;
     const int64_t cb = w * per, ce = cb + per < NB ? cb + per : NB;
     for (int64_t c0 = cb; c0 < ce; c0 += 32) {
@@ -299,7 +314,16 @@ __global__ __launch_bounds__(256) void qk_probe_v_kernel(int rmax, const double*
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) red[wave][(l4 + 4 * rr) * 16 + l16] = acc[rr];
     __syncthreads();
-    vpart[(int64_t)blockIdx.x * 256 + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    if (tid < 256) {  // fixed-order pairwise sum over the waves
+        double s[PV_WAVES];
+#pragma unroll
+        for (int v = 0; v < PV_WAVES; ++v) s[v] = red[v][tid];
+#pragma unroll
+        for (int h = PV_WAVES / 2; h >= 1; h >>= 1)
+#pragma unroll
+            for (int v = 0; v < h; ++v) s[v] += s[v + h];
+        vpart[(int64_t)blockIdx.x * 256 + tid] = s[0];
+    }
 }
 
 // e2 partials over 16-column blocks of A: d = X_A^T U - A2^T V, epart[b][p] = sum of d[c][p]^2
@@ -442,8 +466,8 @@ int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const d
     if (!TA || !XA || !A2 || !TB || !XB || !B2) return fail(ctx, QK_EARG, "qk_compress_operands: null buffer");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_compress_operands: hipSetDevice");
     const int64_t N = NA > NB ? NA : NB;
-    int64_t gx = (N + 255) / 256;
-    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 4;
+    int64_t gx = (N + 63) / 64;
+    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 8;
     gx = gx < cap ? gx : cap;
     hipLaunchKernelGGL(qk_compress_kernel, dim3((unsigned)gx, 2), dim3(256), 0, ctx->stream, K, rmax, TA, XA, NA, A2,
                        TB, XB, NB, B2);
@@ -475,7 +499,7 @@ int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx,
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_probe_errors: hipSetDevice");
     double* vpart = work;
     double* epart = work + PV_GRID * 256;
-    hipLaunchKernelGGL(qk_probe_v_kernel, dim3(PV_GRID), dim3(256), 0, ctx->stream, rmax, B2, ldb2, NB, probes, ldp,
+    hipLaunchKernelGGL(qk_probe_v_kernel, dim3(PV_GRID), dim3(64 * PV_WAVES), 0, ctx->stream, rmax, B2, ldb2, NB, probes, ldp,
                        vpart);
     hipLaunchKernelGGL(qk_probe_d_kernel, dim3(gd), dim3(256), 0, ctx->stream, K, rmax, XA, ldx, NA, A2, lda2, U, vpart,
                        PV_GRID, epart);

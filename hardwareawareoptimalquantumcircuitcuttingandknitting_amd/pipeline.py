@@ -356,6 +356,13 @@ class KnitPipeline:
         self.dev_rank = bool(self.data_rank and cA is not None and self.ops.num_terms <= 64
                              and hasattr(self.be, "rank_factors"))
         self._pending = []  # device (rank, accepted) of steps not yet read back
+        # slice mode, fused preparation: every rank factors the same all-reduced Grams with the same
+        # deterministic kernel, so no broadcast of the factors, and each rank checks the rows of R its
+        # own slice holds (this rank's A columns against every probe) and decides for its slice alone
+        # (a rejection takes the exact contraction of that slice only): two collectives fewer per step.
+        # Factors that differed between ranks would mix compressed columns and fail the local check.
+        # QKNIT_SLICE_SYNC=1: rank 0's factors broadcast, probe errors summed over ranks (one decision).
+        self.slice_sync = os.environ.get("QKNIT_SLICE_SYNC", "0") == "1"
         self.last_kernel = None  # kernel of the last compressed contraction (None: qk_gemm_keyed)
         self.last_prep = None  # data-rank preparation of the last step: "fused" (qk_prep_operands) or "torch"
         self._probe = None
@@ -805,11 +812,12 @@ class KnitPipeline:
             U = red[2 * K * K:].view(K, npr).contiguous()
             TA, TB, r = be.rank_factors(G[0].contiguous(), G[1].contiguous())
             R8 = TA.shape[0]
-            fac = T.cat([TA.reshape(-1), TB.reshape(-1), r.to(T.float64)])
-            dist.broadcast(fac, src=self._group_rank0(), group=self.group)
-            TA = fac[:R8 * K].view(R8, K)
-            TB = fac[R8 * K:2 * R8 * K].view(R8, K)
-            r = fac[-1:].to(T.int32)
+            if self.slice_sync:
+                fac = T.cat([TA.reshape(-1), TB.reshape(-1), r.to(T.float64)])
+                dist.broadcast(fac, src=self._group_rank0(), group=self.group)
+                TA = fac[:R8 * K].view(R8, K)
+                TB = fac[R8 * K:2 * R8 * K].view(R8, K)
+                r = fac[-1:].to(T.int32)
             A2l, B2l = be.compress(TA.contiguous(), XA, TB.contiguous(), XB)
             loc = T.cat([A2l.reshape(-1), B2l.reshape(-1)])
         else:
@@ -838,7 +846,8 @@ class KnitPipeline:
         if self._fused_prep(qs):
             # this rank's A columns against all probes (B2 / probes: every column), summed over ranks
             e2, _, _ = be.probe_errors(XA, A2, U, B2, x_full.contiguous(), a2_cols=(self.rank * bwA, bwA))
-            dist.all_reduce(e2, group=self.group)
+            if self.slice_sync:
+                dist.all_reduce(e2, group=self.group)
             k_eff, _ = be.probe_accept(e2, r, self.rank_tol)
             self._pending.append((r, k_eff))
         else:
