@@ -372,3 +372,32 @@ def test_init_prefixes_share_init_tiles():
         enc = sweep_plan.encode(fs.prog, tile_bits=12)
         if enc.packed or len(enc.passes) != 2:
             assert engine.init_prefixes(enc, fs.jobs) is None
+
+
+@pytest.mark.parametrize("drop", ["1", "0"])
+def test_narrow_final_tile_and_dropped_phases_emulated(monkeypatch, drop):
+    """A syc 32 5 fragment encoded for the per-program kernels as the GPU runs it — 13-bit INIT tile,
+    FINAL pass narrowed to 10 bits (sweep_plan.narrow_final_tile), trailing unit-modulus diagonals
+    dropped or kept (QKNIT_DROP_PHASES) — through the emulator vs the oracle."""
+    monkeypatch.setenv("QKNIT_DROP_PHASES", drop)
+    _, cut = cutting.config_cut_circuit("syc", 32, 5, 2)[:2]
+    virt = VirtualCircuit(cut)
+    view = qvm.CutView(cut)
+    cl = engine.clbit_indexer(virt.circuit)
+    frag, fcirc = list(virt.fragment_circuits.items())[1]
+    prog = compile_fragment(fcirc, frag, cl)
+    all_labels = virt.get_instance_labels(frag)
+    labels = [all_labels[3], all_labels[777]]
+    jobs = build_jobs(prog, labels)
+    enc = sweep_plan.encode(prog, tile_bits=13, final_tile_bits=10)
+    assert [enc.pass_tile_bits(i) for i in range(len(enc.passes))] == [13, 10]
+    kept = len(sweep_plan.drop_trailing_phases(prog).ops)
+    assert (kept < len(prog.ops)) == (drop == "1")
+    p = emulate(enc, jobs.slot_mats, jobs.sign)
+    offs = jobs.label_offsets
+    q = np.stack([p[offs[i]:offs[i + 1]].sum(0) for i in range(len(labels))])
+    from oracle.statevector import simulate
+    for li, label in enumerate(labels):
+        d = simulate(view.instance_ops(list(frag), label), len(frag))
+        ref = dense.fold(d, view.num_clbits, prog.clbits)
+        np.testing.assert_allclose(q[li], ref, atol=1e-13, rtol=0)
