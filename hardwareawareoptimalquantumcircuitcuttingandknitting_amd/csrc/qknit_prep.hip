@@ -256,7 +256,13 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
     double* out = bs ? B2 : A2;
     const int64_t N = bs ? NB : NA;
     const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
-    for (int e = threadIdx.x; e < rmax * K; e += 256) T[e / K][e % K] = Tg[e];
+    {  // T (at most 8 x 64): both loads of a thread in flight together (a load-wait loop here cost a
+       // memory latency per iteration in every workgroup)
+        const int n = rmax * K, e0 = threadIdx.x, e1 = threadIdx.x + 256;
+        const double t0 = e0 < n ? Tg[e0] : 0.0, t1 = e1 < n ? Tg[e1] : 0.0;
+        if (e0 < n) T[e0 / K][e0 % K] = t0;
+        if (e1 < n) T[e1 / K][e1 % K] = t1;
+    }
     __syncthreads();
     for (int64_t c0 = (int64_t)blockIdx.x * 64; c0 < N; c0 += (int64_t)gridDim.x * 64) {
         const int64_t c = c0 + l;
@@ -381,8 +387,15 @@ __global__ __launch_bounds__(256) void qk_probe_accept_kernel(const double* __re
                                                               double* __restrict__ err_out) {
     __shared__ double acc[256];
     const int tid = threadIdx.x, p = tid % PNP;
-    double s = 0.0;
-    for (int b = tid / PNP; b < n; b += 256 / PNP) s += epart[(int64_t)b * PNP + p];
+    // eight independent partial sums (loads in flight together), combined in a fixed order
+    constexpr int STEP = 256 / PNP;
+    double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int b = tid / PNP;
+    for (; b + 7 * STEP < n; b += 8 * STEP)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s8[u] += epart[(int64_t)(b + u * STEP) * PNP + p];
+    for (; b < n; b += STEP) s8[0] += epart[(int64_t)b * PNP + p];
+    const double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     acc[tid] = s;
     __syncthreads();
     for (int w = 128; w >= PNP; w >>= 1) {
@@ -467,7 +480,7 @@ int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const d
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_compress_operands: hipSetDevice");
     const int64_t N = NA > NB ? NA : NB;
     int64_t gx = (N + 63) / 64;
-    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 8;
+    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 2;  // x 2 sides: 4 workgroups per CU
     gx = gx < cap ? gx : cap;
     hipLaunchKernelGGL(qk_compress_kernel, dim3((unsigned)gx, 2), dim3(256), 0, ctx->stream, K, rmax, TA, XA, NA, A2,
                        TB, XB, NB, B2);

@@ -49,6 +49,14 @@ def main():
     timed("compress_operands", lambda: engine.compress_operands(ctx, TA, XA, TB, XB))
     timed("probe_errors (v, d, accept)", lambda: engine.probe_errors(ctx, XA, A2, U, B2, P, r=r, tol=1e-14))
     timed("rank_factors", lambda: engine.rank_factors_device(ctx, GA, GB))
+    # the same compress on a non-power-of-two row length (row stride N + 64 doubles): a much lower
+    # time per byte would point at HBM channel camping of the 2^19-byte row stride
+    XAp, XBp = (torch.randn(K, N + 64, dtype=torch.float64, device="cuda", generator=g) for _ in range(2))
+    timed("compress_operands N+64", lambda: engine.compress_operands(ctx, TA, XAp, TB, XBp))
+    XAq, XBq = (torch.randn(K, N + 512, dtype=torch.float64, device="cuda", generator=g) for _ in range(2))
+    timed("compress_operands N+512", lambda: engine.compress_operands(ctx, TA, XAq, TB, XBq))
+    XAh, XBh = (torch.randn(K, N // 2, dtype=torch.float64, device="cuda", generator=g) for _ in range(2))
+    timed("compress_operands N/2", lambda: engine.compress_operands(ctx, TA, XAh, TB, XBh))
     z = torch.zeros(1, dtype=torch.float64, device="cuda")
     timed("torch add_ (1 element)", lambda: z.add_(1.0))
 
