@@ -34,8 +34,12 @@ def run(key, steps):
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
 
-    name, n, d, p, var = cutting.BASELINE_CONFIGS[key]
-    _, cut, desc = cutting.config_cut_circuit(name, n, d, p, var)
+    # "KEY@sS": the same config on the generator seed S instead of the default (e.g. syc_32_5_p2@s7:
+    # whether the data rank the headline relies on is particular to one circuit)
+    base, _, sd = key.partition("@s")
+    seed = int(sd) if sd else None
+    name, n, d, p, var = cutting.BASELINE_CONFIGS[base]
+    _, cut, desc = cutting.config_cut_circuit(name, n, d, p, var, seed=seed)
     virt = VirtualCircuit(cut)
     factored = len(virt.vgate_instructions) > 0
     pipe = KnitPipeline(virt, factored=factored)
@@ -57,7 +61,8 @@ def run(key, steps):
     tr = pipe.sweep_traffic()
     counts = pipe.instance_counts()
     row = {
-        "config": key, "workload": f"{name} {n} {d} p={p}" + (" (forced cuts)" if var == "forced" else ""),
+        "config": key, "workload": f"{name} {n} {d} p={p}" + (" (forced cuts)" if var == "forced" else "")
+        + (f" (seed {seed})" if seed is not None else ""),
         "cuts": desc, "instances_ref": counts["instances_ref"], "branch_jobs": counts["branch_jobs"],
         "knit": "factored" if factored else "direct", "gemm_mnk": [M, N, K],
         "instances_per_s": counts["instances_ref"] / wall, "full_knit_ms": wall * 1e3,
@@ -65,6 +70,8 @@ def run(key, steps):
         "sweep_hbm_frac": tr["hbm"] / (sweep_ms * 1e-3) / 1e9 / HBM if sweep_ms > 0 else None,
     }
     row["data_rank"] = pipe.data_rank
+    row["light_cone_terms"] = counts.get("labels")
+    row["rank_fallbacks"] = getattr(pipe, "rank_fallbacks", None)
     row["knit_kernel"] = pipe.last_kernel or "qk_gemm_keyed (smallk / glds / keyed by shape)"
     if K > 8:
         row["knit_mfma_frac"] = 2.0 * M * N * K / (knit_ms * 1e-3) / 1e12 / MFMA
