@@ -303,12 +303,13 @@ def test_syc_32_full_knit_equals_uncut(T, depth, variant, factored):
     T.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("factored", [False, True])
-def test_gather_mode_through_rccl_single_rank(T, factored):
+@pytest.mark.parametrize("factored,data_rank", [(False, None), (True, None), (True, True)])
+def test_gather_mode_through_rccl_single_rank(T, factored, data_rank):
     """The multi-GPU gather path (job-dealt rows, all_to_all of the row side, all_gather of the
     column side, output-row block contraction) on the HIP backend with a real RCCL
     process group of world size 1 (the only size one GPU allows; 2-4 ranks run under gloo in
-    test_distributed.py)."""
+    test_distributed.py); with data_rank=True the per-step compression of the row block (forced on
+    for these small outputs) must give the exact contraction's result."""
     import socket
 
     import torch.distributed as dist
@@ -325,7 +326,8 @@ def test_gather_mode_through_rccl_single_rank(T, factored):
     try:
         for name in ("cx_3cuts", "three_wide", "move_gate", "hwe_16_1_p3"):
             _, cut = CASES[name]()
-            pipe = KnitPipeline(VirtualCircuit(cut), factored=factored, rank=0, world=1, mode="gather")
+            pipe = KnitPipeline(VirtualCircuit(cut), factored=factored, rank=0, world=1, mode="gather",
+                                data_rank=data_rank)
             res = pipe.step().cpu().numpy()
             cls = pipe.ops.clbits
             kA = deposit_keys(cls[pipe.order[0]])
