@@ -596,8 +596,8 @@ def main():
             "fp64_flops_model": traffic["flops"],
         },
     }
-    cnt = sweep_counters(line["config"]["workload"])
-    if cnt is not None:  # counter bytes / flops per step, over this run's sweep time
+    cnt = sweep_counters(line["config"]["workload"]) if world == 1 else None
+    if cnt is not None:  # counter bytes / flops per step (one GPU's whole sweep), over this run's sweep time
         src, c = cnt
         line["sweep"].update({
             "counters": src,
