@@ -533,7 +533,10 @@ def generate_multi(encs: list) -> tuple[str, list]:
         name = f"qk_sweepm_{key}_r{r}"
         names.append(name)
         tb = encs[members[0]].pass_tile_bits(r)
-        body.append(f'extern "C" __global__ __launch_bounds__({1 << (tb - 4)}) void {name}(qk_multi_args a) {{')
+        # QKNIT_SWEEP_WAVES_PER_EU: minimum waves per SIMD the compiler must fit (register budget)
+        wpe = os.environ.get("QKNIT_SWEEP_WAVES_PER_EU")
+        lb = f"{1 << (tb - 4)}, {int(wpe)}" if wpe else f"{1 << (tb - 4)}"
+        body.append(f'extern "C" __global__ __launch_bounds__({lb}) void {name}(qk_multi_args a) {{')
         body.append(f"    __shared__ double2 lds[{1 << tb}];")
         body.append("    const long long b = blockIdx.x;")
         # caller-ordered blocks (qk_sweep_compiled_multi block_maps): program << 56 | block in its range;
