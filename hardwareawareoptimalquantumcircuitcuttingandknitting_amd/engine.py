@@ -751,7 +751,15 @@ def _compress_core(transforms: list, terms: int, tol: float = 1e-10):
     r = int((S > tol * S[0]).sum()) if S.size and S[0] > 0 else 0
     if r == 0 or r >= terms:
         return transforms, terms
-    return [np.ascontiguousarray((U[:, :r] * S[:r]).T), np.ascontiguousarray(Vt[:r])], r
+    T0, T1 = np.ascontiguousarray((U[:, :r] * S[:r]).T), np.ascontiguousarray(Vt[:r])
+    # once per plan: the truncated core against the untruncated product, entry by entry (the per-step
+    # probe check compares against operands that already went through this core, so it cannot see
+    # this truncation). The dropped part has spectral norm S[r] <= tol S[0], which bounds every entry;
+    # anything larger means the SVD went wrong: keep the uncompressed transforms.
+    err = float(np.abs(C - T0.T @ T1).max())
+    if not err <= 4 * tol * S[0] + 64 * np.finfo(np.float64).eps * float(np.abs(C).max()):
+        return transforms, terms
+    return [T0, T1], r
 
 
 def data_rank_factors(GA: np.ndarray, GB: np.ndarray, **kw):

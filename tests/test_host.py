@@ -401,3 +401,21 @@ def test_narrow_final_tile_and_dropped_phases_emulated(monkeypatch, drop):
         d = simulate(view.instance_ops(list(frag), label), len(frag))
         ref = dense.fold(d, view.num_clbits, prog.clbits)
         np.testing.assert_allclose(q[li], ref, atol=1e-13, rtol=0)
+
+
+def test_core_compression_verified_against_untruncated_core():
+    """engine._compress_core (transforms [terms, swept rows] per fragment): a rank-5 core W_0^T W_1 is
+    compressed to 5 terms that reproduce it entry by entry; with a coarse tolerance on a full-rank core
+    the truncation stays within its stated bound (4 tol S_0) or the transforms come back unchanged."""
+    rng = np.random.default_rng(5)
+    W0 = rng.standard_normal((96, 40))
+    W1 = rng.standard_normal((96, 5)) @ rng.standard_normal((5, 30))
+    (T0, T1), r = engine._compress_core([W0, W1], 96)
+    C = W0.T @ W1
+    assert r == 5 and T0.shape == (5, 40) and T1.shape == (5, 30)
+    np.testing.assert_allclose(T0.T @ T1, C, atol=1e-9 * np.abs(C).max(), rtol=0)
+    W1 = rng.standard_normal((96, 30))
+    C = W0.T @ W1
+    (T0, T1), r = engine._compress_core([W0, W1], 96, tol=0.5)
+    S = np.linalg.svd(C, compute_uv=False)
+    assert r < 30 and np.abs(C - T0.T @ T1).max() <= 4 * 0.5 * S[0]
