@@ -241,8 +241,8 @@ __global__ __launch_bounds__(256) void qk_prep_reduce_kernel(const double* __res
 
 // out[j][c] = sum_k T[j][k] X[k][c] for j < rmax, both sides (blockIdx.y). A workgroup takes 64 columns;
 // its four waves split K in quarters (16 rows each: every load of a thread in flight at once) and sum
-// their partial products through LDS in a fixed order: one memory latency per column block instead of
-// K / 16 in a row (32 -> ~10 us on syc 32 5; the 1/8-width blocks of an 8-rank slice were as slow)
+// their partial products through LDS in a fixed order. 31 us for syc 32 5's two 64 x 2^16 operands (72 MB:
+// ~2.3 TB/s, linear in the column count); two columns per lane with 16-B loads measured slower (35 us)
 __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const double* __restrict__ TA,
                                                           const double* __restrict__ XA, int64_t NA,
                                                           double* __restrict__ A2, const double* __restrict__ TB,

@@ -741,6 +741,21 @@ def test_prep_operands_matches_torch(T, K, RA, RB, NA, NB):
             engine.prep_operands(ctx, WtA[:, :5].contiguous(), qA, WtB[:, :5].contiguous(), qB, P)
 
 
+@pytest.mark.parametrize("K,NA,NB", [(64, 4096, 1001), (24, 129, 8192), (64, 65536, 65536)])
+def test_compress_operands_matches_torch(T, K, NA, NB):
+    """qk_compress_operands against torch: even and odd column counts (rows not 16-B aligned), ragged
+    last column blocks, K below 64."""
+    ctx = engine.get_context(0)
+    g = T.Generator(device="cuda").manual_seed(K + NA + NB)
+    TA, TB = (T.randn(8, K, dtype=T.float64, device="cuda", generator=g) for _ in range(2))
+    XA = T.randn(K, NA, dtype=T.float64, device="cuda", generator=g)
+    XB = T.randn(K, NB, dtype=T.float64, device="cuda", generator=g)
+    A2, B2 = engine.compress_operands(ctx, TA, XA, TB, XB)
+    T.cuda.synchronize()
+    for got, ref in ((A2, TA @ XA), (B2, TB @ XB)):
+        assert float((got - ref).abs().max()) <= 1e-13 * float(ref.abs().max())
+
+
 @pytest.mark.parametrize("K,ra,rb,r,noise", [(64, 8, 8, 2, 0.0), (64, 5, 12, 4, 0.0), (64, 20, 20, 8, 0.0),
                                              (64, 8, 8, 2, 1e-9), (24, 3, 3, 3, 0.0)])
 def test_probe_check_and_compress(T, K, ra, rb, r, noise):
