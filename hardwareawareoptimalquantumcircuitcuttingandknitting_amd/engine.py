@@ -809,8 +809,10 @@ def prep_operands(ctx: Context, WtA, qA, WtB, qB, probes, out=None):
     assert probes.shape[1] == NB and all(t.is_contiguous() for t in (WtA, qA, WtB, qB, probes))
     dev = qA.device
     if out is None:
+        # G and U share one buffer (views of it, G first): a multi-GPU rank all-reduces them in one call
+        gu = T.empty(2 * K * K + K * N_PROBES, dtype=T.float64, device=dev)
         out = (T.empty((K, NA), dtype=T.float64, device=dev), T.empty((K, NB), dtype=T.float64, device=dev),
-               T.empty((2, K, K), dtype=T.float64, device=dev), T.empty((K, N_PROBES), dtype=T.float64, device=dev))
+               gu[:2 * K * K].view(2, K, K), gu[2 * K * K:].view(K, N_PROBES))
     XA, XB, G, U = out
     need = ctypes.c_int64()
     ctx.check(ctx.lib.qk_prep_workspace_bytes(ctx.handle, NA, NB, ctypes.byref(need)), "qk_prep_workspace_bytes")
@@ -830,8 +832,10 @@ def compress_operands(ctx: Context, TA, XA, TB, XB):
     T = torch()
     rmax, K = TA.shape
     assert TB.shape == (rmax, K) and XA.shape[0] == K and XB.shape[0] == K
-    A2 = T.empty((rmax, XA.shape[1]), dtype=T.float64, device=XA.device)
-    B2 = T.empty((rmax, XB.shape[1]), dtype=T.float64, device=XB.device)
+    # A2 and B2 share one buffer (A2 first): a multi-GPU rank all-gathers them in one call
+    ab = T.empty(rmax * (XA.shape[1] + XB.shape[1]), dtype=T.float64, device=XA.device)
+    A2 = ab[:rmax * XA.shape[1]].view(rmax, XA.shape[1])
+    B2 = ab[rmax * XA.shape[1]:].view(rmax, XB.shape[1])
     ctx.check(ctx.lib.qk_compress_operands(ctx.handle, K, rmax, TA.data_ptr(), XA.data_ptr(), XA.shape[1],
                                            A2.data_ptr(), TB.data_ptr(), XB.data_ptr(), XB.shape[1], B2.data_ptr()),
               "qk_compress_operands")

@@ -170,6 +170,18 @@ def _xcd_tile_order(enc, r: int) -> np.ndarray:
     return perm
 
 
+def _joined(T, a, b):
+    """``cat([a.flatten(), b.flatten()])`` without the copy when ``a`` and ``b`` are adjacent views of
+    one flat buffer (engine.prep_operands' G / U, engine.compress_operands' A2 / B2): the buffer."""
+    base = a._base
+    if (base is not None and b._base is base and base.dim() == 1 and a.is_contiguous() and b.is_contiguous()
+            and a.data_ptr() == base.data_ptr()
+            and b.data_ptr() == a.data_ptr() + a.numel() * a.element_size()
+            and base.numel() == a.numel() + b.numel()):
+        return base
+    return T.cat([a.reshape(-1), b.reshape(-1)])
+
+
 class HipBackend:
     """Device work of the pipeline on one GPU through the C ABI."""
 
@@ -800,13 +812,15 @@ class KnitPipeline:
         ia, ib = self.order[0], self.order[-1]
         bwA, bwB = qs[ia].shape[1], qs[ib].shape[1]
         x_full = self._probes(bwB * P, qs[ib].device)  # [N_PROBES, wB]
-        x = x_full[:, self.rank * bwB:(self.rank + 1) * bwB].contiguous()
+        if getattr(self, "_x_local", None) is None or self._x_local.shape[1] != bwB:  # fixed probes: once
+            self._x_local = x_full[:, self.rank * bwB:(self.rank + 1) * bwB].contiguous()
+        x = self._x_local
         npr = self.N_PROBES
         if self._fused_prep(qs):
             mats, G, U = self._prep_fused(qs, x)
             XA, XB = mats[ia], mats[ib]
             K = XA.shape[0]
-            red = T.cat([G.reshape(-1), U.reshape(-1)])
+            red = _joined(T, G, U)
             dist.all_reduce(red, group=self.group)
             G = red[:2 * K * K].view(2, K, K)
             U = red[2 * K * K:].view(K, npr).contiguous()
@@ -819,7 +833,7 @@ class KnitPipeline:
                 TB = fac[R8 * K:2 * R8 * K].view(R8, K)
                 r = fac[-1:].to(T.int32)
             A2l, B2l = be.compress(TA.contiguous(), XA, TB.contiguous(), XB)
-            loc = T.cat([A2l.reshape(-1), B2l.reshape(-1)])
+            loc = _joined(T, A2l, B2l)
         else:
             mats = self.operands(qs)
             self.last_prep = "torch"
