@@ -290,45 +290,55 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
     }
 }
 
-constexpr int PV_GRID = 32;   // workgroups of the V = B'' P^T partial sums (probe_d sums their partials)
-constexpr int PV_WAVES = 16;  // waves per workgroup: 512 column ranges in flight (4 waves: 27 us, latency)
+constexpr int PV_GRID = 64;  // workgroups of the V = B'' P^T partial sums (probe_d sums their partials)
 
-// V partials: vpart[b][j][p] = sum over this workgroup's columns c of B2[j][c] P[p][c] (j < rmax)
-__global__ __launch_bounds__(64 * PV_WAVES) void qk_probe_v_kernel(int rmax, const double* __restrict__ B2,
-                                                                  int64_t ldb2, int64_t NB,
-                                                                  const double* __restrict__ P, int64_t ldp,
-                                                                  double* __restrict__ vpart) {
-    __shared__ double red[PV_WAVES][256];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, l4 = lane >> 4;
-    d4_t acc = {0, 0, 0, 0};
-    // this wave's contiguous column range, 8 k-steps (32 columns) per batch, loads issued first
-    const int64_t nw = (int64_t)gridDim.x * PV_WAVES, w = (int64_t)blockIdx.x * PV_WAVES + wave;
-    const int64_t per = ((NB / 4 + nw - 1) / nw) * 4;
-    const int64_t cb = w * per, ce = cb + per < NB ? cb + per : NB;
-    for (int64_t c0 = cb; c0 < ce; c0 += 32) {
-        double av[8], bv[8];
+// V partials: vpart[b][j][p] = sum over this workgroup's columns c of B2[j][c] P[p][c] (j < rmax), on the
+// VALU: a lane takes one column per iteration (every load a coalesced 512-B row segment), wave w the
+// probes 4w..4w+3, acc[j][q] in registers; then a wave reduction and one store per (j, p). The MFMA form
+// before it fed a 16 x 4 operand block per instruction — 16 rows x 32 B per load, 4x the cache lines
+// — and took 25 us for syc 32 5's 8 x 2^16 B'' against 16 probes.
+__global__ __launch_bounds__(256) void qk_probe_v_kernel(int rmax, const double* __restrict__ B2, int64_t ldb2,
+                                                         int64_t NB, const double* __restrict__ P, int64_t ldp,
+                                                         double* __restrict__ vpart) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double acc[8][4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int64_t c = c0 + 4 * u + l4;
-            const bool cv = c < ce;
-            av[u] = (cv && l16 < rmax) ? B2[(int64_t)l16 * ldb2 + c] : 0.0;  // A[j][c]
-            bv[u] = cv ? P[(int64_t)l16 * ldp + c] : 0.0;                     // B[c][p]
-        }
+    for (int jj = 0; jj < 8; ++jj)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
+        for (int q = 0; q < 4; ++q) acc[jj][q] = 0.0;
+#pragma unroll 4
+    for (int64_t c = (int64_t)blockIdx.x * 64 + lane; c < NB; c += (int64_t)gridDim.x * 64) {
+        double b[8], pv[4];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) b[jj] = jj < rmax ? B2[(int64_t)jj * ldb2 + c] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pv[q] = P[(int64_t)(4 * wave + q) * ldp + c];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[jj][q] = fma(b[jj], pv[q], acc[jj][q]);
     }
+    // wave sums in a fixed order (xor butterfly: every lane ends with the total)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) red[wave][(l4 + 4 * rr) * 16 + l16] = acc[rr];
-    __syncthreads();
-    if (tid < 256) {  // fixed-order pairwise sum over the waves
-        double s[PV_WAVES];
+    for (int jj = 0; jj < 8; ++jj)
 #pragma unroll
-        for (int v = 0; v < PV_WAVES; ++v) s[v] = red[v][tid];
+        for (int q = 0; q < 4; ++q) {
+            double v = acc[jj][q];
 #pragma unroll
-        for (int h = PV_WAVES / 2; h >= 1; h >>= 1)
+            for (int s = 1; s < 64; s <<= 1) v += __shfl_xor(v, s, 64);
+            acc[jj][q] = v;
+        }
+    // vpart layout [b][j][p] with j < 16 (rows >= rmax zero): lane j16 * 4 + q of wave w writes (j16, 4w + q)
+    double* out = vpart + (int64_t)blockIdx.x * 256;
+    if (lane < 64) {
+        const int j16 = lane >> 2, q = lane & 3;
+        double v = 0.0;
 #pragma unroll
-            for (int v = 0; v < h; ++v) s[v] += s[v + h];
-        vpart[(int64_t)blockIdx.x * 256 + tid] = s[0];
+        for (int jj = 0; jj < 8; ++jj)
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq)
+                if (jj == j16 && qq == q) v = acc[jj][qq];
+        out[j16 * 16 + 4 * wave + q] = v;
     }
 }
 
@@ -512,7 +522,7 @@ int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx,
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_probe_errors: hipSetDevice");
     double* vpart = work;
     double* epart = work + PV_GRID * 256;
-    hipLaunchKernelGGL(qk_probe_v_kernel, dim3(PV_GRID), dim3(64 * PV_WAVES), 0, ctx->stream, rmax, B2, ldb2, NB, probes, ldp,
+    hipLaunchKernelGGL(qk_probe_v_kernel, dim3(PV_GRID), dim3(256), 0, ctx->stream, rmax, B2, ldb2, NB, probes, ldp,
                        vpart);
     hipLaunchKernelGGL(qk_probe_d_kernel, dim3(gd), dim3(256), 0, ctx->stream, K, rmax, XA, ldx, NA, A2, lda2, U, vpart,
                        PV_GRID, epart);
