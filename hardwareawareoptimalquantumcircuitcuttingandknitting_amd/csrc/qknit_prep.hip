@@ -206,10 +206,12 @@ __global__ __launch_bounds__(PTH, QK_PREP_WG_PER_CU) void qk_prep_operands_kerne
 // out (sums in a fixed order): GA [K][K], GB [K][K], U [K][16] (from the B side's partials). A
 // workgroup takes 64 consecutive outputs; its 4 waves sum every 4th partial row (coalesced 512-B row
 // segments, 4 x more loads in flight than one thread per output), then LDS adds the 4 sums.
-__global__ __launch_bounds__(256) void qk_prep_reduce_kernel(const double* __restrict__ part, int nblk, int K,
-                                                             double* __restrict__ GA, double* __restrict__ GB,
-                                                             double* __restrict__ U) {
-    __shared__ double acc[4][64];
+constexpr int PRW = 16;  // waves per reduction workgroup (each sums every 16th partial: 4 in-flight rounds
+                         // of 8 loads at 512 partials; 4 waves took 16 rounds, 26 us)
+__global__ __launch_bounds__(64 * PRW) void qk_prep_reduce_kernel(const double* __restrict__ part, int nblk,
+                                                                  int K, double* __restrict__ GA,
+                                                                  double* __restrict__ GB, double* __restrict__ U) {
+    __shared__ double acc[PRW][64];
     const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
     const int e = blockIdx.x * 64 + lane;  // [0, 2 K^2 + 16 K)
     const int KK = K * K;
@@ -228,15 +230,24 @@ __global__ __launch_bounds__(256) void qk_prep_reduce_kernel(const double* __res
         const double* p = part + (int64_t)sd * nblk * PPART + off;
         double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // 8 loads in flight per thread, fixed summation order
         int b = grp;
-        for (; b + 28 < nblk; b += 32)
+        for (; b + 7 * PRW < nblk; b += 8 * PRW)
 #pragma unroll
-            for (int u = 0; u < 8; ++u) t[u] += p[(int64_t)(b + 4 * u) * PPART];
-        for (; b < nblk; b += 4) t[0] += p[(int64_t)b * PPART];
+            for (int u = 0; u < 8; ++u) t[u] += p[(int64_t)(b + PRW * u) * PPART];
+        for (; b < nblk; b += PRW) t[0] += p[(int64_t)b * PPART];
         s = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
     }
     acc[grp][lane] = s;
     __syncthreads();
-    if (grp == 0 && dst) *dst = (acc[0][lane] + acc[1][lane]) + (acc[2][lane] + acc[3][lane]);
+    if (grp == 0 && dst) {  // fixed-order pairwise sum over the waves
+        double v[PRW];
+#pragma unroll
+        for (int w = 0; w < PRW; ++w) v[w] = acc[w][lane];
+#pragma unroll
+        for (int h = PRW / 2; h >= 1; h >>= 1)
+#pragma unroll
+            for (int w = 0; w < h; ++w) v[w] += v[w + h];
+        *dst = v[0];
+    }
 }
 
 // out[j][c] = sum_k T[j][k] X[k][c] for j < rmax, both sides (blockIdx.y). A workgroup takes 64 columns;
@@ -474,7 +485,7 @@ int qk_prep_operands(qk_ctx* ctx, int K, int RA, const double* WtA, const double
     args.part = work;
     hipLaunchKernelGGL(qk_prep_operands_kernel, dim3(G), dim3(PTH), 0, ctx->stream, args);
     const int outs = 2 * K * K + PNP * K;
-    hipLaunchKernelGGL(qk_prep_reduce_kernel, dim3((outs + 63) / 64), dim3(256), 0, ctx->stream, work, G, K, GA,
+    hipLaunchKernelGGL(qk_prep_reduce_kernel, dim3((outs + 63) / 64), dim3(64 * PRW), 0, ctx->stream, work, G, K, GA,
                        GB, U);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_prep_operands: ") + hipGetErrorString(e)).c_str());
