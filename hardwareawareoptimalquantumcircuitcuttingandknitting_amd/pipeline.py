@@ -673,6 +673,7 @@ class KnitPipeline:
         return mats
 
     N_PROBES = 16
+    RANK_GIVE_UP = 3  # consecutive rejected host-path compressions after which a pipeline stops trying
 
     def _probes(self, n: int, device):
         """The fixed Gaussian probes, TRANSPOSED: [N_PROBES, n] (products with the wide operands go
@@ -712,11 +713,17 @@ class KnitPipeline:
             end.record()
             self.events.append((start, end))
         if low is not None and not float(low[1]) <= self.rank_tol:
-            # not numerically low-rank to the tolerance: exact contraction, and for every later step
-            self.data_rank = False
+            # not numerically low-rank to the tolerance: exact contraction for this step; compression is
+            # given up only after RANK_GIVE_UP consecutive rejections (a borderline step does not turn
+            # the fast path off for the pipeline's life)
+            self._rank_rejects = getattr(self, "_rank_rejects", 0) + 1
+            if self._rank_rejects >= self.RANK_GIVE_UP:
+                self.data_rank = False
             self.rank_fallbacks += 1
             self.last_rank = None
             res = self._contract(mats)
+        elif low is not None:
+            self._rank_rejects = 0
         if self.mode == "reduce":
             import torch.distributed as dist
 
