@@ -151,11 +151,13 @@ def _xcd_tile_order(enc, r: int) -> np.ndarray:
     become the slow bits of the block order, so such tiles land 2^(other bits) blocks apart — a
     multiple of 8 when >= 3 other bits — and blocks b, b + 8, ... share an XCD (dealt round-robin,
     MI355X_MICROARCH.md), whose L2 then merges the partial lines before they go to HBM.
-    Identity when no outside bit is that low or fewer than 3 others remain."""
+    Identity when no outside bit is that low or fewer than 3 others remain. ``QKNIT_XCD_LINE_BITS``
+    overrides the line width (measured on syc 32 5: 4, 5, 7 bits 0.134-0.135 ms, 8 bits 0.140)."""
     tm = int(enc.passes[r]["tile_mask"])
     outside = [q for q in range(enc.n) if not (tm >> q) & 1]
-    low = [i for i, q in enumerate(outside) if q < XCD_LINE_BITS]
-    high = [i for i, q in enumerate(outside) if q >= XCD_LINE_BITS]
+    lb = int(os.environ.get("QKNIT_XCD_LINE_BITS", XCD_LINE_BITS))
+    low = [i for i, q in enumerate(outside) if q < lb]
+    high = [i for i, q in enumerate(outside) if q >= lb]
     bpu = 1 << len(outside)
     if not low or len(high) < 3 or os.environ.get("QKNIT_FINAL_XCD_ORDER", "1") == "0":
         return np.arange(bpu)
