@@ -1194,7 +1194,7 @@ __global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlocked
 }
 
 constexpr int64_t OB_STAGE_BYTES = 24 * 1024;  // LDS budget of the blocked kernel's operand stage
-constexpr int OB_WG_PER_CU = 32;  // bench: 5.86 ms per write vs 5.90 at 16, 6.00 at 8 (grid-stride over 2^16 tasks)
+constexpr int OB_WG_PER_CU = 64;  // bench, one box: 5.82 ms per write at 64, 5.85 at 32, 5.90 at 16, 6.00 at 8, 5.83 one per task
 
 // Widest task (TB <= 16 and <= align_bits, >= 9: one 512-output iteration) whose operand stage fits
 // OB_STAGE_BYTES; 0: none. align_bits = trailing zero bits of the output range's begin and count.
