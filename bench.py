@@ -45,6 +45,8 @@ def parse():
                     help="skip the syc 32 1 sweep-only measurement (north_star_sweep)")
     ap.add_argument("--cpu-sample-labels", type=int, default=12)
     ap.add_argument("--no-npd", action="store_true", help="skip the NPD timing on the 2^N output")
+    ap.add_argument("--no-drop-in", action="store_true",
+                    help="skip the drop_in block (run_virtual_circuit(virt, dense=True), first call + steady state)")
     ap.add_argument("--no-general", action="store_true",
                     help="skip knit_general (the same step without data-rank compression)")
     ap.add_argument("--pipeline", action="store_true",
@@ -145,8 +147,11 @@ def cpu_baseline_qvm(cut, processes: int = 8, accuracy: float = 1e-5, return_res
                                                    f"label (cap {QVM_MAX_CLBITS} clbits)"}
     times = {}
     t0 = time.perf_counter()
-    with Pool(processes=processes) as pool:
+    pool = Pool(processes=processes)
+    try:
         _, npd = qvm.run(cut, accuracy, pool=pool, times=times)
+    finally:
+        _close_pool(pool)
     wall = time.perf_counter() - t0
     view = qvm.CutView(cut)
     inst = sum(len(view.labels(list(r))) for r in view.qregs if len(r))
@@ -159,6 +164,24 @@ def cpu_baseline_qvm(cut, processes: int = 8, accuracy: float = 1e-5, return_res
 
 
 _KW = {}
+
+
+def _close_pool(pool) -> None:
+    """Stop a worker pool and reap every worker (``with Pool()`` only terminates them: the driver saw
+    a child process still alive when the bench exited)."""
+    pool.close()
+    pool.join()
+
+
+def cpu_workers() -> tuple[int, str]:
+    """Worker processes of the CPU baselines: the box's per-GPU CPU share (``OMP_NUM_THREADS``, which
+    the GPU pool sets to it; its rules cap worker pools there, while ``sched_getaffinity`` lists every
+    core of the host), else every core this process may run on."""
+    aff = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and 0 < int(env) < aff:
+        return int(env), f"OMP_NUM_THREADS={env}: the GPU box's CPU share per GPU ({aff} host cores visible)"
+    return aff, "all cores in sched_getaffinity"
 
 
 def _byte_pext_tables(clbits):
@@ -221,25 +244,22 @@ def cpu_baseline_same(pipe, cut, qs_host, n_inst_sample: int = 8, out_block_bits
 
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import data_rank
 
-    try:
-        from threadpoolctl import threadpool_info
-
-        threads = max([t.get("num_threads", 1) for t in threadpool_info()] + [1])
-    except Exception:
-        threads = os.cpu_count() or 1
     from multiprocessing import Pool
 
     view = qvm.CutView(cut)
     frags = [list(r) for r in view.qregs if len(r)]
-    procs = max(1, min(threads, len(os.sched_getaffinity(0))))
+    procs, procs_why = cpu_workers()
     jobs = []
     for fi, f in enumerate(frags):
         jobs += [(fi, li) for li in range(min(len(view.labels(f)), max(1, procs // len(frags))))]
     _KW.update(view=view, frags=frags)  # inherited by the forked workers
-    with Pool(procs) as pool:
+    pool = Pool(procs)
+    try:
         t0 = time.perf_counter()
         pool.map(_instance_worker, jobs)  # one exact instance per process, all at once
         t_batch = time.perf_counter() - t0
+    finally:
+        _close_pool(pool)
     done = len(jobs)
     t_inst = t_batch  # wall time of one concurrent batch of `done` instances
     swept = pipe.instance_counts()["instances_swept"]
@@ -258,19 +278,25 @@ def cpu_baseline_same(pipe, cut, qs_host, n_inst_sample: int = 8, out_block_bits
     chunk = 1 << (out_block_bits - 2)
     tasks = 4 * procs
     nblk = chunk * tasks
-    with Pool(procs, initializer=_knit_worker_init, initargs=(A2, B2, _byte_pext_tables(cA),
-                                                                _byte_pext_tables(cB))) as pool:
+    pool = Pool(procs, initializer=_knit_worker_init, initargs=(A2, B2, _byte_pext_tables(cA), _byte_pext_tables(cB)))
+    try:
         pool.map(_knit_worker_chunk, [(0, 1024)] * procs)  # workers up
         t2 = time.perf_counter()
         out = pool.map(_knit_worker_chunk, [(i * chunk, (i + 1) * chunk) for i in range(tasks)])
         t_blk = time.perf_counter() - t2
+    finally:
+        _close_pool(pool)
     scale = (1 << pipe.N) // nblk
     total = t_sweep + t_prep + t_blk * scale
     del out
+    aff = len(os.sched_getaffinity(0))
     return {
         "value": pipe.instance_counts()["instances_ref"] / total,
         "unit": "instances/s",
         "cores": int(procs),
+        "cores_why": procs_why,
+        # every visible core at perfect scaling (an upper bound on this baseline, not measured)
+        "value_all_cores_bound": pipe.instance_counts()["instances_ref"] / total * aff / procs,
         "kind": "port",
         "algorithm": "same as the GPU step (basis-reduced exact instances, factored light-cone knit, "
                      "data-rank compression, output-order write)",
@@ -310,6 +336,47 @@ def knit_general(pipe_kw: dict, steps: int) -> dict:
     del pipe
     torch.cuda.empty_cache()
     return out
+
+
+def drop_in_timing(cut, ref_out, steps: int, device: int) -> dict:
+    """The reference API on the same workload: ``run_virtual_circuit(virt, dense=True)``
+    (``run.py:23-71``, called at ``Utilities.py:79``), which runs the cached plan of the benched
+    engine. ``first_call_ms``: plan cache empty (fragment compile, job tables, transforms, uploads;
+    the hiprtc sweep modules are already cached in this process by the bench's own pipeline);
+    ``steady_ms``: later calls on a fresh ``VirtualCircuit`` of the same cut (the plan is found by the
+    circuit's content hash), each result freed before the next call. ``max_abs_diff_vs_step``: the
+    drop-in's distribution against the bench step's output, every one of the 2^N entries."""
+    import torch
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.run import clear_plan_cache, run_virtual_circuit
+
+    clear_plan_cache()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out, info = run_virtual_circuit(VirtualCircuit(cut), dense=True, device=device)
+    torch.cuda.synchronize()
+    first = time.perf_counter() - t0
+    diff = 0.0
+    chunk = 1 << 28
+    for i in range(0, out.numel(), chunk):
+        diff = max(diff, float((out[i:i + chunk] - ref_out[i:i + chunk]).abs().max()))
+    del out
+    times, infos = [], []
+    for _ in range(max(steps, 3)):
+        virt = VirtualCircuit(cut)
+        t0 = time.perf_counter()
+        out, info = run_virtual_circuit(virt, dense=True, device=device)
+        times.append(time.perf_counter() - t0)
+        infos.append(info)
+        del out
+    clear_plan_cache()
+    torch.cuda.empty_cache()
+    return {"api": "run_virtual_circuit(virt, dense=True)", "first_call_ms": first * 1e3,
+            "steady_ms": float(sum(times) / len(times)) * 1e3, "steady_min_ms": min(times) * 1e3,
+            "run_time_ms": float(sum(i.run_time for i in infos) / len(infos)) * 1e3,
+            "knit_time_ms": float(sum(i.knit_time for i in infos) / len(infos)) * 1e3,
+            "calls": len(times), "max_abs_diff_vs_step": diff}
 
 
 def npd_timing(dense, accuracy: float) -> dict:
@@ -624,6 +691,9 @@ def main():
         from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import quasi_distr
 
         line["npd"] = npd_timing(pipe.out, quasi_distr.ACCURACY)
+    if world == 1 and not args.no_drop_in:
+        line["drop_in"] = drop_in_timing(cut, pipe.out, args.steps, local)
+        line["drop_in"]["vs_ms_per_step"] = line["drop_in"]["steady_ms"] / ms_per_step
     qs_host = None
     if world == 1 and not args.no_cpu_baseline and pipe.dev_rank:
         qs_host = [q.contiguous().cpu().numpy() for q in pipe.sweep()]

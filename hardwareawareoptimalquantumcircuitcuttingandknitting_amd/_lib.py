@@ -87,6 +87,11 @@ SIGNATURES = {
     "qk_threshold_count": (c_i32, [c_vp, c_i64, c_vp, ctypes.c_double, c_vp, c_i64, c_vp]),
     "qk_npd": (c_i32, [c_vp, c_i64, c_vp, ctypes.c_double, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "qk_hellinger": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "qk_knit_select_workspace_bytes": (c_i32, [ctypes.c_int, c_u64, c_u64, ctypes.POINTER(c_i64)]),
+    "qk_knit_select": (c_i32, [c_vp, ctypes.c_int, c_i64, c_vp, c_i64, c_vp, c_i64, c_u64, c_u64, ctypes.c_double,
+                               c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "qk_npd_pairs_workspace_bytes": (c_i32, [c_i64, ctypes.POINTER(c_i64)]),
+    "qk_npd_pairs": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "qk_sample_cdf": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "qk_sample_counts": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_u64, c_vp]),
     "qk_fold_counts": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, ctypes.c_double, c_vp]),

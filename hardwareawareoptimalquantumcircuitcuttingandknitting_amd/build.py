@@ -8,7 +8,8 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", f) for f in ("qknit.hip", "qknit_post.hip", "qknit_jit.hip",
                                                               "qknit_sample.hip", "qknit_rank.hip",
-                                                              "qknit_plan.hip", "qknit_prep.hip")]
+                                                              "qknit_plan.hip", "qknit_prep.hip",
+                                                              "qknit_select.hip")]
 DEPS = SRCS + [os.path.join(HERE, "csrc", h) for h in ("internal.h", "sweep_ops.h")]
 HEADER = os.path.join(os.path.dirname(HERE), "include", "qknit.h")
 OUT = os.path.join(HERE, "libqknit.so")

@@ -513,10 +513,11 @@ def knit_outer_stream(ctx: Context, A, B, clbits_a: list, clbits_b: list, nbits:
 
 def stream_knit_ok(clbits_a: list, clbits_b: list, nbits: int) -> bool:
     """Whether :func:`knit_outer_stream` applies: the two clbit sets partition ``0..nbits-1``
-    (2 <= nbits <= 32) and clbit 0 is on the B side."""
+    (2 <= nbits <= 32), clbit 0 is on the B side, and each list is ascending (the kernels index a
+    fragment's outcomes by pext over its clbit mask, which packs bits in ascending order)."""
     a, b = set(clbits_a), set(clbits_b)
     return (2 <= nbits <= 32 and not (a & b) and (a | b) == set(range(nbits)) and 0 in b
-            and len(a) == len(clbits_a) and len(b) == len(clbits_b))
+            and list(clbits_a) == sorted(a) and list(clbits_b) == sorted(b))
 
 
 def paired_keys(clbits: list) -> bool:
@@ -1101,6 +1102,55 @@ def nearest_probability_distribution(ctx: Context, dense, accuracy: float):
                              keys.data_ptr(), vals.data_ptr(), n_out.data_ptr()), "qk_npd")
     k = int(n_out.item())
     return keys[:k].cpu().numpy(), vals[:k].cpu().numpy()
+
+
+def knit_select(ctx: Context, A, B, clbits_a: list, clbits_b: list, nbits: int, accuracy: float, k_dev=None,
+                capacity: int | None = None):
+    """``qk_knit_select``: the entries ``|v| > accuracy`` of the two-fragment knit
+    ``v[pdep(i, A bits) | pdep(j, B bits)] = sum_k A[k][i] B[k][j]`` (K <= 8), never forming the
+    dense vector; tiles bounded below ``accuracy`` are skipped whole. Returns device ``(keys, vals)``
+    in unspecified order (bit-identical values to the dense write). One host read of the count;
+    reruns with exactly enough room when the first capacity was short."""
+    T = torch()
+    K = A.shape[0]
+    assert B.shape[0] == K and 1 <= K <= 8 and A.is_contiguous() and B.is_contiguous()
+    mA, mB = sum(1 << c for c in clbits_a), sum(1 << c for c in clbits_b)
+    dev = A.device
+    need = ctypes.c_int64()
+    ctx.check(ctx.lib.qk_knit_select_workspace_bytes(nbits, mA, mB, ctypes.byref(need)),
+              "qk_knit_select_workspace_bytes")
+    work = T.empty(max(need.value // 8, 1), dtype=T.float64, device=dev)
+    cnt = T.empty(1, dtype=T.int64, device=dev)
+    cap = min(1 << nbits, 1 << 20) if capacity is None else capacity
+    while True:
+        keys = T.empty(max(cap, 1), dtype=T.int64, device=dev)
+        vals = T.empty(max(cap, 1), dtype=T.float64, device=dev)
+        ctx.check(ctx.lib.qk_knit_select(ctx.handle, nbits, K, A.data_ptr(), A.shape[1], B.data_ptr(), B.shape[1],
+                                         mA, mB, float(accuracy), _ptr(k_dev), work.data_ptr(), work.numel() * 8,
+                                         cap, keys.data_ptr(), vals.data_ptr(), cnt.data_ptr()), "qk_knit_select")
+        n = int(cnt.item())
+        if n <= cap:
+            return keys[:n], vals[:n]
+        cap = n
+
+
+def npd_pairs(ctx: Context, keys, vals):
+    """``qk_npd_pairs``: ``nearest_probability_distribution`` (quasi_distr.py:28-43) of already
+    truncated (key, value) pairs on the GPU; host ``(keys, values)`` ascending by value."""
+    T = torch()
+    n = keys.numel()
+    dev = keys.device
+    need = ctypes.c_int64()
+    ctx.check(ctx.lib.qk_npd_pairs_workspace_bytes(n, ctypes.byref(need)), "qk_npd_pairs_workspace_bytes")
+    ws = T.empty(max(need.value, 1), dtype=T.uint8, device=dev)
+    ok = T.empty(max(n, 1), dtype=T.int64, device=dev)
+    ov = T.empty(max(n, 1), dtype=T.float64, device=dev)
+    n_out = T.zeros(1, dtype=T.int64, device=dev)
+    ctx.check(ctx.lib.qk_npd_pairs(ctx.handle, n, keys.contiguous().data_ptr(), vals.contiguous().data_ptr(),
+                                   ws.data_ptr(), ws.numel(), ok.data_ptr(), ov.data_ptr(), n_out.data_ptr()),
+              "qk_npd_pairs")
+    k = int(n_out.item())
+    return ok[:k].cpu().numpy(), ov[:k].cpu().numpy()
 
 
 def hellinger_sums(ctx: Context, p, q):

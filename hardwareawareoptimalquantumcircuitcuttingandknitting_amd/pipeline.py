@@ -301,6 +301,15 @@ class HipBackend:
     def compress(self, TA, XA, TB, XB):
         return engine.compress_operands(self.ctx, TA, XA, TB, XB)
 
+    def knit_select(self, A, B, clbits_a, clbits_b, nbits, accuracy, k_dev=None):
+        return engine.knit_select(self.ctx, A, B, clbits_a, clbits_b, nbits, accuracy, k_dev=k_dev)
+
+    def npd_pairs(self, keys, vals):
+        return engine.npd_pairs(self.ctx, keys, vals)
+
+    def npd_dense(self, dense, accuracy):
+        return engine.nearest_probability_distribution(self.ctx, dense, accuracy)
+
     def event(self):
         return self.T.cuda.Event(enable_timing=True)
 
@@ -371,11 +380,11 @@ class KnitPipeline:
                              and hasattr(self.be, "rank_factors"))
         self._pending = []  # device (rank, accepted) of steps not yet read back
         # slice mode, fused preparation: every rank factors the same all-reduced Grams with the same
-        # deterministic kernel, so no broadcast of the factors, and each rank checks the rows of R its
-        # own slice holds (this rank's A columns against every probe) and decides for its slice alone
-        # (a rejection takes the exact contraction of that slice only): two collectives fewer per step.
-        # Factors that differed between ranks would mix compressed columns and fail the local check.
-        # QKNIT_SLICE_SYNC=1: rank 0's factors broadcast, probe errors summed over ranks (one decision).
+        # deterministic kernel, so no broadcast of the factors; each rank checks the rows of R in its
+        # A column block against every probe and the squared errors are all-reduced (16 doubles), so
+        # one decision covers all of R and every rank takes it (the exact-slice fallback's
+        # collectives then match across ranks). Factors that differed between ranks would mix
+        # compressed columns and fail the summed check. QKNIT_SLICE_SYNC=1: rank 0's factors broadcast.
         self.slice_sync = os.environ.get("QKNIT_SLICE_SYNC", "0") == "1"
         self.last_kernel = None  # kernel of the last compressed contraction (None: qk_gemm_keyed)
         self.last_prep = None  # data-rank preparation of the last step: "fused" (qk_prep_operands) or "torch"
@@ -809,12 +818,14 @@ class KnitPipeline:
 
     def _prep_slice(self, qs) -> dict:
         """Slice mode (multi-GPU), the preparation of this rank's write: ``qs`` hold every instance
-        row of this rank's column block of each operand (the sweep's all_to_all). Collectives: one
-        all_reduce (the two Grams + the B side against the probes), one broadcast of rank 0's
-        factors and accepted rank (every rank knits with identical ones), one all_gather of the
-        compressed column blocks (rmax x 2^m per fragment); the write itself is local. A rejected
-        compression (read back after the write is queued) falls back to the exact contraction of
-        the slice from all-gathered operands."""
+        row of this rank's column block of each operand (the sweep's all_to_all). Collectives (fused
+        preparation): one all_reduce of the two Grams + the B side against the probes, one
+        all_gather of the compressed column blocks (rmax x 2^m per fragment), one all_reduce of the
+        16 squared probe errors; every rank factors the identical all-reduced Grams with the same
+        deterministic kernel (no broadcast unless QKNIT_SLICE_SYNC=1) and takes the same decision
+        from the summed errors. The write itself is local. A rejected compression (read back after
+        the write is queued) makes every rank take the exact contraction of its slice from
+        all-gathered operands. The torch preparation broadcasts rank 0's factors instead."""
         import torch.distributed as dist
 
         T, be, P = self.T, self.be, self.world
@@ -867,10 +878,11 @@ class KnitPipeline:
         A2 = gat[:, :R8 * bwA].view(P, R8, bwA).permute(1, 0, 2).reshape(R8, P * bwA).contiguous()
         B2 = gat[:, R8 * bwA:].view(P, R8, bwB).permute(1, 0, 2).reshape(R8, P * bwB).contiguous()
         if self._fused_prep(qs):
-            # this rank's A columns against all probes (B2 / probes: every column), summed over ranks
+            # this rank's A columns against all probes (B2 / probes: every column), summed over ranks:
+            # the summed e2 covers every row of R, and every rank takes the same decision from it, so
+            # the exact-slice fallback's collectives (_slice_exact) run on all ranks or on none
             e2, _, _ = be.probe_errors(XA, A2, U, B2, x_full.contiguous(), a2_cols=(self.rank * bwA, bwA))
-            if self.slice_sync:
-                dist.all_reduce(e2, group=self.group)
+            dist.all_reduce(e2, group=self.group)
             k_eff, _ = be.probe_accept(e2, r, self.rank_tol)
             self._pending.append((r, k_eff))
         else:
@@ -1041,7 +1053,7 @@ class KnitPipeline:
         """Two-fragment knit R = A^T B ([K, M], [K, N] operands) rewritten as A''^T B'' with
         r = numerical rank of R rows (engine.data_rank_factors on the two K x K Gram matrices,
         read back once per step). Returns ``(mats'', err)`` — err a device scalar: the largest
-        ||(R - A''^T B'') x||_2 over 8 fixed Gaussian probes x (an estimate of the Frobenius
+        ||(R - A''^T B'') x||_2 over the N_PROBES (16) fixed Gaussian probes x (an estimate of the Frobenius
         norm of the error, computed directly in fp64, no Gram squaring) — or None when the
         compression would not shrink K."""
         T = self.T
@@ -1148,7 +1160,99 @@ class KnitPipeline:
         return self.be.gemm_keyed(A, B.contiguous(), keyA=None, strideA=B.shape[1], keyB=None, strideB=1,
                                   out=self.out)
 
+    def plan_bytes(self) -> int:
+        """Device bytes the plan holds between steps (job tables, sweep rows and workspaces, knit
+        transforms); the output buffer is not counted (run_into: the caller's)."""
+        seen, total = set(), 0
+        for sw in self.sweeps:
+            if sw is None:
+                continue
+            for k in ("slot", "sign", "off", "pjob", "q", "ws"):
+                t = sw.get(k)
+                if t is not None and hasattr(t, "data_ptr") and t.data_ptr() not in seen:
+                    seen.add(t.data_ptr())
+                    total += t.numel() * t.element_size()
+        for W in self.transforms:
+            if W is not None:
+                total += W.numel() * W.element_size()
+        return total
+
+    def covers_outputs(self) -> bool:
+        """Whether one knit writes every output this rank owns: the live fragments' clbits cover all
+        N output bits (in single / slice mode every kernel of the knit then stores each output once,
+        overwriting), so the caller may hand an uninitialised buffer to :meth:`run_into`."""
+        bits = set()
+        for i, fs in enumerate(self.frags):
+            if not fs.dropped:
+                bits |= set(self.ops.clbits[i])
+        return self.mode in ("single", "slice") and bits == set(range(self.N))
+
+    def run_into(self, out):
+        """One step writing the distribution into the caller's ``out`` (2^N fp64, or this rank's slice);
+        the pipeline keeps no reference to it afterwards (the drop-in ``run_virtual_circuit`` returns a
+        fresh buffer per call, and the caching allocator hands the previous call's block back)."""
+        self.out = out
+        try:
+            self.step()
+        finally:
+            self.out = None
+        return out
+
+    def _select_pair(self):
+        """(row side, column side) fragment indices when the dict result can be selected straight
+        from the two knit operands (qk_knit_select): two live fragments, ascending disjoint clbits."""
+        live = [i for i, fs in enumerate(self.frags) if not fs.dropped]
+        if self.mode != "single" or len(live) != 2 or len(self.order) != 2 or not hasattr(self.be, "knit_select"):
+            return None
+        ia, ib = self.order[0], self.order[-1]
+        cA, cB = list(self.ops.clbits[ia]), list(self.ops.clbits[ib])
+        if cA != sorted(cA) or cB != sorted(cB) or set(cA) & set(cB):
+            return None
+        return ia, ib
+
+    def knit_dict(self, accuracy: float, qs=None):
+        """The reference-shaped result of one step (``run.py:71``: ``QuasiDistr`` truncation at
+        ``accuracy``, ``quasi_distr.py:7-10``, then ``nearest_probability_distribution``,
+        ``:28-43``) as host ``(keys, values)`` ascending by value. Where the knit is small-K — the
+        device data rank accepted a compression (syc 32), or the light-cone knit has K <= 8 terms
+        (hwe, bv) — only the entries above ``accuracy`` are formed and kept (qk_knit_select) and
+        NPD runs on those (qk_npd_pairs): the 2^N vector is never written. Otherwise (rejected
+        compression, more than two fragments, K > 8) the dense knit into a scratch buffer, then
+        qk_threshold_count + qk_npd."""
+        if qs is None:
+            qs = self.sweep()
+        pair = self._select_pair()
+        if pair is not None and self.dev_rank:
+            p = self._prep_dev_rank(qs)
+            ia, ib = pair
+            keys, vals = self.be.knit_select(p["A2"], p["B2"], self.ops.clbits[ia], self.ops.clbits[ib], self.N,
+                                             accuracy, k_dev=p["k_eff"])
+            self.last_kernel = "qk_knit_select_kernel"
+            if int(p["k_eff"].reshape(-1)[0]) > 0:
+                return self.be.npd_pairs(keys, vals)
+            mats = p["mats"]  # rejected compression: the exact contraction, dense
+        else:
+            mats = self.operands(qs)
+            if pair is not None and mats[pair[0]].shape[0] <= 8:
+                ia, ib = pair
+                keys, vals = self.be.knit_select(mats[ia].contiguous(), mats[ib].contiguous(), self.ops.clbits[ia],
+                                                 self.ops.clbits[ib], self.N, accuracy)
+                self.last_kernel = "qk_knit_select_kernel"
+                return self.be.npd_pairs(keys, vals)
+        keep = self.out
+        self.out = self.be.zeros((1 << self.N,), self.T.float64)
+        try:
+            dense = self._contract(mats)
+            self.last_kernel = None
+            return self.be.npd_dense(dense, accuracy)
+        finally:
+            self.out = keep
+
+    PENDING_MAX = 32  # device-rank steps whose (rank, accepted) tensors are kept before a read-back
+
     def step(self):
+        if len(self._pending) >= self.PENDING_MAX:
+            self.sync_stats()  # bounded: one host read every PENDING_MAX steps of a long loop
         if self.overlap and self.overlap_ok():
             return self._step_overlapped()
         if not self.record_events:

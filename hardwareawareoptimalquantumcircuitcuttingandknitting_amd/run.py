@@ -22,7 +22,10 @@ covers instance preparation + simulation, ``knit_time`` the contraction.
 """
 from __future__ import annotations
 
+import hashlib
 import logging
+import threading
+from collections import OrderedDict
 from dataclasses import dataclass
 from time import perf_counter
 
@@ -70,17 +73,13 @@ def _foreign_fragment(virt: VirtualCircuit, fs: engine.FragmentState, backend, s
     return T.from_numpy(q).to(T.device("cuda", device))
 
 
-def run_virtual_circuit_dense(virt: VirtualCircuit, shots: int = 20000, *, device: int = 0,
-                              factored: bool = False, out=None, sample: bool = False, seed: int = 0):
-    """Sweep (or shot-sample, ``sample=True``) + knit; returns ``(dense fp64 tensor [2^N] on
-    device, RunTimeInfo)``."""
+def _direct_dense(virt: VirtualCircuit, shots: int, device: int, factored: bool, out, sample: bool, seed: int):
+    """Sweep (or shot-sample) + knit without a cached plan: sampled runs, foreign backends and the
+    explicit ``factored=True/False`` knits of ``engine.knit_dense``."""
     ctx = engine.get_context(device)
     # The factored knit folds labels whose side programs coincide into one operand row; sampled
     # labels differ in their shots even then, so sampling knits directly over the labels.
     factored = factored and not sample
-    log.info("Running virtualizer with %d %s fragments and %d vgates...",
-             len(virt.fragment_circuits),
-             tuple(len(f) for f in virt.fragment_circuits), len(virt.vgate_instructions))
     now = perf_counter()
     native = all(isinstance(virt.get_backend(f), MI355XBackend) for f in virt.fragment_circuits if len(f))
     frags = engine.prepare_fragments(virt, device, basis=factored and native and not sample)
@@ -101,8 +100,170 @@ def run_virtual_circuit_dense(virt: VirtualCircuit, shots: int = 20000, *, devic
     dense = engine.knit_dense(ctx, virt, frags, qs, out=out, factored=factored)
     _sync(device)
     knit_time = perf_counter() - now
-    log.info("Knitted in %.2fs.", knit_time)
     return dense, RunTimeInfo(run_time, knit_time)
+
+
+# ---------------------------------------------------------------------------- plan cache
+PLAN_CACHE_SIZE = 4  # compiled plans kept (LRU), per (circuit fingerprint, device, thread)
+PLAN_CACHE_MAX_BYTES = 16 << 30  # plans holding more device memory (a 32-qubit uncut sweep: 100 GB) are not kept
+_PLANS: OrderedDict = OrderedDict()
+_PLANS_LOCK = threading.Lock()
+
+
+def circuit_fingerprint(virt: VirtualCircuit) -> str:
+    """Content hash of a cut circuit as the sweep and knit see it: every fragment circuit's
+    operations (name, parameters, qubit and global clbit positions; for virtual-gate endpoints the
+    gate type, its parameters and the endpoint side) and the output width. Two ``VirtualCircuit``
+    objects built from the same cut share it, so a repeated ``run_virtual_circuit`` reuses the
+    compiled plan. Cached on the ``VirtualCircuit`` per mutation generation (``_generation``) and on
+    the caller's cut circuit object while its instruction list is the same length (the reference
+    rebuilds a ``VirtualCircuit`` from the same cut circuit on every call, ``Utilities.py:74-79``)."""
+    gen = getattr(virt, "_generation", 0)
+    cached = getattr(virt, "_qk_fingerprint", None)
+    if cached is not None and cached[0] == gen:
+        return cached[1]
+    src = getattr(virt, "_source", None)
+    data = getattr(src, "data", None)
+    stamp = (id(data), len(data)) if isinstance(data, list) else None
+    if stamp is None or stamp != getattr(virt, "_source_stamp", None):
+        stamp = None  # the source changed since this VirtualCircuit was built: hash the fragments only
+    on_src = getattr(src, "_qk_fingerprint", None) if stamp is not None else None
+    if on_src is not None and on_src[0] == stamp:
+        virt._qk_fingerprint = (gen, on_src[1])
+        return on_src[1]
+    h = hashlib.sha1()
+    circ = virt.circuit
+    h.update(repr((circ.num_qubits, circ.num_clbits, len(virt.vgate_instructions))).encode())
+    for frag, fcirc in virt.fragment_circuits.items():
+        h.update(repr(("frag", frag.name, len(frag))).encode())
+        for instr in fcirc:
+            op = instr.operation
+            item = [op.name, tuple(repr(p) for p in getattr(op, "params", ())),
+                    tuple(fcirc.find_qubit(q) for q in instr.qubits), tuple(fcirc.find_clbit(c) for c in instr.clbits)]
+            vg = getattr(op, "_virtual_gate", None)
+            if vg is not None:
+                item += [op.vgate_idx, op.qubit_idx, type(vg).__name__,
+                         tuple(repr(p) for p in getattr(vg, "_params", getattr(vg, "params", ())))]
+            h.update(repr(item).encode())
+    fp = h.hexdigest()
+    virt._qk_fingerprint = (gen, fp)
+    if stamp is not None:
+        try:  # the next VirtualCircuit of this same (unmodified) circuit object reuses it
+            src._qk_fingerprint = (stamp, fp)
+        except AttributeError:
+            pass
+    return fp
+
+
+def _build_plan(virt: VirtualCircuit, device: int):
+    """The benchmarked engine (bench.py): factored knit with light-cone basis + rank-compressed core
+    and the per-step device data rank (``pipeline.KnitPipeline``). A circuit the
+    factored planner refuses (a virtual gate with both endpoints in one fragment) gets the direct
+    knit over all global labels through the same pipeline."""
+    from .pipeline import KnitPipeline
+
+    try:
+        return KnitPipeline(virt, device=device, factored=True)
+    except NotImplementedError as e:
+        log.info("factored plan refused (%s): direct knit", e)
+        return KnitPipeline(virt, device=device, factored=False)
+
+
+def cached_plan(virt: VirtualCircuit, device: int = 0):
+    """The compiled plan (``KnitPipeline``) of ``virt`` on ``device`` for the calling thread: built on
+    the first call, reused while the circuit's fingerprint is unchanged (LRU of PLAN_CACHE_SIZE;
+    plans above PLAN_CACHE_MAX_BYTES of device buffers are rebuilt per call instead).
+    Plans are per thread: a plan owns its sweep buffers, and the reference calls
+    ``run_virtual_circuit`` from concurrent threads (``Utilities.py:85-89``)."""
+    key = (circuit_fingerprint(virt), device, threading.get_ident())
+    with _PLANS_LOCK:
+        pipe = _PLANS.get(key)
+        if pipe is not None:
+            _PLANS.move_to_end(key)
+            return pipe
+    pipe = _build_plan(virt, device)
+    if pipe.plan_bytes() > PLAN_CACHE_MAX_BYTES:
+        return pipe
+    with _PLANS_LOCK:
+        _PLANS[key] = pipe
+        _PLANS.move_to_end(key)
+        while len(_PLANS) > PLAN_CACHE_SIZE:
+            _PLANS.popitem(last=False)
+    return pipe
+
+
+def clear_plan_cache() -> None:
+    with _PLANS_LOCK:
+        _PLANS.clear()
+
+
+def _planned_dense(virt: VirtualCircuit, device: int, out):
+    """One step of the cached plan into a fresh (or the caller's) output buffer. ``run_time`` = host
+    planning (first call) + the sweep (HIP events), ``knit_time`` = the rest of the wall time: the
+    same split as run.py:35,60,65-67 without a host synchronisation between the two."""
+    T = engine.torch()
+    now = perf_counter()
+    pipe = cached_plan(virt, device)
+    pipe.be.bind()
+    if out is None:
+        n = pipe.slice[1] if pipe.mode == "slice" else 1 << pipe.N
+        alloc = T.empty if pipe.covers_outputs() else T.zeros
+        out = alloc(n, dtype=T.float64, device=T.device("cuda", device))
+    e0, e1 = T.cuda.Event(enable_timing=True), T.cuda.Event(enable_timing=True)
+    host = perf_counter() - now
+    e0.record()
+    pipe.out = out
+    try:
+        qs = pipe.sweep()
+        e1.record()
+        pipe.knit(qs)
+    finally:
+        pipe.out = None
+    _sync(device)
+    wall = perf_counter() - now
+    pipe.sync_stats()
+    run_time = host + e0.elapsed_time(e1) * 1e-3
+    return out, RunTimeInfo(run_time, max(wall - run_time, 0.0)), pipe
+
+
+def _planned_dict(virt: VirtualCircuit, device: int, accuracy: float):
+    """The reference-shaped result from the cached plan (``KnitPipeline.knit_dict``): the
+    thresholded knit where it applies, never the dense 2^N vector."""
+    T = engine.torch()
+    now = perf_counter()
+    pipe = cached_plan(virt, device)
+    pipe.be.bind()
+    e0, e1 = T.cuda.Event(enable_timing=True), T.cuda.Event(enable_timing=True)
+    host = perf_counter() - now
+    e0.record()
+    qs = pipe.sweep()
+    e1.record()
+    keys, vals = pipe.knit_dict(accuracy, qs)
+    wall = perf_counter() - now
+    pipe.sync_stats()
+    run_time = host + e0.elapsed_time(e1) * 1e-3
+    return keys, vals, RunTimeInfo(run_time, max(wall - run_time, 0.0))
+
+
+def run_virtual_circuit_dense(virt: VirtualCircuit, shots: int = 20000, *, device: int = 0,
+                              factored: bool | None = None, out=None, sample: bool = False, seed: int = 0):
+    """Sweep (or shot-sample, ``sample=True``) + knit; returns ``(dense fp64 tensor [2^N] on
+    device, RunTimeInfo)``.
+
+    Default (``factored=None``, every fragment on the MI355X backend, exact instances): the cached
+    plan (:func:`cached_plan`) — the engine ``bench.py`` times: factored light-cone knit, per-step
+    device data rank, the write-bound blocked knit. ``factored=True/False`` force the uncached
+    factored / direct ``engine.knit_dense``; sampling and foreign backends take the direct path."""
+    log.info("Running virtualizer with %d %s fragments and %d vgates...",
+             len(virt.fragment_circuits),
+             tuple(len(f) for f in virt.fragment_circuits), len(virt.vgate_instructions))
+    native = all(isinstance(virt.get_backend(f), MI355XBackend) for f in virt.fragment_circuits if len(f))
+    if factored is None and native and not sample:
+        dense, info, _ = _planned_dense(virt, device, out)
+    else:
+        dense, info = _direct_dense(virt, shots, device, bool(factored), out, sample, seed)
+    log.info("Knitted in %.2fs.", info.knit_time)
+    return dense, info
 
 
 def run_virtual_circuit_sharded(virt: VirtualCircuit, group=None, *, device: int | None = None, backend=None):
@@ -131,8 +292,12 @@ def run_virtual_circuit_sharded(virt: VirtualCircuit, group=None, *, device: int
              len(virt.fragment_circuits), tuple(len(f) for f in virt.fragment_circuits),
              len(virt.vgate_instructions), world)
     kw = {"backend": backend} if backend is not None else {}
-    pipe = KnitPipeline(virt, device=device, factored=True, rank=rank, world=world, group=group, **kw)
-    if pipe.mode != "slice":
+    try:
+        pipe = KnitPipeline(virt, device=device, factored=True, rank=rank, world=world, group=group, **kw)
+    except NotImplementedError as e:  # the factored planner refused the circuit: direct knit, reduce mode
+        log.info("factored plan refused (%s): direct knit", e)
+        pipe = None
+    if pipe is None or pipe.mode != "slice":
         pipe = KnitPipeline(virt, device=device, factored=False, rank=rank, world=world, group=group,
                             mode="reduce", **kw)
     on_gpu = backend is None
@@ -154,7 +319,7 @@ def run_virtual_circuit_sharded(virt: VirtualCircuit, group=None, *, device: int
 
 
 def run_virtual_circuit(virt: VirtualCircuit, shots: int = 20000, *, device: int = 0,
-                        dense: bool = False, factored: bool = False, sample: bool = False, seed: int = 0,
+                        dense: bool = False, factored: bool | None = None, sample: bool = False, seed: int = 0,
                         group=None):
     """Reference-compatible entry point (``run.py:23-71``). ``group`` (a ``torch.distributed``
     process group, e.g. ``dist.group.WORLD``) runs it on every rank of the group
@@ -179,12 +344,18 @@ def run_virtual_circuit(virt: VirtualCircuit, shots: int = 20000, *, device: int
         dist.all_reduce(full, group=group)  # shards are disjoint: the sum assembles the distribution
         out = full
     else:
+        native = all(isinstance(virt.get_backend(f), MI355XBackend) for f in virt.fragment_circuits if len(f))
+        if not dense and factored is None and native and not sample:
+            # reference-shaped result straight from the plan: entries above ACCURACY only
+            log.info("Running virtualizer with %d %s fragments and %d vgates...",
+                     len(virt.fragment_circuits), tuple(len(f) for f in virt.fragment_circuits),
+                     len(virt.vgate_instructions))
+            keys, vals, info = _planned_dict(virt, device, _qd.ACCURACY)
+            log.info("Knitted in %.2fs.", info.knit_time)
+            return dict(zip(keys.tolist(), vals.tolist())), info
         out, info = run_virtual_circuit_dense(virt, shots, device=device, factored=factored, sample=sample,
                                               seed=seed)
     if dense:
         return out, info
-    from . import quasi_distr
-
-    keys, vals = engine.nearest_probability_distribution(engine.get_context(device), out,
-                                                         quasi_distr.ACCURACY)
+    keys, vals = engine.nearest_probability_distribution(engine.get_context(device), out, _qd.ACCURACY)
     return dict(zip(keys.tolist(), vals.tolist())), info

@@ -46,6 +46,11 @@ class VirtualCircuit:
     def __init__(self, circuit: QuantumCircuit) -> None:
         from .ingest import adopt_with_map
 
+        # the caller's circuit object: run_virtual_circuit's plan cache keeps the content hash on it,
+        # so VirtualCircuits rebuilt from the same cut per call (Utilities.py:74-79) skip re-hashing
+        self._source = circuit
+        data = getattr(circuit, "data", None)
+        self._source_stamp = (id(data), len(data)) if isinstance(data, list) else None
         # a foreign (qiskit) cut circuit is rebuilt in this IR; its registers stay valid keys
         circuit, self._frag_alias = adopt_with_map(circuit)
         self._vgate_instrs = [instr for instr in circuit if _is_vgate(instr.operation)]
@@ -57,6 +62,9 @@ class VirtualCircuit:
 
         default = MI355XBackend()
         self._frag_to_backend = {qreg: default for qreg in self._frag_circs}
+        # bumped by every mutation of fragments / backends: run_virtual_circuit's plan cache
+        # (run.circuit_fingerprint) recomputes the circuit's fingerprint when it changes
+        self._generation = 0
 
     def _frag(self, fragment):
         """Translate a caller's (possibly foreign) fragment register to the adopted one."""
@@ -122,6 +130,8 @@ class VirtualCircuit:
 
     def replace_fragment_circuit(self, fragment, circuit: QuantumCircuit) -> None:
         self._frag_circs[self._frag(fragment)] = circuit
+        self._generation += 1
+        self._source = None  # the fragments no longer follow from the source circuit alone
 
     def get_backend(self, fragment):
         fragment = self._frag(fragment)
@@ -134,9 +144,11 @@ class VirtualCircuit:
         if fragment not in self._frag_to_backend:
             raise ValueError("Fragment not found.")
         self._frag_to_backend[fragment] = backend
+        self._generation += 1
 
     def set_backend_for_all(self, backend) -> None:
         self._frag_to_backend = {qreg: backend for qreg in self._frag_circs}
+        self._generation += 1
 
     # ------------------------------------------------------------------ construction helpers
     @staticmethod

@@ -322,6 +322,29 @@ int qk_sample_counts(qk_ctx* ctx, int64_t n_labels, int64_t label_base, const in
 int qk_fold_counts(qk_ctx* ctx, int64_t n_labels, const int64_t* label_row_off, int64_t width,
                    const double* row_sign, const unsigned int* counts, int64_t shots, double acc, double* q);
 
+/* ---- thresholded knit (qknit_select.hip): the dict result without the dense 2^N vector --------
+ * Every output v = sum_{k<K} A[k*lda + i] B[k*ldb + j] (i < 2^popcount(maskA), j < 2^popcount(maskB),
+ * key = pdep(i, maskA) | pdep(j, maskB)) with |v| > acc is appended to keys / vals (DEVICE, capacity
+ * entries); *count_dev (DEVICE int64) = the number of such outputs, which may exceed capacity (then
+ * only capacity entries were written: call again with more room). This is the knit of
+ * virtual_circuit.py:50-68 fused with QuasiDistr's ACCURACY truncation (quasi_distr.py:7-10): values
+ * are formed exactly as the dense qk_knit_outer_stream_range writes them (bit-identical), in
+ * unspecified order. Tiles whose per-column-block bound sum_k max|A[k]| max|B[k]| cannot exceed acc
+ * are skipped without forming their outputs. k_dev (DEVICE int32 or NULL) overrides K at run time;
+ * *k_dev <= 0 writes nothing (count 0): the caller falls back to the exact dense contraction.
+ * K <= 8; masks disjoint, inside the nbits output bits. work: qk_knit_select_workspace_bytes. */
+int qk_knit_select_workspace_bytes(int nbits, uint64_t maskA, uint64_t maskB, int64_t* bytes);
+int qk_knit_select(qk_ctx* ctx, int nbits, int64_t K, const double* A, int64_t lda, const double* B, int64_t ldb,
+                   uint64_t maskA, uint64_t maskB, double acc, const int32_t* k_dev, void* work, int64_t work_bytes,
+                   int64_t capacity, int64_t* keys, double* vals, int64_t* count_dev);
+
+/* nearest_probability_distribution (quasi_distr.py:28-43) on count (key, value) pairs (DEVICE, e.g.
+ * qk_knit_select's output, already truncated): writes the kept pairs ascending by value (ties by key)
+ * into out_keys / out_vals (capacity count) and their number into *n_out_dev (DEVICE int64). */
+int qk_npd_pairs_workspace_bytes(int64_t count, int64_t* bytes);
+int qk_npd_pairs(qk_ctx* ctx, int64_t count, const int64_t* keys, const double* vals, void* ws, int64_t ws_bytes,
+                 int64_t* out_keys, double* out_vals, int64_t* n_out_dev);
+
 /* acc3[0] = sum sqrt(max(p,0) max(q,0)), acc3[1] = sum max(p,0), acc3[2] = sum max(q,0) (device).
  * Hellinger fidelity = (acc3[0] / sqrt(acc3[1] acc3[2]))^2 (Utilities.py:222-224). */
 int qk_hellinger(qk_ctx* ctx, int64_t n, const double* p, const double* q, double* acc3);

@@ -35,8 +35,12 @@ def _project(psi, n, q, bit):
     return out
 
 
-def simulate(ops, n_qubits, n_clbits=0):
-    """Exact distribution ``{key: p}`` (entries with p == 0 are omitted)."""
+def simulate_branches(ops, n_qubits):
+    """The branching simulation behind :func:`simulate`: ``(branches, final)`` with ``branches`` a
+    list of ``(p, key)`` — ``p`` the probability vector over the state index (``sum b_q 2^q``) of one
+    mid-circuit measurement branch, ``key`` that branch's measured bits — and ``final`` the map
+    qubit -> clbit of the final measurements. Golden-vector generation restricts these to a few
+    outcomes without building the whole dict (tests/golden/make_golden.py)."""
     last_touch = {}
     for i, (name, _, qs, _) in enumerate(ops):
         if name != "barrier":
@@ -65,9 +69,15 @@ def simulate(ops, n_qubits, n_clbits=0):
             continue
         mat = matrix(name, params)
         branches = [(_apply(st, n_qubits, mat, qs), key) for st, key in branches]
+    # index = sum b_q 2^q (C order, axis 0 = qubit n-1)
+    return [(np.abs(st.reshape(-1)) ** 2, key) for st, key in branches], final
+
+
+def simulate(ops, n_qubits, n_clbits=0):
+    """Exact distribution ``{key: p}`` (entries with p == 0 are omitted)."""
+    branches, final = simulate_branches(ops, n_qubits)
     out = {}
-    for st, key in branches:
-        p = np.abs(st.reshape(-1)) ** 2  # index = sum b_q 2^q (C order, axis 0 = qubit n-1)
+    for p, key in branches:
         if not n_qubits:
             out[key] = out.get(key, 0.0) + float(p[0])
             continue

@@ -13,8 +13,11 @@ Fixtures:
   knit_<case>.json    — reference VirtualCircuit.knit on exact instance
                         distributions (computed by oracle.statevector), ACCURACY 0 and 1e-5
   generators.json     — reference syc/hwe/bv generator op lists (random.seed(1234))
+  knit_samples_<cfg>.json — reference VirtualCircuit.knit of the 2^32-output configs (syc 32 1,
+                        syc 32 5) on exact instances restricted to 64 seeded outcomes per fragment:
+                        4096 exact entries of the full distribution (make_knit_samples)
 
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py [--samples [config ...]]
 """
 import json
 import math
@@ -247,6 +250,128 @@ def make_knit(qd, vg, vc, cut, name):
     return out
 
 
+_SAMPLE_JOB = {}
+
+
+def _restricted_instance(job):
+    """One instance of a fragment, exact (oracle branching statevector), restricted to the sampled
+    data outcomes: ``{data key | config key: p}`` over the fragment's sampled outcomes only."""
+    import numpy as np
+
+    from oracle.statevector import simulate_branches
+
+    fi, label = job
+    view, frag, cl, sample_keys = (_SAMPLE_JOB[k][fi] if k != "view" else _SAMPLE_JOB[k]
+                                   for k in ("view", "frags", "clbits", "keys"))
+    n = len(frag)
+    branches, final = simulate_branches(view.instance_ops(list(frag), label), n)
+    s = np.arange(1 << n, dtype=np.int64)
+    data = np.zeros_like(s)
+    for q, c in final.items():
+        if c < view.num_clbits:
+            data |= ((s >> q) & 1) << c
+    hit = np.isin(data, sample_keys)
+    out = {}
+    for p, key in branches:
+        for k, v in zip(data[hit].tolist(), p[hit].tolist()):
+            if v != 0.0:
+                out[k | key] = out.get(k | key, 0.0) + v
+    return sorted(out.items())
+
+
+def make_knit_samples(qd, vc, config: str, n_samples: int = 64, seed: int = 2026, processes: int = 8):
+    """Reference ``VirtualCircuit.knit`` (ACCURACY = 0) of a 2^32-output BASELINE config on exact
+    instance distributions restricted to ``n_samples`` seeded data outcomes per fragment.
+
+    The knit is entrywise (``qd:55-60``: merges are outer products with disjoint key supports; the
+    per-gate knits, ``vg:105-124,179-194``, combine entries of equal data key), so every output key
+    whose fragment parts are all sampled receives exactly its unrestricted value: n_samples^2 exact
+    entries of the full 2^32 distribution, from the reference's own knit."""
+    from multiprocessing import Pool
+
+    import numpy as np
+    from oracle import dense
+    from oracle.qvm import CutView
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import cutting
+
+    name, n, d, p, var = cutting.BASELINE_CONFIGS[config]
+    _, cut, desc = cutting.config_cut_circuit(name, n, d, p, var)
+    view = CutView(cut)
+    frags = [tuple(r) for r in view.qregs if len(r)]
+    rng = np.random.default_rng(seed)
+    clbits, keys, xs = [], [], []
+    from oracle.statevector import simulate_branches
+
+    for f in frags:
+        cl = dense.fragment_clbits(view, list(f))
+        # 3/4 of the samples from the support of the first label's outcome marginal (shallow circuits
+        # such as syc 32 1 put zero probability on most outcomes), the rest uniform
+        branches, final = simulate_branches(view.instance_ops(list(f), view.labels(list(f))[0]), len(f))
+        s_idx = np.arange(1 << len(f), dtype=np.int64)
+        xi = np.zeros_like(s_idx)
+        for q, c in final.items():
+            if c in cl:
+                xi |= ((s_idx >> q) & 1) << cl.index(c)
+        marg = np.zeros(1 << len(cl))
+        for pb, _ in branches:
+            np.add.at(marg, xi, pb)
+        support = np.nonzero(marg > 0)[0]
+        n_sup = min(len(support), 3 * n_samples // 4)
+        x = set(rng.choice(support, n_sup, replace=False).tolist())
+        while len(x) < n_samples:
+            x.add(int(rng.integers(1 << len(cl))))
+        x = np.array(sorted(x), dtype=np.int64)
+        k = np.zeros_like(x)
+        for i, c in enumerate(cl):
+            k |= ((x >> i) & 1) << c
+        clbits.append(cl)
+        xs.append(x)
+        keys.append(k)
+    _SAMPLE_JOB.update(view=view, frags=frags, clbits=clbits, keys=keys)
+    jobs = [(fi, label) for fi, f in enumerate(frags) for label in view.labels(list(f))]
+    pool = Pool(processes)
+    try:
+        rows = pool.map(_restricted_instance, jobs, chunksize=8)
+    finally:
+        pool.close()
+        pool.join()
+    inputs = {fi: [] for fi in range(len(frags))}
+    for (fi, _), r in zip(jobs, rows):
+        inputs[fi].append(r)
+    ref_vgates = []
+    for instr in cut:
+        op = instr.operation
+        if not op.name.startswith("v_"):
+            continue
+        if op.name != "v_cx":
+            raise ValueError(f"{config}: unexpected virtual gate {op.name}")
+        fa = next(i for i, f in enumerate(frags) if instr.qubits[0] in f)
+        fb = next(i for i, f in enumerate(frags) if instr.qubits[1] in f)
+        ref_vgates.append(NS(operation=_REF_VG.VirtualCX(Gate("cx", 2, [])), qubits=[("F", fa), ("F", fb)]))
+    qd.ACCURACY = 0.0
+    v = object.__new__(vc.VirtualCircuit)
+    v._vgate_instrs = ref_vgates
+    v._circuit = NS(num_clbits=view.num_clbits)
+    results = {tuple([("F", fi)]): [qd.QuasiDistr(dict(x)) for x in inputs[fi]] for fi in inputs}
+    res = v.knit(results, _SerialPool())
+    qd.ACCURACY = 1e-5
+    N = view.num_clbits
+    out_keys = (keys[0][:, None] | keys[1][None, :]).reshape(-1) if len(keys) == 2 else keys[0]
+    vals = [float(res.get(int(k), 0.0)) for k in out_keys]
+    allowed = set(out_keys.tolist())
+    extra = [k for k in res if k >> N or int(k) not in allowed]
+    if extra:
+        raise AssertionError(f"{config}: reference knit produced {len(extra)} keys outside the sampled set")
+    return {"case": config, "cut": desc, "num_clbits": N, "seed": seed, "n_samples": n_samples,
+            "fragment_clbits": clbits, "samples": [x.tolist() for x in xs],
+            "keys": [int(k) for k in out_keys], "values": vals,
+            "instances": len(jobs), "accuracy": 0.0}
+
+
+_REF_VG = None
+
+
 def make_generators():
     import importlib
 
@@ -264,6 +389,22 @@ def make_generators():
     b = bvm.BV(secret="1111", barriers=False, measure=False, regname="q")
     out["bv_5"] = b.gen_circuit().ops
     return out
+
+
+def main_samples():
+    """knit_samples_<config>.json only (2^32-output configs; minutes of CPU on 8 processes)."""
+    global _REF_VG
+    install_placeholders()
+    import qvm.quasi_distr as qd
+    import qvm.virtual_circuit as vc
+    import qvm.virtual_gates as vg
+
+    _REF_VG = vg
+    for config in sys.argv[2:] or ("syc_32_1_p2", "syc_32_5_p2"):
+        obj = make_knit_samples(qd, vc, config)
+        with open(os.path.join(HERE, f"knit_samples_{config}.json"), "w") as f:
+            json.dump(obj, f, separators=(",", ":"))
+        print("wrote", config, "instances", obj["instances"], "nonzero", sum(v != 0 for v in obj["values"]))
 
 
 def main():
@@ -305,4 +446,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "--samples":
+        main_samples()
+    else:
+        main()
