@@ -28,6 +28,12 @@ class QkProgram(ctypes.Structure):
                 ("ops", c_vp), ("groups", c_vp), ("mats", c_vp)]
 
 
+class QkLowrankPlan(ctypes.Structure):
+    _fields_ = [("nbits", c_i32), ("terms", c_i32), ("rows_a", c_i64), ("rows_b", c_i64), ("mask_a", c_u64),
+                ("mask_b", c_u64), ("wt_a", c_vp), ("wt_b", c_vp), ("probes", c_vp), ("lam_tol", ctypes.c_double),
+                ("s_tol", ctypes.c_double), ("s_abs", ctypes.c_double), ("rank_tol", ctypes.c_double)]
+
+
 class QkKnitPlan(ctypes.Structure):
     _fields_ = [("n_frag", c_i32), ("nbits", c_i32), ("terms", c_i64), ("rows", ctypes.POINTER(c_i64)),
                 ("clbit_masks", ctypes.POINTER(c_u64)), ("transforms", ctypes.POINTER(c_vp))]
@@ -87,6 +93,16 @@ SIGNATURES = {
     "qk_threshold_count": (c_i32, [c_vp, c_i64, c_vp, ctypes.c_double, c_vp, c_i64, c_vp]),
     "qk_npd": (c_i32, [c_vp, c_i64, c_vp, ctypes.c_double, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "qk_hellinger": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "qk_knit_lowrank_workspace_bytes": (c_i32, [c_vp, c_vp, ctypes.POINTER(c_i64)]),
+    "qk_knit_lowrank": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "qk_comm_unique_id": (c_i32, [c_vp]),
+    "qk_comm_init": (c_i32, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(c_vp)]),
+    "qk_comm_destroy": (c_i32, [c_vp]),
+    "qk_comm_size": (c_i32, [c_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "qk_allreduce": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64]),
+    "qk_reduce": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_int]),
+    "qk_allgather": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64]),
+    "qk_alltoall": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64]),
     "qk_knit_select_workspace_bytes": (c_i32, [ctypes.c_int, c_u64, c_u64, ctypes.POINTER(c_i64)]),
     "qk_knit_select": (c_i32, [c_vp, ctypes.c_int, c_i64, c_vp, c_i64, c_vp, c_i64, c_u64, c_u64, ctypes.c_double,
                                c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),

@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", f) for f in ("qknit.hip", "qknit_post.hip", "qknit_jit.hip",
                                                               "qknit_sample.hip", "qknit_rank.hip",
                                                               "qknit_plan.hip", "qknit_prep.hip",
-                                                              "qknit_select.hip")]
+                                                              "qknit_select.hip", "qknit_comm.hip")]
 DEPS = SRCS + [os.path.join(HERE, "csrc", h) for h in ("internal.h", "sweep_ops.h")]
 HEADER = os.path.join(os.path.dirname(HERE), "include", "qknit.h")
 OUT = os.path.join(HERE, "libqknit.so")
@@ -34,7 +34,7 @@ def build_library(force: bool = False, verbose: bool = False, out: str = OUT,
         return out
     tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-result", *[f"-D{d}" for d in defines], *SRCS, "-lhiprtc", "-o", tmp]
+           "-Wall", "-Wno-unused-result", *[f"-D{d}" for d in defines], *SRCS, "-lhiprtc", "-lrccl", "-o", tmp]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{res.stderr}")

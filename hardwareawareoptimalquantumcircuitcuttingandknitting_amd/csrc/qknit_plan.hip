@@ -205,3 +205,128 @@ int qk_knit(qk_ctx* ctx, const qk_knit_plan* plan, const double* const* q, void*
 }
 
 }  // extern "C"
+
+// ---- qk_knit_lowrank: the benched single-GPU knit (KnitPipeline's device data rank) in one call -----
+// Steps, all on ctx->stream with no host synchronisation (DESIGN.md §2 "Data-rank compression"):
+//   1. qk_prep_operands   X_A = Wt_A^T q_A, X_B = Wt_B^T q_B, G_A, G_B, U = X_B P^T
+//   2. qk_rank_factors    T_A, T_B, r from the Grams (r = 0: no factorisation of rank <= 8)
+//   3. qk_compress_operands  A'' = T_A X_A, B'' = T_B X_B  (8 rows)
+//   4. qk_probe_errors    accepted rank k = r when every probe error is <= rank_tol, else 0
+//   5. qk_knit_outer_stream_range  the write-bound knit of A'', B'' with K = k (k = 0: nothing)
+//   6. qk_gemm_keyed_pred the exact K-term contraction of X_A, X_B, predicated on k == 0
+namespace {
+
+constexpr int LR_RMAX = 8;
+constexpr int LR_PROBES = 16;
+
+struct LowrankLayout {
+    int64_t xa, xb, g, u, prep, ta, tb, r, a2, b2, e2, k, err, probe, ka, kb, total;
+    int64_t prep_bytes, probe_bytes;
+};
+
+int lowrank_layout(qk_ctx* ctx, const qk_lowrank_plan* p, LowrankLayout& L, std::string& why) {
+    if (!p || p->terms < 2 || p->terms > 64 || (p->terms & 1) || p->rows_a < 1 || p->rows_b < 1 || !p->wt_a ||
+        !p->wt_b || !p->probes || p->nbits < 2 || p->nbits > 32) {
+        why = "qk_knit_lowrank: need even 2 <= terms <= 64, swept rows, transforms, probes, 2 <= nbits <= 32";
+        return QK_EARG;
+    }
+    const uint64_t full = (uint64_t(1) << p->nbits) - 1;
+    if ((p->mask_a & p->mask_b) || (p->mask_a | p->mask_b) != full || !(p->mask_b & 1)) {
+        why = "qk_knit_lowrank: masks must be disjoint, cover all nbits output bits, bit 0 in mask_b";
+        return QK_EARG;
+    }
+    const int64_t NA = int64_t(1) << __builtin_popcountll(p->mask_a), NB = int64_t(1) << __builtin_popcountll(p->mask_b);
+    if (NA % 128 || NB % 128) {
+        why = "qk_knit_lowrank: each fragment needs >= 7 measured clbits (operand widths multiples of 128)";
+        return QK_EARG;
+    }
+    const int64_t K = p->terms;
+    int64_t prep = 0, probe = 0;
+    int rc = qk_prep_workspace_bytes(ctx, NA, NB, &prep);
+    if (!rc) rc = qk_probe_workspace_bytes(ctx, NA, &probe);
+    if (rc) {
+        why = "qk_knit_lowrank: workspace queries failed";
+        return rc;
+    }
+    int64_t off = 0;
+    auto take = [&](int64_t bytes) { const int64_t o = off; off += align16(bytes); return o; };
+    L.xa = take(K * NA * 8);
+    L.xb = take(K * NB * 8);
+    L.g = take(2 * K * K * 8);
+    L.u = take(K * LR_PROBES * 8);
+    L.prep = take(prep);
+    L.ta = take(LR_RMAX * K * 8);
+    L.tb = take(LR_RMAX * K * 8);
+    L.r = take(8);
+    L.a2 = take(LR_RMAX * NA * 8);
+    L.b2 = take(LR_RMAX * NB * 8);
+    L.e2 = take(LR_PROBES * 8);
+    L.k = take(8);
+    L.err = take(8);
+    L.probe = take(probe);
+    L.ka = contiguous_bits(p->mask_a) ? -1 : take(NA * 8);
+    L.kb = contiguous_bits(p->mask_b) ? -1 : take(NB * 8);
+    L.total = off;
+    L.prep_bytes = prep;
+    L.probe_bytes = probe;
+    return QK_OK;
+}
+
+__global__ void qk_copy_i32_kernel(const int32_t* src, int32_t* dst) { *dst = *src; }
+
+}  // namespace
+
+extern "C" {
+
+int qk_knit_lowrank_workspace_bytes(qk_ctx* ctx, const qk_lowrank_plan* plan, int64_t* bytes) {
+    if (!ctx || !bytes) return QK_EARG;
+    LowrankLayout L;
+    std::string why;
+    const int rc = lowrank_layout(ctx, plan, L, why);
+    if (rc) return pfail(ctx, rc, why);
+    *bytes = L.total;
+    return QK_OK;
+}
+
+int qk_knit_lowrank(qk_ctx* ctx, const qk_lowrank_plan* p, const double* q_a, const double* q_b, void* workspace,
+                    int64_t workspace_bytes, double* out, int32_t* rank_out) {
+    if (!ctx) return QK_EARG;
+    LowrankLayout L;
+    std::string why;
+    int rc = lowrank_layout(ctx, p, L, why);
+    if (rc) return pfail(ctx, rc, why);
+    if (!q_a || !q_b || !out || !workspace || workspace_bytes < L.total)
+        return pfail(ctx, QK_EARG, "qk_knit_lowrank: null rows / output, or workspace below qk_knit_lowrank_workspace_bytes");
+    if (hipSetDevice(ctx->device) != hipSuccess) return pfail(ctx, QK_EHIP, "qk_knit_lowrank: hipSetDevice");
+    char* ws = static_cast<char*>(workspace);
+    auto D = [&](int64_t off) { return reinterpret_cast<double*>(ws + off); };
+    const int K = p->terms;
+    const int64_t NA = int64_t(1) << __builtin_popcountll(p->mask_a), NB = int64_t(1) << __builtin_popcountll(p->mask_b);
+    double *XA = D(L.xa), *XB = D(L.xb), *G = D(L.g), *U = D(L.u);
+    int32_t* r = reinterpret_cast<int32_t*>(ws + L.r);
+    int32_t* k = reinterpret_cast<int32_t*>(ws + L.k);
+    rc = qk_prep_operands(ctx, K, (int)p->rows_a, p->wt_a, q_a, NA, NA, XA, (int)p->rows_b, p->wt_b, q_b, NB, NB, XB,
+                          p->probes, G, G + K * K, U, D(L.prep), L.prep_bytes);
+    if (!rc) rc = qk_rank_factors(ctx, K, G, G + K * K, p->lam_tol, p->s_tol, p->s_abs, LR_RMAX, D(L.ta), D(L.tb), r);
+    if (!rc) rc = qk_compress_operands(ctx, K, LR_RMAX, D(L.ta), XA, NA, D(L.a2), D(L.tb), XB, NB, D(L.b2));
+    if (!rc)
+        rc = qk_probe_errors(ctx, K, LR_RMAX, XA, NA, NA, D(L.a2), NA, U, D(L.b2), NB, NB, p->probes, NB, D(L.e2), r,
+                             p->rank_tol, k, D(L.err), D(L.probe), L.probe_bytes);
+    if (!rc)
+        rc = qk_knit_outer_stream_range(ctx, p->nbits, LR_RMAX, D(L.a2), NA, D(L.b2), NB, p->mask_a, p->mask_b, 0,
+                                        int64_t(1) << p->nbits, k, out);
+    if (rc) return rc;
+    int64_t* ka = L.ka >= 0 ? reinterpret_cast<int64_t*>(ws + L.ka) : nullptr;
+    int64_t* kb = L.kb >= 0 ? reinterpret_cast<int64_t*>(ws + L.kb) : nullptr;
+    if (ka) hipLaunchKernelGGL(qk_pdep_keys_kernel, dim3(grid_of(NA)), dim3(256), 0, ctx->stream, NA, p->mask_a, ka);
+    if (kb) hipLaunchKernelGGL(qk_pdep_keys_kernel, dim3(grid_of(NB)), dim3(256), 0, ctx->stream, NB, p->mask_b, kb);
+    const int64_t sa = ka ? 0 : int64_t(1) << __builtin_ctzll(p->mask_a);
+    const int64_t sb = kb ? 0 : int64_t(1) << __builtin_ctzll(p->mask_b);
+    rc = qk_gemm_keyed_pred(ctx, NA, NB, K, XA, NA, XB, NB, ka, sa, kb, sb, out, 0, k);
+    if (rc) return rc;
+    if (rank_out) hipLaunchKernelGGL(qk_copy_i32_kernel, dim3(1), dim3(1), 0, ctx->stream, k, rank_out);
+    if (hipGetLastError() != hipSuccess) return pfail(ctx, QK_EHIP, "qk_knit_lowrank: launch failed");
+    return QK_OK;
+}
+
+}  // extern "C"

@@ -2,8 +2,9 @@
 //
 // Device form of data_rank.rank_factors (see that module for the math): pivoted Cholesky of the two
 // Gram matrices GA = A A^T, GB = B B^T (one wave per side, stopped on the residual trace), core
-// C = L_A^T L_B, its SVD by one-sided (Hestenes) Jacobi rotations on C's columns, the numerical rank r,
-// and T_X = S_r^{1/2} V_r^T L_X[P_X]^{-1} in the pivot columns, written as [rmax][K] (rows >= r zero)
+// C = L_A^T L_B, its rank-revealing LU with complete pivoting C ~= X Y^T (balanced columns), the rank r
+// = pivots above the cut, and T_A = X^T L_A[P_A]^{-1}, T_B = Y^T L_B[P_B]^{-1} in the pivot columns,
+// written as [rmax][K] (rows >= r zero)
 // with r in *r_out. r_out = 0 means "no usable factorisation" (R = 0, no convergence within 32 pivot
 // steps, or r > rmax): the caller's exact contraction then runs (predicated on the same int).
 // The step that consumes these verifies the compressed product on the real operands
@@ -20,7 +21,6 @@ constexpr int RK_K = 64;   // operand rows (K) the kernel handles
 constexpr int RK_RC = 32;  // pivoted-Cholesky steps per side
 constexpr int RK_R = 8;    // largest rank written (rows of TA / TB)
 constexpr int RK_THREADS = 128;
-constexpr int RK_MAX_SWEEPS = 40;
 
 #ifdef QK_RANK_DEBUG  // tuning builds only (tools/build_variants.py): phase clocks + Jacobi sweep count
 __device__ long long qk_rank_dbg[8];
@@ -117,12 +117,11 @@ __device__ __forceinline__ void wargmax(double& v, int& idx) {
 __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a) {
     __shared__ double G[2][RK_K][RK_K + 1];
     __shared__ double L[2][RK_K][RK_RC + 1];
-    __shared__ double C[RK_RC][RK_RC + 1];   // core, then U S in its columns
-    __shared__ double W[RK_RC][RK_RC + 1];   // right rotations
+    __shared__ double C[RK_RC][RK_RC + 1];   // core, then the LU's residual
+    __shared__ double Xs[RK_RC][RK_R + 2];   // balanced LU factor columns x_t, y_t
+    __shared__ double Ys[RK_RC][RK_R + 2];
     __shared__ double Y[2][RK_R][RK_RC];     // triangular-solve results
-    __shared__ double sv[RK_RC];
-    __shared__ int piv[2][RK_RC], nsteps[2], conv[2], order[RK_RC], rank_s, chol_live[2][2];
-    __shared__ double cnorm2;
+    __shared__ int piv[2][RK_RC], nsteps[2], conv[2], rank_s, chol_live[2][2];
     __shared__ double Ts[2][RK_R][RK_K];       // T_A, T_B
 
     const int tid = threadIdx.x, lane = tid & 63, side = tid >> 6, K = a.K;
@@ -206,7 +205,7 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
     bool ok = conv[0] && conv[1] && ra > 0 && rb > 0;
     RK_STAMP(1)
 
-    // ---- 2. core C = L_A^T L_B, W = I
+    // ---- 2. core C = L_A^T L_B
     if (ok) {
         for (int e = tid; e < ra * rb; e += RK_THREADS) {
             const int i = e / rb, j = e % rb;
@@ -214,197 +213,73 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
             for (int k = 0; k < K; ++k) s += L[0][k][i] * L[1][k][j];
             C[i][j] = s;
         }
-        for (int e = tid; e < rb * rb; e += RK_THREADS) W[e / rb][e % rb] = (e / rb == e % rb) ? 1.0 : 0.0;
-    }
-    __syncthreads();
-
-    // ---- 3. one-sided Jacobi on C's columns (round-robin pairs, one thread group per pair). Pairs of
-    // columns both below 1e-15 of the largest column norm are left alone: their singular values are
-    // far under the rank cut (s_tol = 1e-13), and rotating rounding noise would keep the sweeps going
-    if (ok && tid == 0) {
-        double m = 0.0;
-        for (int j = 0; j < rb; ++j) {
-            double c2 = 0.0;
-            for (int i = 0; i < ra; ++i) c2 += C[i][j] * C[i][j];
-            m = fmax(m, c2);
-        }
-        cnorm2 = m;
-    }
-    __syncthreads();
-    if (ok && rb > 1 && ra <= 8 && rb <= 8 && side == 0) {
-        // Register form for cores of at most 8 x 8 (syc 32 5: the common case): lane 8 j + i holds
-        // C[i][j] and W[i][j]; a round's partner column comes by one ds_bpermute per matrix and the
-        // column sums by 3-step DPP reductions over the column's 8 lanes, so a round is a short
-        // register chain instead of LDS round trips (same rotations, same pairing, same stopping rule
-        // as the LDS form below)
-        const int i = lane & 7, j = lane >> 3;
-        const double floor2 = 1e-30 * cnorm2;
-        double c = (i < ra && j < rb) ? C[i][j] : 0.0;
-        double w = (i < rb && j < rb) ? W[i][j] : 0.0;
-        const int n = rb + (rb & 1);
-        auto perm = [](double v, int src_lane) {
-            int2 x = *reinterpret_cast<int2*>(&v);
-            x.x = __builtin_amdgcn_ds_bpermute(src_lane << 2, x.x);
-            x.y = __builtin_amdgcn_ds_bpermute(src_lane << 2, x.y);
-            return *reinterpret_cast<double*>(&x);
-        };
-        for (int sweep = 0; sweep < RK_MAX_SWEEPS; ++sweep) {
-            bool rot = false;
-            for (int round = 0; round < n - 1; ++round) {
-                // partner of column j in this round (the LDS form's round-robin pairs)
-                int pj;
-                if (j == n - 1) pj = round;
-                else if (j == round) pj = n - 1;
-                else pj = (2 * round - j + 2 * (n - 1)) % (n - 1);
-                const bool live = j < n && pj < rb && j < rb;
-                const int src = (pj & 7) * 8 + i;
-                const double cq = perm(c, src), wq = perm(w, src);
-                double own = c * c, oth = cq * cq, cross = c * cq;
-                own += dppd<DPP_XOR1>(own);
-                oth += dppd<DPP_XOR1>(oth);
-                cross += dppd<DPP_XOR1>(cross);
-                own += dppd<DPP_XOR2>(own);
-                oth += dppd<DPP_XOR2>(oth);
-                cross += dppd<DPP_XOR2>(cross);
-                own += dppd<DPP_HALF_MIRROR>(own);
-                oth += dppd<DPP_HALF_MIRROR>(oth);
-                cross += dppd<DPP_HALF_MIRROR>(cross);
-                const bool lo = j < pj;  // column p of the pair (p < q)
-                const double al = lo ? own : oth, be = lo ? oth : own, ga = cross;
-                if (live && ga != 0.0 && fabs(ga) > 1e-13 * sqrt(al * be) && fmax(al, be) > floor2) {
-                    const double zeta = (be - al) * 0.5 * rcp_d(ga);
-                    const double ww = 1.0 + zeta * zeta;
-                    const double tt = copysign(rcp_d(fabs(zeta) + ww * rsq_d(ww)), zeta);
-                    const double cs = rsq_d(1.0 + tt * tt), sn = cs * tt;
-                    // p: c' = cs c_p - sn c_q;  q: c' = sn c_p + cs c_q
-                    c = lo ? cs * c - sn * cq : sn * cq + cs * c;
-                    w = lo ? cs * w - sn * wq : sn * wq + cs * w;
-                    rot = true;
-                }
-            }
-#ifdef QK_RANK_DEBUG
-            if (lane == 0) qk_rank_dbg[5] = sweep + 1;
-#endif
-            if (!__any(rot)) break;
-        }
-        if (i < ra && j < rb) C[i][j] = c;
-        if (i < rb && j < rb) W[i][j] = w;
-    } else if (ok && rb > 1 && side == 0) {  // wave 0 alone: rounds are ordered by the wave's own LDS traffic
-        const double floor2 = 1e-30 * cnorm2;
-        const int n = rb + (rb & 1), npair = n / 2;
-        int tpp = 64 / npair;
-        int pw = 1;
-        while (pw * 2 <= tpp) pw *= 2;
-        tpp = pw;  // power of two lanes per pair
-        const int g = lane / tpp, t = lane % tpp;
-        for (int sweep = 0; sweep < RK_MAX_SWEEPS; ++sweep) {
-            bool rot = false;
-            for (int round = 0; round < n - 1; ++round) {
-                int p = -1, q = -1;
-                if (g < npair) {
-                    if (g == 0) {
-                        p = round;
-                        q = n - 1;
-                    } else {
-                        p = (round + g) % (n - 1);
-                        q = (round - g + (n - 1)) % (n - 1);
-                    }
-                    if (p > q) {
-                        const int x = p;
-                        p = q;
-                        q = x;
-                    }
-                }
-                const bool live = g < npair && q < rb;
-                double al = 0.0, be = 0.0, ga = 0.0;
-                if (live)
-                    for (int i = t; i < ra; i += tpp) {
-                        const double cp = C[i][p], cq = C[i][q];
-                        al += cp * cp;
-                        be += cq * cq;
-                        ga += cp * cq;
-                    }
-                al = wsum(al, tpp);
-                be = wsum(be, tpp);
-                ga = wsum(ga, tpp);
-                // the factors only need to be good enough for the probe check that follows (1e-13
-                // relative orthogonality instead of 1e-15: fewer sweeps chasing rounding)
-                if (live && ga != 0.0 && fabs(ga) > 1e-13 * sqrt(al * be) && fmax(al, be) > floor2) {
-                    // hardware reciprocal / reciprocal-sqrt seeds + one Newton step each (full double
-                    // precision without the IEEE division / sqrt sequences): this is the serial chain
-                    // of every Jacobi round
-                    const double zeta = (be - al) * 0.5 * rcp_d(ga);
-                    const double w = 1.0 + zeta * zeta;
-                    const double tt = copysign(rcp_d(fabs(zeta) + w * rsq_d(w)), zeta);
-                    const double c = rsq_d(1.0 + tt * tt), s = c * tt;
-                    for (int i = t; i < ra; i += tpp) {
-                        const double cp = C[i][p], cq = C[i][q];
-                        C[i][p] = c * cp - s * cq;
-                        C[i][q] = s * cp + c * cq;
-                    }
-                    for (int i = t; i < rb; i += tpp) {
-                        const double wp = W[i][p], wq = W[i][q];
-                        W[i][p] = c * wp - s * wq;
-                        W[i][q] = s * wp + c * wq;
-                    }
-                    rot = true;
-                }
-                // this round's column writes land before the next round's reads (same wave: LDS is in order)
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-            }
-#ifdef QK_RANK_DEBUG
-            if (lane == 0) qk_rank_dbg[5] = sweep + 1;
-#endif
-            if (!__any(rot)) break;
-        }
-    }
-    __syncthreads();
-
-    RK_STAMP(2)
-    // ---- 4. singular values (column norms), descending order, rank
-    if (ok && tid < rb) {
-        double s = 0.0;
-        for (int i = 0; i < ra; ++i) s += C[i][tid] * C[i][tid];
-        sv[tid] = sqrt(s);
-    }
-    __syncthreads();
-    if (tid == 0) {
-        int r = 0;
-        if (ok) {
-            for (int j = 0; j < rb; ++j) order[j] = j;
-            for (int j = 0; j < rb; ++j)  // selection sort, stable
-                for (int k = j + 1; k < rb; ++k)
-                    if (sv[order[k]] > sv[order[j]]) {
-                        const int x = order[j];
-                        order[j] = order[k];
-                        order[k] = x;
-                    }
-            const double s0 = sv[order[0]];
-            const double cut = fmax(a.s_tol * s0, a.s_abs);
-            if (s0 > 0.0)
-                for (int j = 0; j < rb; ++j) r += sv[order[j]] > cut ? 1 : 0;
-            if (r > a.rmax || r > ra) r = 0;
-        }
-        rank_s = r;
     }
     for (int e = tid; e < 2 * RK_R * RK_K; e += RK_THREADS) (&Ts[0][0][0])[e] = 0.0;
     __syncthreads();
+    RK_STAMP(2)
+
+    // ---- 3. complete-pivoting LU of the core (data_rank.cross_factors), wave 0: pivot t is the
+    // residual's largest |entry| (lowest row-major index on ties), x_t = C[:, j] / sqrt|p|,
+    // y_t = sign(p) C[i, :] / sqrt|p|, C -= x_t y_t^T; stop when the largest residual entry is at most
+    // max(s_tol |p_0|, s_abs). At most rmax + 1 pivots: a (rmax + 1)-th one above the cut means r > rmax.
+    // (Replaces round 2's one-sided Jacobi SVD of the core: ~9 sweeps x 7 rounds of serial rotations,
+    // 25 us, for the same rank decision.)
+    if (side == 0) {
+        int r = 0;
+        if (ok) {
+            const int n = ra * rb;
+            const int tmax = (ra < rb ? ra : rb) < a.rmax + 1 ? (ra < rb ? ra : rb) : a.rmax + 1;
+            double cut = 0.0;
+            for (int t = 0; t < tmax; ++t) {
+                double v = -1.0;
+                int idx = 1 << 30;
+                for (int e = lane; e < n; e += 64) {
+                    const double m = fabs(C[e / rb][e % rb]);
+                    if (m > v) {  // ascending e: the first of equal entries stays
+                        v = m;
+                        idx = e;
+                    }
+                }
+                wargmax(v, idx);
+                if (t == 0) cut = fmax(a.s_tol * v, a.s_abs);
+                if (!(v > cut)) break;
+                const int pi = idx / rb, pj = idx % rb;
+                const double p = C[pi][pj];
+                const double sc = 1.0 / sqrt(fabs(p));
+                const double xv = lane < ra ? C[lane][pj] * sc : 0.0;
+                const double yv = lane < rb ? C[pi][lane] * (p > 0.0 ? sc : -sc) : 0.0;
+                if (lane < ra) Xs[lane][t] = xv;
+                if (lane < rb) Ys[lane][t] = yv;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                for (int e = lane; e < n; e += 64) {
+                    const int i = e / rb, j = e % rb;
+                    C[i][j] = fma(-Xs[i][t], Ys[j][t], C[i][j]);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                r = t + 1;
+            }
+            if (r > a.rmax || r > ra) r = 0;
+        }
+        if (lane == 0) rank_s = r;
+    }
+    __syncthreads();
+    RK_STAMP(5)
     const int r = rank_s;
 
-    // ---- 5. T_X[j][piv_X[i]] = sqrt(s_j) y_i,  L_X[P_X]^T y = v_j  (back-substitution, one thread each)
+    // ---- 4. T_A[t][piv_A[i]] = y_i with L_A[P_A]^T y = x_t (T_B alike with y_t): back-substitution,
+    // one thread per (side, t)
     if (tid < 2 * r) {
-        const int sd = tid / r, j = tid % r, col = order[j];
+        const int sd = tid / r, t = tid % r;
         const int rx = sd ? rb : ra;
-        const double sj = sv[col];
-        double* y = Y[sd][j];
+        double* y = Y[sd][t];
         for (int i = rx - 1; i >= 0; --i) {
-            double v = sd ? W[i][col] : C[i][col] / sj;
+            double v = sd ? Ys[i][t] : Xs[i][t];
             for (int k = i + 1; k < rx; ++k) v -= L[sd][piv[sd][k]][i] * y[k];
             y[i] = v / L[sd][piv[sd][i]][i];
         }
-        const double rs = sqrt(sj);
-        for (int i = 0; i < rx; ++i) Ts[sd][j][piv[sd][i]] = rs * y[i];
+        for (int i = 0; i < rx; ++i) Ts[sd][t][piv[sd][i]] = y[i];
     }
     __syncthreads();
     for (int e = tid; e < a.rmax * K; e += RK_THREADS) {

@@ -15,10 +15,17 @@ Steps, on ``GA = A A^T`` and ``GB = B B^T`` ([K, K]):
    terms of the operand, ``A = L_A Q_A + E_A`` with orthonormal rows ``Q_A`` spanning the pivot rows
    of ``A`` and ``||E_A||_F^2 = trace(E)``; the pivot rows lie in that span exactly, so
    ``Q_A = L_A[P_A]^{-1} A[P_A]`` (``L_A[P_A]``: lower triangular).
-2. Core ``C = L_A^T L_B`` ([r_A, r_B]): ``R ~= Q_A^T C Q_B``; SVD ``C = U S W^T``.
-3. Rank ``r`` = singular values above ``max(s_tol * s_0, s_abs)``.
-4. ``T_A = S_r^{1/2} U_r^T L_A[P_A]^{-1}`` placed in the pivot columns (``[r, K]``), ``T_B`` alike with
-   ``W``: ``R ~= (T_A A)^T (T_B B)``.
+2. Core ``C = L_A^T L_B`` ([r_A, r_B]): ``R ~= Q_A^T C Q_B``.
+3. Rank-revealing LU of the core with complete pivoting (cross approximation): pivot ``t`` is the
+   largest ``|entry|`` of the residual ``C_t`` (ties: lowest row-major index), ``x_t = C_t[:, j] /
+   sqrt|p|``, ``y_t = sign(p) C_t[i, :] / sqrt|p|``, ``C_{t+1} = C_t - x_t y_t^T``; stop when the
+   residual's largest entry is at most ``max(s_tol * |p_0|, s_abs)`` (its spectral norm is then at
+   most ``sqrt(r_A r_B)`` times that, and so is every moved entry of ``R``). ``C ~= X Y^T`` with balanced
+   columns, ``r`` = the pivots taken. (Earlier rounds took the core's SVD by one-sided Jacobi: 25 us
+   of serial rotations on the device for the same rank decision; the probe check below is what
+   certifies either.)
+4. ``T_A = X^T L_A[P_A]^{-1}`` placed in the pivot columns (``[r, K]``), ``T_B = Y^T L_B[P_B]^{-1}``:
+   ``R ~= (T_A A)^T (T_B B)``.
 
 Nothing here is trusted for accuracy: the Grams square the condition number, so the caller verifies
 the compressed product on the real operands against fixed Gaussian probes (``qk_probe_errors``,
@@ -66,12 +73,36 @@ def pivoted_cholesky(G: np.ndarray, lam_tol: float = LAM_TOL, rc_max: int = RC_M
     return L[:, :len(piv)], piv, False
 
 
-def _side_factor(L: np.ndarray, piv: list, V: np.ndarray, s: np.ndarray, K: int) -> np.ndarray:
-    """``S^{1/2} V^T L[P]^{-1}`` in the pivot columns of a [r, K] matrix."""
+def cross_factors(C: np.ndarray, s_tol: float = S_TOL, s_abs: float = S_ABS, rmax: int = R_MAX):
+    """``(X [r_A, r], Y [r_B, r])`` with ``C ~= X Y^T`` by complete-pivoting LU (module doc, step 3);
+    ``r`` may exceed ``rmax`` by one (the caller rejects that), 0 when ``C = 0``."""
+    R = np.array(C, dtype=np.float64)
+    ra, rb = R.shape
+    X, Y = [], []
+    p0 = float(np.abs(R).max()) if R.size else 0.0
+    if p0 <= 0:
+        return np.zeros((ra, 0)), np.zeros((rb, 0))
+    cut = max(s_tol * p0, s_abs)
+    for _ in range(min(ra, rb, rmax + 1)):
+        flat = int(np.argmax(np.abs(R)))  # first (row-major) on ties
+        i, j = divmod(flat, rb)
+        p = R[i, j]
+        if not abs(p) > cut:
+            break
+        sc = 1.0 / np.sqrt(abs(p))
+        x, y = R[:, j] * sc, R[i, :] * (sc if p > 0 else -sc)
+        R = R - np.outer(x, y)
+        X.append(x)
+        Y.append(y)
+    return np.array(X).T.reshape(ra, -1), np.array(Y).T.reshape(rb, -1)
+
+
+def _side_factor(L: np.ndarray, piv: list, V: np.ndarray, K: int) -> np.ndarray:
+    """``V^T L[P]^{-1}`` in the pivot columns of a [r, K] matrix."""
     LP = np.tril(L[piv])  # lower triangular up to rounding (a pivot row's later columns vanish)
     Y = np.linalg.solve(LP.T, V)  # L[P]^T Y = V  ->  Y^T = V^T L[P]^{-1}
     T = np.zeros((V.shape[1], K))
-    T[:, piv] = (Y * np.sqrt(s)[None, :]).T
+    T[:, piv] = Y.T
     return T
 
 
@@ -85,13 +116,11 @@ def rank_factors(GA: np.ndarray, GB: np.ndarray, lam_tol: float = LAM_TOL, s_tol
     LB, pb, okb = pivoted_cholesky(GB, lam_tol, rc_max)
     if not (oka and okb) or not pa or not pb:
         return None
-    U, s, Wt = np.linalg.svd(LA.T @ LB)
-    if s.size == 0 or s[0] <= 0:
-        return None
-    r = int((s > max(s_tol * s[0], s_abs)).sum())
+    X, Y = cross_factors(LA.T @ LB, s_tol, s_abs, rmax)
+    r = X.shape[1]
     if r == 0 or r > rmax:
         return None
-    return _side_factor(LA, pa, U[:, :r], s[:r], K), _side_factor(LB, pb, Wt[:r].T, s[:r], K)
+    return _side_factor(LA, pa, X, K), _side_factor(LB, pb, Y, K)
 
 
 # the engine's historical name (pipeline host path, tests)

@@ -895,6 +895,22 @@ def _endpoints(virt, j):
     return out
 
 
+def factored_ok(virt) -> bool:
+    """Whether the factored knit (per-gate rank factors split between two fragments, basis reduction
+    on each fragment's slots) applies: every virtual gate joins two different fragments. A gate with
+    both endpoints in one fragment (allowed by the reference's label logic, vc:39-48,50-68) takes
+    the direct knit over all global labels instead."""
+    frag_of = {}
+    for frag in virt.fragment_circuits:
+        for q in frag:
+            frag_of[q] = frag
+    for instr in virt.vgate_instructions:
+        a, b = instr.qubits[0], instr.qubits[1]
+        if frag_of.get(a) is frag_of.get(b):
+            return False
+    return True
+
+
 def _fragment_sides(virt, fs: FragmentState):
     sides = [None] * len(virt.vgate_instructions)
     members = set(fs.fragment)
@@ -967,6 +983,74 @@ def knit_plan_c(ctx: Context, virt, frags: list, qs: list, factored: bool = Fals
     ctx.check(ctx.lib.qk_knit(ctx.handle, ctypes.byref(plan), qp, ws.data_ptr(), ws.numel(), out.data_ptr()), "qk_knit")
     torch().cuda.current_stream(ctx.device).synchronize()  # Ws / ws / qc die with this frame
     return out
+
+
+def knit_lowrank_c(ctx: Context, pipe, qs: list, out=None, rank_tol: float | None = None):
+    """The single-GPU data-rank knit through the one-call C entry ``qk_knit_lowrank`` (what a host
+    that is not Python calls) with a pipeline's plan: its device transforms, clbit
+    masks, probes and tolerances. Returns ``(out [2^N], accepted rank: device int32 [1])``."""
+    from . import data_rank as dr
+
+    T = torch()
+    ia, ib = pipe.order[0], pipe.order[-1]
+    WA, WB = pipe.transforms[ia], pipe.transforms[ib]
+    assert WA is not None and WB is not None, "qk_knit_lowrank needs the factored (transform) knit"
+    qa, qb = qs[ia].contiguous(), qs[ib].contiguous()
+    probes = pipe._probes(qb.shape[1], qb.device)
+    plan = _lib.QkLowrankPlan(pipe.N, WA.shape[1], WA.shape[0], WB.shape[0],
+                              sum(1 << c for c in pipe.ops.clbits[ia]), sum(1 << c for c in pipe.ops.clbits[ib]),
+                              WA.data_ptr(), WB.data_ptr(), probes.data_ptr(), dr.LAM_TOL, dr.S_TOL, dr.S_ABS,
+                              pipe.rank_tol if rank_tol is None else rank_tol)
+    need = ctypes.c_int64()
+    ctx.check(ctx.lib.qk_knit_lowrank_workspace_bytes(ctx.handle, ctypes.byref(plan), ctypes.byref(need)),
+              "qk_knit_lowrank_workspace_bytes")
+    ws = T.empty(max(need.value, 1), dtype=T.uint8, device=qa.device)
+    if out is None:
+        out = T.empty(1 << pipe.N, dtype=T.float64, device=qa.device)
+    rank = T.empty(1, dtype=T.int32, device=qa.device)
+    ctx.check(ctx.lib.qk_knit_lowrank(ctx.handle, ctypes.byref(plan), qa.data_ptr(), qb.data_ptr(), ws.data_ptr(),
+                                      ws.numel(), out.data_ptr(), rank.data_ptr()), "qk_knit_lowrank")
+    torch().cuda.current_stream(ctx.device).synchronize()  # ws dies with this frame
+    return out, rank
+
+
+class Comm:
+    """An RCCL communicator owned through the C ABI (``qk_comm_init``): the collectives a host that
+    is not Python uses for the multi-GPU knit; tests drive them through ctypes."""
+
+    def __init__(self, ctx: Context, uid: bytes, nranks: int, rank: int):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        ctx.check(ctx.lib.qk_comm_init(ctx.handle, buf, nranks, rank, ctypes.byref(h)), "qk_comm_init")
+        self.handle = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * 128)()
+        _lib.check(None, _lib.lib().qk_comm_unique_id(buf), "qk_comm_unique_id")
+        return bytes(buf)
+
+    def allreduce(self, send, recv):
+        self.ctx.check(self.ctx.lib.qk_allreduce(self.ctx.handle, self.handle, send.data_ptr(), recv.data_ptr(),
+                                                 send.numel()), "qk_allreduce")
+
+    def reduce(self, send, recv, root: int = 0):
+        self.ctx.check(self.ctx.lib.qk_reduce(self.ctx.handle, self.handle, send.data_ptr(), _ptr(recv), send.numel(),
+                                              root), "qk_reduce")
+
+    def allgather(self, send, recv):
+        self.ctx.check(self.ctx.lib.qk_allgather(self.ctx.handle, self.handle, send.data_ptr(), recv.data_ptr(),
+                                                 send.numel()), "qk_allgather")
+
+    def alltoall(self, send, recv, nranks: int):
+        self.ctx.check(self.ctx.lib.qk_alltoall(self.ctx.handle, self.handle, send.data_ptr(), recv.data_ptr(),
+                                                send.numel() // nranks), "qk_alltoall")
+
+    def close(self):
+        if self.handle:
+            self.ctx.lib.qk_comm_destroy(self.handle)
+            self.handle = None
 
 
 def knit_dense(ctx: Context, virt, frags: list[FragmentState], qs: list, out=None,

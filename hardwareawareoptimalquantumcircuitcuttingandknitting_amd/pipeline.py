@@ -328,6 +328,8 @@ class KnitPipeline:
         self.T = engine.torch()
         self.virt = virt
         self.rank, self.world, self.group = rank, world, group
+        # a virtual gate with both endpoints in one fragment: the direct knit (engine.factored_ok)
+        factored = factored and engine.factored_ok(virt)
         self.factored = factored
         # light_cone (factored knit): exact light-cone projections in the basis reduction and the
         # rank-compressed two-fragment core (fragment_program.slot_relevance,

@@ -79,7 +79,7 @@ def _direct_dense(virt: VirtualCircuit, shots: int, device: int, factored: bool,
     ctx = engine.get_context(device)
     # The factored knit folds labels whose side programs coincide into one operand row; sampled
     # labels differ in their shots even then, so sampling knits directly over the labels.
-    factored = factored and not sample
+    factored = factored and not sample and engine.factored_ok(virt)
     now = perf_counter()
     native = all(isinstance(virt.get_backend(f), MI355XBackend) for f in virt.fragment_circuits if len(f))
     frags = engine.prepare_fragments(virt, device, basis=factored and native and not sample)
@@ -159,14 +159,13 @@ def _build_plan(virt: VirtualCircuit, device: int):
     """The benchmarked engine (bench.py): factored knit with light-cone basis + rank-compressed core
     and the per-step device data rank (``pipeline.KnitPipeline``). A circuit the
     factored planner refuses (a virtual gate with both endpoints in one fragment) gets the direct
-    knit over all global labels through the same pipeline."""
+    knit over all global labels through the same pipeline (``engine.factored_ok``)."""
     from .pipeline import KnitPipeline
 
-    try:
-        return KnitPipeline(virt, device=device, factored=True)
-    except NotImplementedError as e:
-        log.info("factored plan refused (%s): direct knit", e)
+    if not engine.factored_ok(virt):
+        log.info("a virtual gate with both endpoints in one fragment: direct knit")
         return KnitPipeline(virt, device=device, factored=False)
+    return KnitPipeline(virt, device=device, factored=True)
 
 
 def cached_plan(virt: VirtualCircuit, device: int = 0):
@@ -292,11 +291,9 @@ def run_virtual_circuit_sharded(virt: VirtualCircuit, group=None, *, device: int
              len(virt.fragment_circuits), tuple(len(f) for f in virt.fragment_circuits),
              len(virt.vgate_instructions), world)
     kw = {"backend": backend} if backend is not None else {}
-    try:
+    pipe = None
+    if engine.factored_ok(virt):  # else (both endpoints of a gate in one fragment): direct knit, reduce mode
         pipe = KnitPipeline(virt, device=device, factored=True, rank=rank, world=world, group=group, **kw)
-    except NotImplementedError as e:  # the factored planner refused the circuit: direct knit, reduce mode
-        log.info("factored plan refused (%s): direct knit", e)
-        pipe = None
     if pipe is None or pipe.mode != "slice":
         pipe = KnitPipeline(virt, device=device, factored=False, rank=rank, world=world, group=group,
                             mode="reduce", **kw)

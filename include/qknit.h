@@ -245,6 +245,50 @@ int qk_knit_workspace_bytes(const qk_knit_plan* plan, int64_t* bytes);
 int qk_knit(qk_ctx* ctx, const qk_knit_plan* plan, const double* const* q, void* workspace, int64_t workspace_bytes,
             double* out);
 
+/* ---- plan-level low-rank knit: the benched single-GPU step's knit in one call (qknit_plan.hip) ----
+ * KnitPipeline's device data rank for a two-fragment knit, chained on the context's
+ * stream with no host synchronisation: qk_prep_operands -> qk_rank_factors -> qk_compress_operands ->
+ * qk_probe_errors -> qk_knit_outer_stream_range (write-bound, K = accepted rank) -> qk_gemm_keyed_pred
+ * (the exact terms-wide contraction, runs only when the check rejected). Same result as qk_knit on the
+ * same transforms within the probe tolerance. q_a / q_b: the swept rows ([rows][2^popcount(mask)]).
+ * *rank_out (DEVICE int32, may be NULL): the accepted rank, 0 when the exact contraction ran.
+ * Replaces virtual_circuit.py:50-68 (merge + per-gate knits) for hosts that are not Python. */
+typedef struct qk_lowrank_plan {
+    int32_t nbits;           /* output clbits (2 <= nbits <= 32): out has 2^nbits entries, all written */
+    int32_t terms;           /* K: contraction terms (light-cone transforms), even, <= 64 */
+    int64_t rows_a, rows_b;  /* swept rows of the two fragments */
+    uint64_t mask_a, mask_b; /* clbit masks: disjoint, covering the nbits output bits, bit 0 in mask_b,
+                                >= 7 bits each */
+    const double* wt_a;      /* DEVICE [rows_a][terms] */
+    const double* wt_b;      /* DEVICE [rows_b][terms] */
+    const double* probes;    /* DEVICE [16][2^popcount(mask_b)]: fixed Gaussian probe vectors */
+    double lam_tol, s_tol, s_abs;  /* qk_rank_factors tolerances (data_rank.py LAM_TOL / S_TOL / S_ABS) */
+    double rank_tol;         /* probe acceptance bound (KnitPipeline.rank_tol) */
+} qk_lowrank_plan;
+
+int qk_knit_lowrank_workspace_bytes(qk_ctx* ctx, const qk_lowrank_plan* plan, int64_t* bytes);
+int qk_knit_lowrank(qk_ctx* ctx, const qk_lowrank_plan* plan, const double* q_a, const double* q_b, void* workspace,
+                    int64_t workspace_bytes, double* out, int32_t* rank_out);
+
+/* ---- collectives (qknit_comm.hip: RCCL over xGMI) ----------------------------------------------
+ * The reference's Pool(8) sum of partial knits (run.py:64-67) across GPUs, for a host that is not
+ * Python: one process per GPU; rank 0 calls qk_comm_unique_id and the host hands the 128 bytes to
+ * every rank (MPI, a file, torch.distributed), then each calls qk_comm_init with its context. The
+ * collectives run on the context's stream over fp64 element counts (sums). Reduce mode = each rank's
+ * partial qk_knit over its label slice + qk_reduce to the root; slice mode's exchanges
+ * are qk_alltoall (column blocks), qk_allreduce (Grams, probe errors) and qk_allgather (compressed
+ * operands). */
+#define QK_COMM_ID_BYTES 128
+typedef struct qk_comm qk_comm;
+int qk_comm_unique_id(uint8_t* id);
+int qk_comm_init(qk_ctx* ctx, const uint8_t* id, int nranks, int rank, qk_comm** out);
+int qk_comm_destroy(qk_comm* comm);
+int qk_comm_size(qk_comm* comm, int* nranks, int* rank);
+int qk_allreduce(qk_ctx* ctx, qk_comm* comm, const double* send, double* recv, int64_t count);
+int qk_reduce(qk_ctx* ctx, qk_comm* comm, const double* send, double* recv, int64_t count, int root);
+int qk_allgather(qk_ctx* ctx, qk_comm* comm, const double* send, double* recv, int64_t count);
+int qk_alltoall(qk_ctx* ctx, qk_comm* comm, const double* send, double* recv, int64_t count);
+
 /* ---- data-rank factors (qknit_rank.hip; data_rank.py is the host form) ----------------------
  * Two-fragment knit R = A^T B (A: [K][M], B: [K][N] operands of virtual_circuit.py:50-68's knit)
  * from its Gram matrices GA = A A^T, GB = B B^T ([K][K], DEVICE): pivoted Cholesky of each Gram

@@ -156,3 +156,26 @@ def light_cone(seed: int = 13):
     for i, q in enumerate([1, 2, 3, 4, 5]):
         qc.measure(q, i)
     return qc, cut_circuit(qc, CutSpec([[0, 1, 2], [3, 4, 5]], cuts))
+
+
+def same_fragment_cut(seed: int = 13):
+    """A cross-fragment CX cut plus a cut CX whose two qubits sit in the SAME fragment: that virtual
+    gate's two endpoints both live in fragment 0 (the reference's label / knit logic, vc:39-48,50-68,
+    handles it generically; the factored planner refuses it and the engine falls back)."""
+    rng = random.Random(seed)
+    n0, n1 = 3, 2
+    qr = QuantumRegister(n0 + n1, "q")
+    qc = QuantumCircuit(qr)
+    left, right = [0, 1, 2], [3, 4]
+    _rand_layer(qc, range(5), rng)
+    qc.cx(2, 3)
+    cut_idx = [len(qc.data) - 1]
+    _rand_layer(qc, range(5), rng)
+    qc.cx(0, 1)
+    cut_idx.append(len(qc.data) - 1)
+    _rand_layer(qc, range(5), rng)
+    qc.cx(1, 2)
+    qc.cx(4, 3)
+    _rand_layer(qc, range(5), rng)
+    qc.measure_all()
+    return qc, cut_circuit(qc, CutSpec([left, right], cut_idx))

@@ -17,7 +17,7 @@ Fixtures:
                         syc 32 5) on exact instances restricted to 64 seeded outcomes per fragment:
                         4096 exact entries of the full distribution (make_knit_samples)
 
-Usage: python tests/golden/make_golden.py [--samples [config ...]]
+Usage: python tests/golden/make_golden.py [--samples [config ...] | --knit case ...]
 """
 import json
 import math
@@ -432,7 +432,14 @@ def main():
         "cp": circuits.two_fragment("cp"), "cx_3cuts": circuits.two_fragment("cx", 3, 3, n_cuts=3),
         "move": circuits.wire_cut(), "move_gate": circuits.wire_cut(3, 2, extra_gate_cut=True),
         "three": circuits.three_fragment(), "partial": circuits.partial_measure(),
+        "same_fragment": circuits.same_fragment_cut(),
     }
+    only = sys.argv[2:] if len(sys.argv) > 2 and sys.argv[1] == "--knit" else None
+    if only:  # regenerate just these knit fixtures
+        for k in only:
+            dump(f"knit_{k}.json", make_knit(qd, vg, vc, cases[k][1], k))
+        print("wrote", only)
+        return
     for key in ("bv_5_1_p2", "hwe_16_1_p2", "hwe_16_1_p3"):
         name, n, d, p, var = cutting.BASELINE_CONFIGS[key]
         circ, cut, _ = cutting.config_cut_circuit(name, n, d, p, var)

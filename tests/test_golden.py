@@ -130,6 +130,7 @@ def _case_circuits(case):
         "cp": lambda: circuits.two_fragment("cp"), "cx_3cuts": lambda: circuits.two_fragment("cx", 3, 3, n_cuts=3),
         "move": lambda: circuits.wire_cut(), "move_gate": lambda: circuits.wire_cut(3, 2, extra_gate_cut=True),
         "three": lambda: circuits.three_fragment(), "partial": lambda: circuits.partial_measure(),
+        "same_fragment": lambda: circuits.same_fragment_cut(),
     }
     if case in builders:
         return builders[case]()
