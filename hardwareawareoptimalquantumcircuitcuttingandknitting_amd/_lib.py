@@ -31,7 +31,8 @@ class QkProgram(ctypes.Structure):
 class QkLowrankPlan(ctypes.Structure):
     _fields_ = [("nbits", c_i32), ("terms", c_i32), ("rows_a", c_i64), ("rows_b", c_i64), ("mask_a", c_u64),
                 ("mask_b", c_u64), ("wt_a", c_vp), ("wt_b", c_vp), ("probes", c_vp), ("lam_tol", ctypes.c_double),
-                ("s_tol", ctypes.c_double), ("s_abs", ctypes.c_double), ("rank_tol", ctypes.c_double)]
+                ("s_tol", ctypes.c_double), ("s_abs", ctypes.c_double), ("rank_tol", ctypes.c_double),
+                ("rank_tol_rel", ctypes.c_double)]
 
 
 class QkKnitPlan(ctypes.Structure):
@@ -83,8 +84,12 @@ SIGNATURES = {
                                      c_vp]),
     "qk_probe_workspace_bytes": (c_i32, [c_vp, c_i64, ctypes.POINTER(c_i64)]),
     "qk_probe_errors": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64,
-                                c_i64, c_vp, c_i64, c_vp, c_vp, ctypes.c_double, c_vp, c_vp, c_vp, c_i64]),
-    "qk_probe_accept": (c_i32, [c_vp, c_vp, ctypes.c_int, c_vp, ctypes.c_double, c_vp, c_vp]),
+                                c_i64, c_vp, c_i64, c_vp, c_vp, ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp,
+                                c_i64]),
+    "qk_compress_probe_workspace_bytes": (c_i32, [c_vp, c_i64, c_i64, ctypes.POINTER(c_i64)]),
+    "qk_compress_probe": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp,
+                                  c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp, c_vp, c_i64]),
+    "qk_probe_accept": (c_i32, [c_vp, c_vp, ctypes.c_int, c_vp, ctypes.c_double, ctypes.c_double, c_vp, c_vp]),
     "qk_knit_workspace_bytes": (c_i32, [ctypes.POINTER(QkKnitPlan), ctypes.POINTER(c_i64)]),
     "qk_knit": (c_i32, [c_vp, ctypes.POINTER(QkKnitPlan), c_vp, c_vp, c_i64, c_vp]),
     "qk_khatri_rao": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),

@@ -361,7 +361,7 @@ __global__ __launch_bounds__(256) void qk_probe_d_kernel(int K, int rmax, const 
                                                          double* __restrict__ epart) {
     __shared__ double Us[PK][PNP];
     __shared__ double Vs[16][PNP];
-    __shared__ double ep[4][PNP];
+    __shared__ double ep[4][2 * PNP];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, l4 = lane >> 4;
     {
         double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(256) void qk_probe_d_kernel(int K, int rmax, const 
     }
     for (int e = tid; e < PK * PNP; e += 256) Us[e / PNP][e % PNP] = (e / PNP) < K ? U[e] : 0.0;
     __syncthreads();
-    double e2 = 0.0;
+    double e2 = 0.0, f2 = 0.0;  // squared errors and squared reference products (R p)
     const int ksteps = (K + 3) / 4;
     for (int64_t cb = (int64_t)blockIdx.x * 4 + wave; cb * 16 < NA; cb += (int64_t)gridDim.x * 4) {
         const int64_t c = cb * 16 + l16;
@@ -384,6 +384,8 @@ __global__ __launch_bounds__(256) void qk_probe_d_kernel(int K, int rmax, const 
             const double av = k < K ? XA[(int64_t)k * ldx + c] : 0.0;  // A[c][k]
             acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Us[k][l16], acc, 0, 0, 0);
         }
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) f2 = fma(acc[rr], acc[rr], f2);  // (X_A^T U)[c][p] = (R p)_c
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
             const int j = 4 * jj + l4;
@@ -395,43 +397,229 @@ __global__ __launch_bounds__(256) void qk_probe_d_kernel(int K, int rmax, const 
     }
     e2 += __shfl_xor(e2, 16, 64);
     e2 += __shfl_xor(e2, 32, 64);
-    if (l4 == 0) ep[wave][l16] = e2;
+    f2 += __shfl_xor(f2, 16, 64);
+    f2 += __shfl_xor(f2, 32, 64);
+    if (l4 == 0) {
+        ep[wave][l16] = e2;
+        ep[wave][PNP + l16] = f2;
+    }
     __syncthreads();
-    if (tid < PNP) epart[(int64_t)blockIdx.x * PNP + tid] = ep[0][tid] + ep[1][tid] + ep[2][tid] + ep[3][tid];
+    if (tid < 2 * PNP)
+        epart[(int64_t)blockIdx.x * 2 * PNP + tid] = ep[0][tid] + ep[1][tid] + ep[2][tid] + ep[3][tid];
 }
 
-// e2_out[p] = sum_b epart[b][p]; with k_out: *err_out = sqrt(max_p e2), *k_out = (r > 0 && err <= tol) ? r : 0.
-// 256 threads: thread t sums rows b = t / 16, + 16, ... of probe t % 16, then a fixed-order LDS tree.
+// rows of 32: e2[p] (squared errors) then f2[p] (squared reference products ||R p||^2).
+// e2_out[0..32) = sum_b epart[b][.]; with k_out: *err_out = sqrt(max_p e2), and the accepted rank
+// *k_out = (r > 0 && err <= max(tol, rel_tol sqrt(max_p f2))) ? r : 0 — the bound scales with the knit
+// itself (||R p|| ~ ||R||_F) above the absolute floor tol.
+// 256 threads: thread t sums rows b = t / 32, + 8, ... of entry t % 32, then a fixed-order LDS tree.
+constexpr int PE = 2 * PNP;
 __global__ __launch_bounds__(256) void qk_probe_accept_kernel(const double* __restrict__ epart, int n,
                                                               const int32_t* __restrict__ r_dev, double tol,
-                                                              double* __restrict__ e2_out, int32_t* __restrict__ k_out,
-                                                              double* __restrict__ err_out) {
+                                                              double rel_tol, double* __restrict__ e2_out,
+                                                              int32_t* __restrict__ k_out, double* __restrict__ err_out) {
     __shared__ double acc[256];
-    const int tid = threadIdx.x, p = tid % PNP;
+    const int tid = threadIdx.x, p = tid % PE;
     // eight independent partial sums (loads in flight together), combined in a fixed order
-    constexpr int STEP = 256 / PNP;
+    constexpr int STEP = 256 / PE;
     double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int b = tid / PNP;
+    int b = tid / PE;
     for (; b + 7 * STEP < n; b += 8 * STEP)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s8[u] += epart[(int64_t)(b + u * STEP) * PNP + p];
-    for (; b < n; b += STEP) s8[0] += epart[(int64_t)b * PNP + p];
+        for (int u = 0; u < 8; ++u) s8[u] += epart[(int64_t)(b + u * STEP) * PE + p];
+    for (; b < n; b += STEP) s8[0] += epart[(int64_t)b * PE + p];
     const double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     acc[tid] = s;
     __syncthreads();
-    for (int w = 128; w >= PNP; w >>= 1) {
+    for (int w = 128; w >= PE; w >>= 1) {
         if (tid < w) acc[tid] += acc[tid + w];
         __syncthreads();
     }
-    if (tid < PNP && e2_out) e2_out[tid] = acc[tid];
+    if (tid < PE && e2_out) e2_out[tid] = acc[tid];
     if (tid == 0 && k_out) {
-        double m = 0.0;
-        for (int q = 0; q < PNP; ++q) m = fmax(m, acc[q]);
+        double m = 0.0, f = 0.0;
+        for (int q = 0; q < PNP; ++q) {
+            m = fmax(m, acc[q]);
+            f = fmax(f, acc[PNP + q]);
+        }
         const double err = sqrt(m);
+        const double bound = fmax(tol, rel_tol * sqrt(f));
         const int r = *r_dev;
         if (err_out) *err_out = err;
-        *k_out = (r > 0 && err <= tol) ? r : 0;
+        *k_out = (r > 0 && err <= bound) ? r : 0;
     }
+}
+
+// ---- single-GPU tail of the data-rank step in two launches (qk_compress_probe) -----------------------
+// Replaces qk_compress_operands + qk_probe_errors (4 launches: compress, V partials, d, accept) where one
+// GPU holds every column: the V partials ride on the B side's compression, the probe rows on the A side's,
+// each side's operand X is read once, row-contiguous (a thread per column, a workgroup per 256 columns:
+// each k is one 2-KiB run per workgroup, and the workgroups of a launch sweep the rows together); the
+// per-workgroup partials are folded in workgroup order by one-workgroup kernels (deterministic).
+//   qk_cp_b_kernel: B'' = T_B X_B; V partial = B''_tile P_tile^T (f64 MFMA from LDS tiles)
+//   qk_cp_vsum_kernel: V [8][16]
+//   qk_cp_a_kernel: A'' = T_A X_A; (R p)_c = X_A[:, c]^T U, d_c = (R p)_c - A''[:, c]^T V; partials of
+//                   e2 = sum d^2 and f2 = sum (R p)_c^2
+//   qk_probe_accept_kernel: e2 / f2 [32], err and the accepted rank
+constexpr int CP_T = 256;     // columns per workgroup tile = threads
+constexpr int CP_KU = 16;     // X rows loaded per unrolled step (loads in flight per thread)
+
+struct CpArgs {
+    int K, rmax;
+    const double* T;     // [rmax][K]
+    const double* X;     // [K][N]
+    int64_t N;
+    double* out;         // [rmax][N]
+    const double* P;     // B side: probes [16][N]
+    const double* U;     // A side: [K][16]
+    double* V;           // [8][16]: written by the B side's last workgroup, read by the A side
+    double* part;        // [gridDim.x][128 or 32]
+};
+
+// out[j][c] = sum_k T[j][k] X[k][c] for the thread's column c (rows j < rmax; returned in a[8])
+__device__ __forceinline__ void cp_column(const CpArgs& g, const double (*sT)[PK], int64_t c, double a[8],
+                                          double* rp, const double (*sU)[PNP]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = 0.0;
+    if (rp)
+#pragma unroll
+        for (int p = 0; p < PNP; ++p) rp[p] = 0.0;
+    const bool live = c < g.N;
+    for (int k0 = 0; k0 < g.K; k0 += CP_KU) {
+        double x[CP_KU];
+#pragma unroll
+        for (int u = 0; u < CP_KU; ++u) x[u] = (live && k0 + u < g.K) ? g.X[(int64_t)(k0 + u) * g.N + c] : 0.0;
+#pragma unroll
+        for (int u = 0; u < CP_KU; ++u) {
+            const int k = k0 + u;
+            if (k < g.K) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[j] = fma(sT[j][k], x[u], a[j]);
+                if (rp)
+#pragma unroll
+                    for (int p = 0; p < PNP; ++p) rp[p] = fma(x[u], sU[k][p], rp[p]);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(CP_T) void qk_cp_b_kernel(CpArgs g) {
+    __shared__ double sT[8][PK];
+    __shared__ double sB2[8][CP_T + 4];
+    __shared__ double sP[PNP][CP_T + 4];
+    __shared__ double red[4][8][PNP];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, l4 = lane >> 4;
+    for (int e = tid; e < 8 * PK; e += CP_T) sT[e / PK][e % PK] = (e / PK < g.rmax && e % PK < g.K) ? g.T[(e / PK) * g.K + e % PK] : 0.0;
+    __syncthreads();
+    d4_t v = {0, 0, 0, 0};  // V^T block of this wave: rows j (l4 + 4 rr), columns p (l16)
+    const int64_t tiles = (g.N + CP_T - 1) / CP_T;
+    for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const int64_t c = t * CP_T + tid;
+        double a[8];
+        cp_column(g, sT, c, a, nullptr, nullptr);
+        const bool live = c < g.N;
+        if (live)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < g.rmax) g.out[(int64_t)j * g.N + c] = a[j];
+        __syncthreads();  // the previous tile's MFMA readers are done with sB2 / sP
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sB2[j][tid] = a[j];
+#pragma unroll
+        for (int p = 0; p < PNP; ++p) sP[p][tid] = live ? g.P[(int64_t)p * g.N + c] : 0.0;
+        __syncthreads();
+        // V^T[j][p] += sum over the wave's 64 columns of B''[j][col] P[p][col] (A operand: rows j, 8..15 zero)
+#pragma unroll
+        for (int s4 = 0; s4 < 16; ++s4) {
+            const int col = 64 * wave + 4 * s4 + l4;
+            const double av = l16 < 8 ? sB2[l16][col] : 0.0;
+            v = __builtin_amdgcn_mfma_f64_16x16x4f64(av, sP[l16][col], v, 0, 0, 0);
+        }
+    }
+    // the waves' blocks summed in wave order -> this workgroup's partial [8][16]
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+        const int j = l4 + 4 * rr;
+        if (j < 8) red[wave][j][l16] = v[rr];
+    }
+    __syncthreads();
+    if (tid < 8 * PNP) {
+        const int j = tid >> 4, p = tid & 15;
+        g.part[(int64_t)blockIdx.x * 128 + tid] = (red[0][j][p] + red[1][j][p]) + (red[2][j][p] + red[3][j][p]);
+    }
+}
+
+// V [8][16] = sum of the n per-workgroup partials of qk_cp_b_kernel, in workgroup order (one workgroup,
+// 128 threads: thread t owns entry t, eight independent chains, combined in a fixed order). A kernel of
+// its own: a last-workgroup fold inside qk_cp_b_kernel needs a device-scope release per workgroup, an
+// L2 write-back on gfx950 (measured: 49 us for the launch instead of the loads' ~10).
+__global__ __launch_bounds__(128) void qk_cp_vsum_kernel(const double* __restrict__ part, int n, double* __restrict__ V) {
+    const int tid = threadIdx.x;
+    double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int b = 0;
+    for (; b + 8 <= n; b += 8)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s8[u] += part[(int64_t)(b + u) * 128 + tid];
+    for (; b < n; ++b) s8[0] += part[(int64_t)b * 128 + tid];
+    V[tid] = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
+}
+
+__global__ __launch_bounds__(CP_T) void qk_cp_a_kernel(CpArgs g) {
+    __shared__ double sT[8][PK];
+    __shared__ double sU[PK][PNP];
+    __shared__ double sV[8][PNP];
+    __shared__ double red[4][2 * PNP];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int e = tid; e < 8 * PK; e += CP_T) sT[e / PK][e % PK] = (e / PK < g.rmax && e % PK < g.K) ? g.T[(e / PK) * g.K + e % PK] : 0.0;
+    for (int e = tid; e < PK * PNP; e += CP_T) sU[e / PNP][e % PNP] = e / PNP < g.K ? g.U[e] : 0.0;
+    if (tid < 8 * PNP) sV[tid >> 4][tid & 15] = g.V[tid];
+    __syncthreads();
+    double e2[PNP], f2[PNP];
+#pragma unroll
+    for (int p = 0; p < PNP; ++p) e2[p] = f2[p] = 0.0;
+    const int64_t tiles = (g.N + CP_T - 1) / CP_T;
+    for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const int64_t c = t * CP_T + tid;
+        double a[8], rp[PNP];
+        cp_column(g, sT, c, a, rp, sU);
+        if (c < g.N) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < g.rmax) g.out[(int64_t)j * g.N + c] = a[j];
+#pragma unroll
+            for (int p = 0; p < PNP; ++p) {
+                double d = rp[p];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) d = fma(-a[j], sV[j][p], d);
+                e2[p] = fma(d, d, e2[p]);
+                f2[p] = fma(rp[p], rp[p], f2[p]);
+            }
+        }
+    }
+    // sums over the workgroup in a fixed order: xor butterflies in each wave, then the 4 waves
+#pragma unroll
+    for (int p = 0; p < PNP; ++p) {
+#pragma unroll
+        for (int sh = 1; sh < 64; sh <<= 1) {
+            e2[p] += __shfl_xor(e2[p], sh, 64);
+            f2[p] += __shfl_xor(f2[p], sh, 64);
+        }
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int p = 0; p < PNP; ++p) {
+            red[wave][p] = e2[p];
+            red[wave][PNP + p] = f2[p];
+        }
+    __syncthreads();
+    if (tid < 2 * PNP)
+        g.part[(int64_t)blockIdx.x * 2 * PNP + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+}
+
+int cp_grid(qk_ctx* ctx, int64_t N) {
+    const int64_t tiles = (N + CP_T - 1) / CP_T;
+    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 4;
+    return (int)(tiles < cap ? (tiles > 0 ? tiles : 1) : cap);
 }
 
 int probe_grid_d(qk_ctx* ctx, int64_t NA) {
@@ -513,14 +701,14 @@ int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const d
 
 int qk_probe_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t* bytes) {
     if (!ctx || !bytes) return QK_EARG;
-    *bytes = (int64_t)(PV_GRID * 256 + probe_grid_d(ctx, NA) * PNP) * (int64_t)sizeof(double);
+    *bytes = (int64_t)(PV_GRID * 256 + probe_grid_d(ctx, NA) * PE) * (int64_t)sizeof(double);
     return QK_OK;
 }
 
 int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx, int64_t NA, const double* A2,
                     int64_t lda2, const double* U, const double* B2, int64_t ldb2, int64_t NB, const double* probes,
-                    int64_t ldp, double* e2, const int32_t* r_dev, double tol, int32_t* k_out, double* err_out,
-                    double* work, int64_t work_bytes) {
+                    int64_t ldp, double* e2, const int32_t* r_dev, double tol, double rel_tol, int32_t* k_out,
+                    double* err_out, double* work, int64_t work_bytes) {
     if (!ctx) return QK_EARG;
     if (K < 1 || K > PK || rmax < 1 || rmax > 8 || NA < 16 || NA % 16 || NB < 4 || NB % 4)
         return fail(ctx, QK_EARG, "qk_probe_errors: need 1 <= K <= 64, 1 <= rmax <= 8, NA % 16 == 0, NB % 4 == 0");
@@ -528,7 +716,7 @@ int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx,
         return fail(ctx, QK_EARG, "qk_probe_errors: null buffer");
     if (ldx < NA || ldb2 < NB || ldp < NB) return fail(ctx, QK_EARG, "qk_probe_errors: leading dimension");
     const int gd = probe_grid_d(ctx, NA);
-    if (work_bytes < (int64_t)(PV_GRID * 256 + gd * PNP) * (int64_t)sizeof(double))
+    if (work_bytes < (int64_t)(PV_GRID * 256 + gd * PE) * (int64_t)sizeof(double))
         return fail(ctx, QK_EARG, "qk_probe_errors: workspace too small (qk_probe_workspace_bytes)");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_probe_errors: hipSetDevice");
     double* vpart = work;
@@ -537,20 +725,55 @@ int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx,
                        vpart);
     hipLaunchKernelGGL(qk_probe_d_kernel, dim3(gd), dim3(256), 0, ctx->stream, K, rmax, XA, ldx, NA, A2, lda2, U, vpart,
                        PV_GRID, epart);
-    hipLaunchKernelGGL(qk_probe_accept_kernel, dim3(1), dim3(256), 0, ctx->stream, epart, gd, r_dev, tol, e2, k_out,
-                       err_out);
+    hipLaunchKernelGGL(qk_probe_accept_kernel, dim3(1), dim3(256), 0, ctx->stream, epart, gd, r_dev, tol, rel_tol, e2,
+                       k_out, err_out);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_probe_errors: ") + hipGetErrorString(e)).c_str());
     return QK_OK;
 }
 
-int qk_probe_accept(qk_ctx* ctx, const double* e2, int n, const int32_t* r_dev, double tol, int32_t* k_out,
-                    double* err_out) {
+int qk_compress_probe_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes) {
+    if (!ctx || !bytes) return QK_EARG;
+    // V [8][16] + the two launches' partials
+    *bytes = (int64_t)(128 + (int64_t)cp_grid(ctx, NB) * 128 + (int64_t)cp_grid(ctx, NA) * 2 * PNP) * 8;
+    return QK_OK;
+}
+
+int qk_compress_probe(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, double* A2,
+                      const double* TB, const double* XB, int64_t NB, double* B2, const double* U, const double* probes,
+                      const int32_t* r_dev, double tol, double rel_tol, double* e2, int32_t* k_out, double* err_out,
+                      void* work, int64_t work_bytes) {
+    if (!ctx) return QK_EARG;
+    if (K < 1 || K > PK || rmax < 1 || rmax > 8 || NA < 1 || NB < 1)
+        return fail(ctx, QK_EARG, "qk_compress_probe: need 1 <= K <= 64, 1 <= rmax <= 8, N >= 1");
+    if (!TA || !XA || !A2 || !TB || !XB || !B2 || !U || !probes || !r_dev || !work)
+        return fail(ctx, QK_EARG, "qk_compress_probe: null buffer");
+    int64_t need = 0;
+    qk_compress_probe_workspace_bytes(ctx, NA, NB, &need);
+    if (work_bytes < need) return fail(ctx, QK_EARG, "qk_compress_probe: workspace too small (qk_compress_probe_workspace_bytes)");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_compress_probe: hipSetDevice");
+    double* V = static_cast<double*>(work);
+    double* part = V + 128;
+    const int gb = cp_grid(ctx, NB), ga = cp_grid(ctx, NA);
+    CpArgs b{K, rmax, TB, XB, NB, B2, probes, nullptr, V, part};
+    hipLaunchKernelGGL(qk_cp_b_kernel, dim3(gb), dim3(CP_T), 0, ctx->stream, b);
+    hipLaunchKernelGGL(qk_cp_vsum_kernel, dim3(1), dim3(128), 0, ctx->stream, part, gb, V);
+    CpArgs a{K, rmax, TA, XA, NA, A2, nullptr, U, V, part};
+    hipLaunchKernelGGL(qk_cp_a_kernel, dim3(ga), dim3(CP_T), 0, ctx->stream, a);
+    hipLaunchKernelGGL(qk_probe_accept_kernel, dim3(1), dim3(256), 0, ctx->stream, part, ga, r_dev, tol, rel_tol, e2,
+                       k_out, err_out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_compress_probe: ") + hipGetErrorString(e)).c_str());
+    return QK_OK;
+}
+
+int qk_probe_accept(qk_ctx* ctx, const double* e2, int n, const int32_t* r_dev, double tol, double rel_tol,
+                    int32_t* k_out, double* err_out) {
     if (!ctx) return QK_EARG;
     if (!e2 || !r_dev || !k_out || n < 1) return fail(ctx, QK_EARG, "qk_probe_accept: null buffer or n < 1");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_probe_accept: hipSetDevice");
-    hipLaunchKernelGGL(qk_probe_accept_kernel, dim3(1), dim3(256), 0, ctx->stream, e2, n, r_dev, tol, nullptr, k_out,
-                       err_out);
+    hipLaunchKernelGGL(qk_probe_accept_kernel, dim3(1), dim3(256), 0, ctx->stream, e2, n, r_dev, tol, rel_tol, nullptr,
+                       k_out, err_out);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_probe_accept: ") + hipGetErrorString(e)).c_str());
     return QK_OK;

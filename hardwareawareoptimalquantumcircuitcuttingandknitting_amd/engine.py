@@ -425,6 +425,7 @@ def sample_fragment(ctx: Context, fs: "FragmentState", shots: int, seed: int, ac
     width = 1 << fs.prog.m
     slot_t, sign_t, off_t = jobs_to_device(jobs, ctx.device)
     pjob, _ = sweep_jobs(ctx, fs.dprog, slot_t, sign_t, jobs.n_jobs)
+    pjob = fold_traced(ctx, pjob, fs.fold)  # one sign per job: |sum_t sign P| = sum_t P
     cdf = T.empty_like(pjob)
     n_seg = len(jobs.label_offsets) - 1
     ctx.check(ctx.lib.qk_sample_cdf(ctx.handle, n_seg, off_t.data_ptr(), width, pjob.data_ptr(),
@@ -573,6 +574,9 @@ class FragmentState:
     # u is `expand[u] @ q_basis` (fragment_program.basis_reduce)
     basis_labels: list | None = None
     expand: np.ndarray | None = None
+    # traced qubits beyond what a FINAL tile holds: the device program measures `log2(fold)` of them
+    # too (widened outputs) and fold_traced sums them out after the sweep (_device_program)
+    fold: int = 1
 
     @property
     def swept_labels(self) -> list:
@@ -589,6 +593,38 @@ class FragmentState:
         if self.expand is not None:
             raise ValueError("basis-reduced fragment: labels are combinations of swept rows")
         return self.uidx if self.uidx is not None else np.arange(len(self.labels), dtype=np.int64)
+
+
+TRACED_MAX = 12 - 5  # traced qubits a SPLIT program's FINAL tile holds (sweep_plan: 12-bit tiles, 5 low bits)
+
+
+def _device_program(prog: FragmentProgram):
+    """``(program the device runs, fold)``. The FINAL pass traces out unmeasured qubits inside its
+    tile, so a SPLIT program (n > 12) may trace at most TRACED_MAX of them (sweep_plan.schedule_passes).
+    With more, the device program measures the lowest extra ones as well (``m`` widened: they are the
+    next state bits above the measured ones) and the output row holds ``fold`` blocks of 2^m values,
+    one per extra-bit pattern; :func:`fold_traced` sums them after the sweep (a row reduction)."""
+    if prog.n <= 12 or prog.n - prog.m <= TRACED_MAX:
+        return prog, 1
+    m_w = prog.n - TRACED_MAX
+    return dataclasses.replace(prog, m=m_w), 1 << (m_w - prog.m)
+
+
+_FOLD_OFFS: dict = {}
+
+
+def fold_traced(ctx: Context, x, fold: int):
+    """Rows of a widened sweep output ``[rows, fold * 2^m]`` summed over their ``fold`` blocks ->
+    ``[rows, 2^m]`` (qk_reduce_labels over each row's blocks); the identity for ``fold == 1``."""
+    if fold <= 1:
+        return x
+    T = torch()
+    rows, w = x.shape
+    key = (rows, fold, str(x.device))
+    off = _FOLD_OFFS.get(key)
+    if off is None:
+        off = _FOLD_OFFS[key] = T.arange(rows + 1, dtype=T.int64, device=x.device) * fold
+    return reduce_labels(ctx, x.contiguous().view(rows * fold, w // fold), off, rows)
 
 
 def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = True,
@@ -622,14 +658,15 @@ def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = 
         want.append(_worth_compiling(prog, jobs) if jit is None else (jit and len(prog.ops) <= 400))
         out.append(FragmentState(frag, labels, prog, None, jobs, touches, dropped, uidx, unique,
                                  red.labels if red is not None else None,
-                                 red.expand if red is not None else None))
+                                 red.expand if red is not None else None, _device_program(prog)[1]))
     split = [(fs.prog.n, fs.jobs.n_jobs) for fs, w in zip(out, want) if w and not fs.dropped and fs.prog.n > 12]
     tb = jit_tile_bits(split) if split else JIT_TILE_BITS_MAX
-    jit_progs = [fs.prog for fs, w in zip(out, want) if w and not fs.dropped and fs.prog.n > 12]
+    jit_progs = [_device_program(fs.prog)[0] for fs, w in zip(out, want) if w and not fs.dropped and fs.prog.n > 12]
     ftb = jit_final_tile_bits(jit_progs, tb) if (upload and jit_progs) else None
     for fs, w in zip(out, want):
         if upload and not fs.dropped:
-            fs.dprog = DeviceProgram.upload(fs.prog, device, jit=w, tile_bits=tb, final_tile_bits=ftb)
+            fs.dprog = DeviceProgram.upload(_device_program(fs.prog)[0], device, jit=w, tile_bits=tb,
+                                            final_tile_bits=ftb)
     return out
 
 
@@ -666,11 +703,11 @@ def sweep_fragment(ctx: Context, fs: FragmentState, label_range=None):
                    jobs.branch_bits[j0:j1])
     slot_t, sign_t, off_t = jobs_to_device(sub, ctx.device)
     if sub.n_jobs != hi - lo and fs.dprog.module is not None:  # branching, compiled: fused FINAL
-        return sweep_labels(ctx, fs.dprog, slot_t, sign_t, sub.n_jobs, off_t, hi - lo)[0]
+        return fold_traced(ctx, sweep_labels(ctx, fs.dprog, slot_t, sign_t, sub.n_jobs, off_t, hi - lo)[0], fs.fold)
     pjob, _ = sweep_jobs(ctx, fs.dprog, slot_t, sign_t, sub.n_jobs)
     if sub.n_jobs == hi - lo:  # no branching: jobs are labels
-        return pjob
-    return reduce_labels(ctx, pjob, off_t, hi - lo)
+        return fold_traced(ctx, pjob, fs.fold)
+    return fold_traced(ctx, reduce_labels(ctx, pjob, off_t, hi - lo), fs.fold)
 
 
 @dataclass
@@ -844,13 +881,45 @@ def compress_operands(ctx: Context, TA, XA, TB, XB):
 
 
 _PROBE_WORK: dict = {}
+_CP_WORK: dict = {}
 
 
-def probe_errors(ctx: Context, XA, A2, U, B2, probes, r=None, tol: float = 0.0, a2_cols: tuple | None = None):
-    """``qk_probe_errors``: squared probe errors ``e2`` ([16]) of the compressed knit over the columns of
-    ``XA`` ([K, NA]); ``A2`` ([rmax, *]) holds those columns at ``a2_cols = (offset, count)`` of its rows
-    (default: all). ``U = XB probes^T`` and ``B2`` / ``probes`` span all of B's columns. With ``r`` (device
-    int32 [1]) also the accepted rank ``k`` and the error: returns ``(e2, k, err)``, else ``(e2, None, None)``."""
+def compress_probe(ctx: Context, TA, XA, TB, XB, U, probes, r, tol: float, rel_tol: float = 0.0):
+    """``qk_compress_probe`` (single GPU, every column of both operands here): the compressed operands
+    ``A2 = TA XA``, ``B2 = TB XB`` and the probe check of ``qk_probe_errors`` + ``qk_probe_accept`` in two
+    launches. Returns ``(A2, B2, e2 [32], k, err)``, all on the device."""
+    T = torch()
+    rmax, K = TA.shape
+    NA, NB = XA.shape[1], XB.shape[1]
+    assert TB.shape == (rmax, K) and XA.shape[0] == K and XB.shape[0] == K and U.shape == (K, N_PROBES)
+    assert probes.shape == (N_PROBES, NB) and all(t.is_contiguous() for t in (TA, XA, TB, XB, U, probes))
+    dev = XA.device
+    ab = T.empty(rmax * (NA + NB), dtype=T.float64, device=dev)
+    A2, B2 = ab[:rmax * NA].view(rmax, NA), ab[rmax * NA:].view(rmax, NB)
+    need = ctypes.c_int64()
+    ctx.check(ctx.lib.qk_compress_probe_workspace_bytes(ctx.handle, NA, NB, ctypes.byref(need)),
+              "qk_compress_probe_workspace_bytes")
+    key = (str(dev), T.cuda.current_stream(dev).cuda_stream)
+    work = _CP_WORK.get(key)
+    if work is None or work.numel() < need.value:
+        work = _CP_WORK[key] = T.empty(max(need.value, 8), dtype=T.uint8, device=dev)
+    e2 = T.empty(2 * N_PROBES, dtype=T.float64, device=dev)
+    k = T.empty(1, dtype=T.int32, device=dev)
+    err = T.empty(1, dtype=T.float64, device=dev)
+    ctx.check(ctx.lib.qk_compress_probe(ctx.handle, K, rmax, TA.data_ptr(), XA.data_ptr(), NA, A2.data_ptr(),
+                                        TB.data_ptr(), XB.data_ptr(), NB, B2.data_ptr(), U.data_ptr(),
+                                        probes.data_ptr(), r.data_ptr(), tol, rel_tol, e2.data_ptr(), k.data_ptr(),
+                                        err.data_ptr(), work.data_ptr(), work.numel()), "qk_compress_probe")
+    return A2, B2, e2, k, err
+
+
+def probe_errors(ctx: Context, XA, A2, U, B2, probes, r=None, tol: float = 0.0, a2_cols: tuple | None = None,
+                 rel_tol: float = 0.0):
+    """``qk_probe_errors``: ``e2`` ([32]) = the squared probe errors of the compressed knit ([:16]) and the
+    squared reference products ``||R p||^2`` ([16:]) over the columns of ``XA`` ([K, NA]); ``A2`` ([rmax, *])
+    holds those columns at ``a2_cols = (offset, count)`` of its rows (default: all). ``U = XB probes^T`` and
+    ``B2`` / ``probes`` span all of B's columns. With ``r`` (device int32 [1]) also the accepted rank ``k``
+    (error <= max(tol, rel_tol max ||R p||)) and the error: ``(e2, k, err)``, else ``(e2, None, None)``."""
     T = torch()
     K, NA = XA.shape
     rmax = A2.shape[0]
@@ -866,23 +935,23 @@ def probe_errors(ctx: Context, XA, A2, U, B2, probes, r=None, tol: float = 0.0, 
     work = _PROBE_WORK.get(key)
     if work is None or work.numel() * 8 < need.value:
         work = _PROBE_WORK[key] = T.empty(max(need.value // 8, 1), dtype=T.float64, device=dev)
-    e2 = T.empty(N_PROBES, dtype=T.float64, device=dev)
+    e2 = T.empty(2 * N_PROBES, dtype=T.float64, device=dev)
     k = T.empty(1, dtype=T.int32, device=dev) if r is not None else None
     err = T.empty(1, dtype=T.float64, device=dev) if r is not None else None
     ctx.check(ctx.lib.qk_probe_errors(ctx.handle, K, rmax, XA.data_ptr(), NA, NA, A2.data_ptr() + 8 * off,
                                       A2.shape[1], U.data_ptr(), B2.data_ptr(), NB, NB, probes.data_ptr(), NB,
-                                      e2.data_ptr(), _ptr(r), tol, _ptr(k), _ptr(err), work.data_ptr(),
+                                      e2.data_ptr(), _ptr(r), tol, rel_tol, _ptr(k), _ptr(err), work.data_ptr(),
                                       work.numel() * 8), "qk_probe_errors")
     return e2, k, err
 
 
-def probe_accept(ctx: Context, e2, r, tol: float):
-    """``qk_probe_accept``: ``(k, err)`` from summed squared probe errors ``e2`` ([16])."""
+def probe_accept(ctx: Context, e2, r, tol: float, rel_tol: float = 0.0):
+    """``qk_probe_accept``: ``(k, err)`` from summed ``e2`` rows ([32]: squared errors, squared references)."""
     T = torch()
     k = T.empty(1, dtype=T.int32, device=e2.device)
     err = T.empty(1, dtype=T.float64, device=e2.device)
-    ctx.check(ctx.lib.qk_probe_accept(ctx.handle, e2.data_ptr(), 1, r.data_ptr(), tol, k.data_ptr(), err.data_ptr()),
-              "qk_probe_accept")
+    ctx.check(ctx.lib.qk_probe_accept(ctx.handle, e2.data_ptr(), 1, r.data_ptr(), tol, rel_tol, k.data_ptr(),
+                                      err.data_ptr()), "qk_probe_accept")
     return k, err
 
 
@@ -985,7 +1054,8 @@ def knit_plan_c(ctx: Context, virt, frags: list, qs: list, factored: bool = Fals
     return out
 
 
-def knit_lowrank_c(ctx: Context, pipe, qs: list, out=None, rank_tol: float | None = None):
+def knit_lowrank_c(ctx: Context, pipe, qs: list, out=None, rank_tol: float | None = None,
+                   rank_tol_rel: float | None = None):
     """The single-GPU data-rank knit through the one-call C entry ``qk_knit_lowrank`` (what a host
     that is not Python calls) with a pipeline's plan: its device transforms, clbit
     masks, probes and tolerances. Returns ``(out [2^N], accepted rank: device int32 [1])``."""
@@ -1000,7 +1070,8 @@ def knit_lowrank_c(ctx: Context, pipe, qs: list, out=None, rank_tol: float | Non
     plan = _lib.QkLowrankPlan(pipe.N, WA.shape[1], WA.shape[0], WB.shape[0],
                               sum(1 << c for c in pipe.ops.clbits[ia]), sum(1 << c for c in pipe.ops.clbits[ib]),
                               WA.data_ptr(), WB.data_ptr(), probes.data_ptr(), dr.LAM_TOL, dr.S_TOL, dr.S_ABS,
-                              pipe.rank_tol if rank_tol is None else rank_tol)
+                              pipe.rank_tol if rank_tol is None else rank_tol,
+                              pipe.rank_tol_rel if rank_tol_rel is None else rank_tol_rel)
     need = ctypes.c_int64()
     ctx.check(ctx.lib.qk_knit_lowrank_workspace_bytes(ctx.handle, ctypes.byref(plan), ctypes.byref(need)),
               "qk_knit_lowrank_workspace_bytes")

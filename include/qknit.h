@@ -247,7 +247,7 @@ int qk_knit(qk_ctx* ctx, const qk_knit_plan* plan, const double* const* q, void*
 
 /* ---- plan-level low-rank knit: the benched single-GPU step's knit in one call (qknit_plan.hip) ----
  * KnitPipeline's device data rank for a two-fragment knit, chained on the context's
- * stream with no host synchronisation: qk_prep_operands -> qk_rank_factors -> qk_compress_operands ->
+ * stream with no host synchronisation: qk_prep_operands -> qk_rank_factors -> qk_compress_probe ->
  * qk_probe_errors -> qk_knit_outer_stream_range (write-bound, K = accepted rank) -> qk_gemm_keyed_pred
  * (the exact terms-wide contraction, runs only when the check rejected). Same result as qk_knit on the
  * same transforms within the probe tolerance. q_a / q_b: the swept rows ([rows][2^popcount(mask)]).
@@ -263,7 +263,8 @@ typedef struct qk_lowrank_plan {
     const double* wt_b;      /* DEVICE [rows_b][terms] */
     const double* probes;    /* DEVICE [16][2^popcount(mask_b)]: fixed Gaussian probe vectors */
     double lam_tol, s_tol, s_abs;  /* qk_rank_factors tolerances (data_rank.py LAM_TOL / S_TOL / S_ABS) */
-    double rank_tol;         /* probe acceptance bound (KnitPipeline.rank_tol) */
+    double rank_tol;         /* probe acceptance bound, absolute floor (KnitPipeline.rank_tol) ... */
+    double rank_tol_rel;     /* ... and relative to max_p ||R p|| (KnitPipeline.rank_tol_rel) */
 } qk_lowrank_plan;
 
 int qk_knit_lowrank_workspace_bytes(qk_ctx* ctx, const qk_lowrank_plan* plan, int64_t* bytes);
@@ -315,19 +316,32 @@ int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const d
                          const double* TB, const double* XB, int64_t NB, double* B2);
 
 /* Acceptance check of a compressed knit on the real operands (the probe products of the torch form,
- * not materialised): e2[p] = ||(X_A^T X_B - A2^T B2) P_p||^2 summed over the NA columns of X_A given
- * (X_A: [K][ldx], A2: [rmax][lda2] the same columns; U = X_B P^T [K][16] over ALL columns of X_B; B2:
- * [rmax][ldb2] and P: [16][ldp] over all NB columns). With k_out: *err_out = sqrt(max_p e2[p]) and
- * *k_out = (*r_dev > 0 && err <= tol) ? *r_dev : 0 (the accepted rank; 0 = exact contraction).
- * qk_probe_accept does that last step on e2 rows summed elsewhere (multi-GPU: all-reduced partial
- * e2 of each rank's columns; n rows of 16). e2 / r_dev / k_out / err_out: DEVICE. */
+ * not materialised): e2[p] = ||(X_A^T X_B - A2^T B2) P_p||^2 and e2[16 + p] = ||X_A^T X_B P_p||^2
+ * (the reference product, ~||R||_F^2), summed over the NA columns of X_A given (X_A: [K][ldx], A2:
+ * [rmax][lda2] the same columns; U = X_B P^T [K][16] over ALL columns of X_B; B2: [rmax][ldb2] and P:
+ * [16][ldp] over all NB columns); e2 holds 32 doubles. With k_out: *err_out = sqrt(max_p e2[p]) and
+ * *k_out = (*r_dev > 0 && err <= max(tol, rel_tol sqrt(max_p e2[16 + p]))) ? *r_dev : 0 (the accepted
+ * rank; 0 = exact contraction). qk_probe_accept does that last step on e2 rows summed elsewhere
+ * (multi-GPU: all-reduced partial e2 of each rank's columns; n rows of 32). e2 / r_dev / k_out /
+ * err_out: DEVICE. */
 int qk_probe_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t* bytes);
 int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx, int64_t NA, const double* A2,
                     int64_t lda2, const double* U, const double* B2, int64_t ldb2, int64_t NB, const double* probes,
-                    int64_t ldp, double* e2, const int32_t* r_dev, double tol, int32_t* k_out, double* err_out,
-                    double* work, int64_t work_bytes);
-int qk_probe_accept(qk_ctx* ctx, const double* e2, int n, const int32_t* r_dev, double tol, int32_t* k_out,
-                    double* err_out);
+                    int64_t ldp, double* e2, const int32_t* r_dev, double tol, double rel_tol, int32_t* k_out,
+                    double* err_out, double* work, int64_t work_bytes);
+int qk_probe_accept(qk_ctx* ctx, const double* e2, int n, const int32_t* r_dev, double tol, double rel_tol,
+                    int32_t* k_out, double* err_out);
+
+/* Single GPU (every column of both operands on this device): qk_compress_operands + qk_probe_errors (with
+ * k_out) — the B side's compression carries the V = B'' P^T partial sums, the A side's the probe rows, so
+ * each operand is read once (row-contiguous, a thread per column); one-workgroup kernels fold the partials
+ * in a fixed order. Same outputs: A2 [rmax][NA], B2 [rmax][NB], e2 [32], *k_out, *err_out (DEVICE).
+ * work: qk_compress_probe_workspace_bytes. */
+int qk_compress_probe_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes);
+int qk_compress_probe(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, double* A2,
+                      const double* TB, const double* XB, int64_t NB, double* B2, const double* U, const double* probes,
+                      const int32_t* r_dev, double tol, double rel_tol, double* e2, int32_t* k_out, double* err_out,
+                      void* work, int64_t work_bytes);
 
 /* ---- post-processing (reference-shaped results; quasi_distr.py:3-43, run.py:71) ---------- */
 

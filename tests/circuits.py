@@ -179,3 +179,30 @@ def same_fragment_cut(seed: int = 13):
     _rand_layer(qc, range(5), rng)
     qc.measure_all()
     return qc, cut_circuit(qc, CutSpec([left, right], cut_idx))
+
+
+def many_traced(seed: int = 17, n0: int = 14, measured: tuple = (0, 5, 9)):
+    """A 14-qubit fragment that measures only 3 of its qubits (11 traced out: more than a SPLIT
+    program's FINAL tile holds, engine._device_program widens and folds) joined by one CX cut to a
+    3-qubit fragment measured in full."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.circuit import ClassicalRegister
+    rng = random.Random(seed)
+    n = n0 + 3
+    qr = QuantumRegister(n, "q")
+    cr = ClassicalRegister(len(measured) + 3, "c")
+    qc = QuantumCircuit(qr, cr)
+    _rand_layer(qc, range(n), rng)
+    for i in range(n0 - 1):
+        qc.cx(i, i + 1)
+    _rand_layer(qc, range(n0), rng)
+    qc.cx(n0 - 1, n0)
+    cut = [len(qc.data) - 1]
+    qc.cx(n0, n0 + 1)
+    qc.cx(n0 + 2, n0 + 1)
+    _rand_layer(qc, range(n), rng)
+    for i in range(0, n0 - 1, 2):
+        qc.cx(i + 1, i)
+    _rand_layer(qc, range(n0), rng)
+    for c, q in enumerate(list(measured) + [n0, n0 + 1, n0 + 2]):
+        qc.measure(q, c)
+    return qc, cut_circuit(qc, CutSpec([list(range(n0)), list(range(n0, n))], cut))

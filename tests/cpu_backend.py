@@ -116,20 +116,24 @@ class CpuBackend:
         XA, XB = WtA.T @ qA, WtB.T @ qB
         return XA, XB, torch.stack([XA @ XA.T, XB @ XB.T]), XB @ probes.T
 
-    def probe_errors(self, XA, A2, U, B2, probes, r=None, tol=0.0, a2_cols=None):
-        """qk_probe_errors' contract: squared probe errors over XA's columns (+ accepted rank)."""
+    def probe_errors(self, XA, A2, U, B2, probes, r=None, tol=0.0, a2_cols=None, rel_tol=0.0):
+        """qk_probe_errors' contract: squared probe errors and squared reference products ([32]) over
+        XA's columns (+ accepted rank)."""
         A2c = A2 if a2_cols is None else A2[:, a2_cols[0]:a2_cols[0] + a2_cols[1]]
-        d = XA.T @ U - A2c.T @ (B2 @ probes.T)
-        e2 = (d * d).sum(dim=0)
+        ref = XA.T @ U
+        d = ref - A2c.T @ (B2 @ probes.T)
+        e2 = torch.cat([(d * d).sum(dim=0), (ref * ref).sum(dim=0)])
         if r is None:
             return e2, None, None
-        k, err = self.probe_accept(e2, r, tol)
+        k, err = self.probe_accept(e2, r, tol, rel_tol)
         return e2, k, err
 
-    def probe_accept(self, e2, r, tol):
-        err = float(e2.max().sqrt())
+    def probe_accept(self, e2, r, tol, rel_tol=0.0):
+        n = e2.numel() // 2
+        err = float(e2[:n].max().sqrt())
+        bound = max(tol, rel_tol * float(e2[n:].max().sqrt()))
         rv = int(r.reshape(-1)[0])
-        return torch.tensor([rv if rv > 0 and err <= tol else 0], dtype=torch.int32), torch.tensor([err])
+        return torch.tensor([rv if rv > 0 and err <= bound else 0], dtype=torch.int32), torch.tensor([err])
 
     def compress(self, TA, XA, TB, XB):
         return (TA @ XA).contiguous(), (TB @ XB).contiguous()

@@ -444,3 +444,32 @@ def test_circuit_fingerprint_keys_the_plan_cache():
     fc.h(fc.qubits[0])
     a.replace_fragment_circuit(frag, fc)
     assert circuit_fingerprint(a) != before
+
+
+def test_traced_qubits_beyond_final_tile_widen_and_fold():
+    """A SPLIT fragment tracing out more qubits than its FINAL tile holds (sweep_plan refuses it):
+    the device program measures the lowest extra ones too (engine._device_program) and the widened
+    rows, summed over their fold blocks, equal the oracle's instance distributions (encoded program
+    run by the numpy emulator)."""
+    qc, cut = circuits.many_traced()
+    view = qvm.CutView(cut)
+    v = VirtualCircuit(cut)
+    seen = False
+    for frag, fcirc in v.fragment_circuits.items():
+        prog = compile_fragment(fcirc, frag, engine.clbit_indexer(v.circuit))
+        dprog, fold = engine._device_program(prog)
+        if prog.n > 12:
+            assert prog.n - prog.m > engine.TRACED_MAX and fold == 1 << (dprog.m - prog.m) and fold > 1
+            with pytest.raises(NotImplementedError):
+                sweep_plan.encode(prog)
+            seen = True
+        labels = v.get_instance_labels(frag)
+        jobs = build_jobs(prog, labels)
+        enc = sweep_plan.encode(dprog)
+        p = emulate(enc, jobs.slot_mats, jobs.sign)
+        p = p.reshape(p.shape[0], fold, -1).sum(axis=1)
+        offs = jobs.label_offsets
+        q = np.stack([p[offs[i]:offs[i + 1]].sum(0) for i in range(len(offs) - 1)])
+        ref, _ = dense.fragment_q(view, list(frag))
+        np.testing.assert_allclose(q, ref, atol=1e-12, rtol=0)
+    assert seen

@@ -14,7 +14,13 @@ lifted (the stand-in all_reduce leaves partial Grams, whose factors need not pas
 the accepted rank is reported. The factorisation runs on the true Grams (from a one-GPU step):
 the partial ones would factor to a different rank.
 
-    python tools/rank_sim.py --world 2 4 8 --steps 5
+    python tools/rank_sim.py --world 2 4 8 --steps 5 [--xgmi-gbs 50 --coll-lat-us 20] [--overlap]
+
+``--xgmi-gbs B``: every stand-in collective also holds its stream for ``lat + received / (links x B)``
+(torch.cuda._sleep, calibrated; ``links`` = world - 1 <= 7: fully connected xGMI, each peer's share
+on its own link), a model of the transfer time on the rank's timeline. ``--overlap``: pipelined
+steps (KnitPipeline._step_overlapped: step i+1's sweep, preparation and collectives on a CU-masked
+stream under step i's write), the default of the multi-GPU bench.
 """
 import argparse
 import json
@@ -37,6 +43,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="syc_32_5_p2")
+    ap.add_argument("--xgmi-gbs", type=float, default=0.0, help="modelled per-link xGMI GB/s (0: no delay)")
+    ap.add_argument("--coll-lat-us", type=float, default=20.0, help="modelled latency per collective")
+    ap.add_argument("--overlap", action="store_true", help="pipelined steps (CU-masked prep stream)")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -47,9 +56,23 @@ def main():
     name, n, d, p, variant = cutting.BASELINE_CONFIGS[args.workload]
     _, cut, _ = cutting.config_cut_circuit(name, n, d, p, variant)
     recv = {}
+    cyc_per_us = [0.0]
+    if args.xgmi_gbs > 0:  # calibrate torch.cuda._sleep (cycles of the shader clock) against events
+        s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(1000000)
+        s_.record()
+        torch.cuda._sleep(2000000)
+        e_.record()
+        torch.cuda.synchronize()
+        cyc_per_us[0] = 2000000 / (s_.elapsed_time(e_) * 1e3)
 
     def note(kind, nbytes):
         recv[kind] = recv.get(kind, 0) + nbytes
+        if args.xgmi_gbs > 0:  # the modelled transfer holds the issuing stream
+            links = max(1, min(world_now[0] - 1, 7))
+            us = args.coll_lat_us + nbytes / (links * args.xgmi_gbs * 1e9) * 1e6
+            torch.cuda._sleep(int(us * cyc_per_us[0]))
+            model[kind] = model.get(kind, 0.0) + us
 
     def all_to_all_single(out, inp, group=None, async_op=False):
         out.view(-1).copy_(inp.reshape(-1))
@@ -78,6 +101,7 @@ def main():
     dist.all_gather_into_tensor = all_gather_into_tensor
     dist.get_global_rank = lambda group, r: r
     world_now = [1]
+    model = {}
 
     # the stand-in all_reduce leaves each rank's partial Grams; factorise the TRUE Grams instead (taken
     # from a one-GPU step) so the simulated rank compresses to the real rank, with the same kernel
@@ -96,10 +120,14 @@ def main():
         real = pipe.be.rank_factors
         pipe.be.rank_factors = lambda GA, GB, real=real: real(*G_true)
         pipe.rank_tol = float("inf")
+        if args.overlap:
+            torch.cuda.set_stream(torch.cuda.Stream())
+            pipe.overlap = pipe.overlap_ok()
         for _ in range(args.warmup):
             pipe.step()
         torch.cuda.synchronize()
         recv.clear()
+        model.clear()
         pipe.record_events = True
         t0 = time.perf_counter()
         for _ in range(args.steps):
@@ -108,14 +136,18 @@ def main():
         ms = (time.perf_counter() - t0) / args.steps * 1e3
         pipe.sync_stats()
         knit = sum(s.elapsed_time(e) for s, e in pipe.events) / len(pipe.events)
-        sweep = sum(s.elapsed_time(e) for s, e in pipe.sweep_events) / len(pipe.sweep_events)
+        sweep = sum(s.elapsed_time(e) for s, e in pipe.sweep_events) / max(len(pipe.sweep_events), 1)
         prep = sum(s.elapsed_time(e) for s, e in pipe.prep_events) / max(len(pipe.prep_events), 1)
         M, N, K = pipe.gemm_shape()
         print(json.dumps({"workload": args.workload, "mode": pipe.mode, "world": world, "rank": args.rank,
                           "slice": list(pipe.slice), "ms_per_step_no_xgmi": round(ms, 3),
                           "sweep_ms": round(sweep, 3), "prep_ms": round(prep, 3), "knit_ms": round(knit, 3),
                           "knit_GBs": round(8 * M * N / (knit * 1e-3) / 1e9, 1), "accepted_rank": pipe.last_rank,
-                          "received_bytes_per_step": {k: v // args.steps for k, v in recv.items()}}), flush=True)
+                          "received_bytes_per_step": {k: v // args.steps for k, v in recv.items()},
+                          "xgmi_model": ({"per_link_GBs": args.xgmi_gbs, "latency_us": args.coll_lat_us,
+                                          "us_per_step": {k: round(v / args.steps, 1) for k, v in model.items()}}
+                                         if args.xgmi_gbs > 0 else None),
+                          "overlap": bool(pipe.overlap), "cus": pipe.overlap_cus}), flush=True)
         del pipe
         torch.cuda.empty_cache()
 
