@@ -450,19 +450,21 @@ __global__ __launch_bounds__(256) void qk_probe_accept_kernel(const double* __re
     }
 }
 
-// ---- single-GPU tail of the data-rank step in two launches (qk_compress_probe) -----------------------
-// Replaces qk_compress_operands + qk_probe_errors (4 launches: compress, V partials, d, accept) where one
-// GPU holds every column: the V partials ride on the B side's compression, the probe rows on the A side's,
-// each side's operand X is read once, row-contiguous (a thread per column, a workgroup per 256 columns:
-// each k is one 2-KiB run per workgroup, and the workgroups of a launch sweep the rows together); the
-// per-workgroup partials are folded in workgroup order by one-workgroup kernels (deterministic).
-//   qk_cp_b_kernel: B'' = T_B X_B; V partial = B''_tile P_tile^T (f64 MFMA from LDS tiles)
+// ---- single-GPU tail of the data-rank step (qk_compress_probe) --------------------------------------------
+// Replaces qk_compress_operands + qk_probe_errors where one GPU holds every column: the V partial sums
+// ride on the B side's compression and the probe rows on the A side's, so each operand X is read once
+// (128 MB of reads -> 80 MB for syc 32 5). A workgroup takes 64-column tiles, a lane one column, the four
+// waves a quarter of K each (16 loads in flight per lane, one 512-B row segment per wave load); the
+// quarters meet in LDS. Per-workgroup partials are folded in workgroup order by one-workgroup kernels
+// (deterministic; a last-workgroup fold inside the launch needs a device-scope release per workgroup,
+// an L2 write-back on gfx950, measured slower).
+//   qk_cp_b_kernel: B'' = T_B X_B; V partial = B''_tile P_tile^T
 //   qk_cp_vsum_kernel: V [8][16]
 //   qk_cp_a_kernel: A'' = T_A X_A; (R p)_c = X_A[:, c]^T U, d_c = (R p)_c - A''[:, c]^T V; partials of
 //                   e2 = sum d^2 and f2 = sum (R p)_c^2
 //   qk_probe_accept_kernel: e2 / f2 [32], err and the accepted rank
-constexpr int CP_T = 256;     // columns per workgroup tile = threads
-constexpr int CP_KU = 16;     // X rows loaded per unrolled step (loads in flight per thread)
+constexpr int CP_C = 64;      // columns per workgroup tile (a lane per column, the 4 waves split K in quarters)
+constexpr int CP_T = 256;     // threads
 
 struct CpArgs {
     int K, rmax;
@@ -472,87 +474,89 @@ struct CpArgs {
     double* out;         // [rmax][N]
     const double* P;     // B side: probes [16][N]
     const double* U;     // A side: [K][16]
-    double* V;           // [8][16]: written by the B side's last workgroup, read by the A side
-    double* part;        // [gridDim.x][128 or 32]
+    double* V;           // [8][16]: summed by qk_cp_vsum_kernel, read by the A side
+    double* part;        // [gridDim.x][128 (B) or 32 (A)]
 };
 
-// out[j][c] = sum_k T[j][k] X[k][c] for the thread's column c (rows j < rmax; returned in a[8])
-__device__ __forceinline__ void cp_column(const CpArgs& g, const double (*sT)[PK], int64_t c, double a[8],
-                                          double* rp, const double (*sU)[PNP]) {
+// Lane l of wave q: the partial sums over k in [16q, 16q + 16) of this tile's column c0 + l — a[j] of
+// T X (j < 8) and, with sU, r[p] of X^T U (p < 16) — into the LDS partial planes. The 16 loads of a lane
+// are in flight together; each is one 512-B row segment per wave.
+template <bool PROBE>
+__device__ __forceinline__ void cp_partials(const CpArgs& g, const double (*sTt)[8], const double (*sU)[PNP],
+                                            int64_t c0, double (*pa)[8][CP_C], double (*pr)[PNP][CP_C]) {
+    const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int64_t c = c0 + lane;
+    const bool live = c < g.N;
+    double xv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int k = 16 * q + u;
+        xv[u] = (live && k < g.K) ? g.X[(int64_t)k * g.N + c] : 0.0;
+    }
+    double a[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] = 0.0;
-    if (rp)
+    double r[PROBE ? PNP : 1];
 #pragma unroll
-        for (int p = 0; p < PNP; ++p) rp[p] = 0.0;
-    const bool live = c < g.N;
-    for (int k0 = 0; k0 < g.K; k0 += CP_KU) {
-        double x[CP_KU];
+    for (int p = 0; p < (PROBE ? PNP : 1); ++p) r[p] = 0.0;
 #pragma unroll
-        for (int u = 0; u < CP_KU; ++u) x[u] = (live && k0 + u < g.K) ? g.X[(int64_t)(k0 + u) * g.N + c] : 0.0;
+    for (int u = 0; u < 16; ++u) {
+        const int k = 16 * q + u;  // rows >= K: T / U are zero there (and xv is 0)
 #pragma unroll
-        for (int u = 0; u < CP_KU; ++u) {
-            const int k = k0 + u;
-            if (k < g.K) {
+        for (int j = 0; j < 8; ++j) a[j] = fma(sTt[k][j], xv[u], a[j]);
+        if (PROBE)
 #pragma unroll
-                for (int j = 0; j < 8; ++j) a[j] = fma(sT[j][k], x[u], a[j]);
-                if (rp)
-#pragma unroll
-                    for (int p = 0; p < PNP; ++p) rp[p] = fma(x[u], sU[k][p], rp[p]);
-            }
-        }
+            for (int p = 0; p < PNP; ++p) r[p] = fma(xv[u], sU[k][p], r[p]);
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pa[q][j][lane] = a[j];
+    if (PROBE)
+#pragma unroll
+        for (int p = 0; p < PNP; ++p) pr[q][p][lane] = r[p];
 }
 
-__global__ __launch_bounds__(CP_T) void qk_cp_b_kernel(CpArgs g) {
-    __shared__ double sT[8][PK];
-    __shared__ double sB2[8][CP_T + 4];
-    __shared__ double sP[PNP][CP_T + 4];
-    __shared__ double red[4][8][PNP];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, l4 = lane >> 4;
-    for (int e = tid; e < 8 * PK; e += CP_T) sT[e / PK][e % PK] = (e / PK < g.rmax && e % PK < g.K) ? g.T[(e / PK) * g.K + e % PK] : 0.0;
+__global__ __launch_bounds__(CP_T, 2) void qk_cp_b_kernel(CpArgs g) {
+    __shared__ double sTt[PK][8];       // T^T (rows >= rmax / K zero)
+    __shared__ double pa[4][8][CP_C];   // per-wave partials of B'' = T X
+    __shared__ double sB2[8][CP_C];
+    __shared__ double sP[PNP][CP_C];
+    __shared__ double vh[2][128];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int e = tid; e < 8 * PK; e += CP_T) {
+        const int k = e >> 3, j = e & 7;
+        sTt[k][j] = (j < g.rmax && k < g.K) ? g.T[j * g.K + k] : 0.0;
+    }
     __syncthreads();
-    d4_t v = {0, 0, 0, 0};  // V^T block of this wave: rows j (l4 + 4 rr), columns p (l16)
-    const int64_t tiles = (g.N + CP_T - 1) / CP_T;
+    const int jp = tid & 127, half = tid >> 7;   // V partial: pair (j, p) = (jp >> 4, jp & 15), column half
+    double v = 0.0;
+    const int64_t tiles = (g.N + CP_C - 1) / CP_C;
     for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
-        const int64_t c = t * CP_T + tid;
-        double a[8];
-        cp_column(g, sT, c, a, nullptr, nullptr);
-        const bool live = c < g.N;
-        if (live)
+        const int64_t c0 = t * CP_C, c = c0 + lane;
+        cp_partials<false>(g, sTt, nullptr, c0, pa, nullptr);
+        // the probes' tile (wave w: probes 4w..4w+3), loaded while the partials land
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j < g.rmax) g.out[(int64_t)j * g.N + c] = a[j];
-        __syncthreads();  // the previous tile's MFMA readers are done with sB2 / sP
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sB2[j][tid] = a[j];
-#pragma unroll
-        for (int p = 0; p < PNP; ++p) sP[p][tid] = live ? g.P[(int64_t)p * g.N + c] : 0.0;
+        for (int i = 0; i < 4; ++i) sP[4 * wave + i][lane] = c < g.N ? g.P[(int64_t)(4 * wave + i) * g.N + c] : 0.0;
         __syncthreads();
-        // V^T[j][p] += sum over the wave's 64 columns of B''[j][col] P[p][col] (A operand: rows j, 8..15 zero)
 #pragma unroll
-        for (int s4 = 0; s4 < 16; ++s4) {
-            const int col = 64 * wave + 4 * s4 + l4;
-            const double av = l16 < 8 ? sB2[l16][col] : 0.0;
-            v = __builtin_amdgcn_mfma_f64_16x16x4f64(av, sP[l16][col], v, 0, 0, 0);
+        for (int i = 0; i < 2; ++i) {  // wave w owns rows 2w, 2w + 1 of B''
+            const int j = 2 * wave + i;
+            const double b = (pa[0][j][lane] + pa[1][j][lane]) + (pa[2][j][lane] + pa[3][j][lane]);
+            sB2[j][lane] = b;
+            if (j < g.rmax && c < g.N) g.out[(int64_t)j * g.N + c] = b;
         }
+        __syncthreads();
+        const int j = jp >> 4, p = jp & 15;
+#pragma unroll 8
+        for (int l = 32 * half; l < 32 * half + 32; ++l) v = fma(sB2[j][l], sP[p][l], v);
+        __syncthreads();  // the next tile's partials / probes overwrite the planes
     }
-    // the waves' blocks summed in wave order -> this workgroup's partial [8][16]
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-        const int j = l4 + 4 * rr;
-        if (j < 8) red[wave][j][l16] = v[rr];
-    }
+    vh[half][jp] = v;
     __syncthreads();
-    if (tid < 8 * PNP) {
-        const int j = tid >> 4, p = tid & 15;
-        g.part[(int64_t)blockIdx.x * 128 + tid] = (red[0][j][p] + red[1][j][p]) + (red[2][j][p] + red[3][j][p]);
-    }
+    if (tid < 128) g.part[(int64_t)blockIdx.x * 128 + tid] = vh[0][tid] + vh[1][tid];
 }
 
 // V [8][16] = sum of the n per-workgroup partials of qk_cp_b_kernel, in workgroup order (one workgroup,
-// 128 threads: thread t owns entry t, eight independent chains, combined in a fixed order). A kernel of
-// its own: a last-workgroup fold inside qk_cp_b_kernel needs a device-scope release per workgroup, an
-// L2 write-back on gfx950 (measured: 49 us for the launch instead of the loads' ~10).
+// 128 threads: thread t owns entry t, eight independent chains, combined in a fixed order).
 __global__ __launch_bounds__(128) void qk_cp_vsum_kernel(const double* __restrict__ part, int n, double* __restrict__ V) {
     const int tid = threadIdx.x;
     double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -564,61 +568,67 @@ __global__ __launch_bounds__(128) void qk_cp_vsum_kernel(const double* __restric
     V[tid] = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
 }
 
-__global__ __launch_bounds__(CP_T) void qk_cp_a_kernel(CpArgs g) {
-    __shared__ double sT[8][PK];
+__global__ __launch_bounds__(CP_T, 2) void qk_cp_a_kernel(CpArgs g) {
+    __shared__ double sTt[PK][8];
     __shared__ double sU[PK][PNP];
     __shared__ double sV[8][PNP];
-    __shared__ double red[4][2 * PNP];
+    __shared__ double pa[4][8][CP_C];
+    __shared__ double pr[4][PNP][CP_C];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int e = tid; e < 8 * PK; e += CP_T) sT[e / PK][e % PK] = (e / PK < g.rmax && e % PK < g.K) ? g.T[(e / PK) * g.K + e % PK] : 0.0;
+    for (int e = tid; e < 8 * PK; e += CP_T) {
+        const int k = e >> 3, j = e & 7;
+        sTt[k][j] = (j < g.rmax && k < g.K) ? g.T[j * g.K + k] : 0.0;
+    }
     for (int e = tid; e < PK * PNP; e += CP_T) sU[e / PNP][e % PNP] = e / PNP < g.K ? g.U[e] : 0.0;
     if (tid < 8 * PNP) sV[tid >> 4][tid & 15] = g.V[tid];
     __syncthreads();
-    double e2[PNP], f2[PNP];
-#pragma unroll
-    for (int p = 0; p < PNP; ++p) e2[p] = f2[p] = 0.0;
-    const int64_t tiles = (g.N + CP_T - 1) / CP_T;
+    double e2[4] = {0, 0, 0, 0}, f2[4] = {0, 0, 0, 0};  // wave w: probes 4w..4w+3
+    const int64_t tiles = (g.N + CP_C - 1) / CP_C;
     for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
-        const int64_t c = t * CP_T + tid;
-        double a[8], rp[PNP];
-        cp_column(g, sT, c, a, rp, sU);
+        const int64_t c0 = t * CP_C, c = c0 + lane;
+        cp_partials<true>(g, sTt, sU, c0, pa, pr);
+        __syncthreads();
+        double a[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = (pa[0][j][lane] + pa[1][j][lane]) + (pa[2][j][lane] + pa[3][j][lane]);
         if (c < g.N) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
+            for (int i = 0; i < 2; ++i) {  // wave w stores rows 2w, 2w + 1 of A''
+                const int j = 2 * wave + i;
                 if (j < g.rmax) g.out[(int64_t)j * g.N + c] = a[j];
+            }
 #pragma unroll
-            for (int p = 0; p < PNP; ++p) {
-                double d = rp[p];
+            for (int i = 0; i < 4; ++i) {
+                const int p = 4 * wave + i;
+                const double rp = (pr[0][p][lane] + pr[1][p][lane]) + (pr[2][p][lane] + pr[3][p][lane]);
+                double d = rp;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) d = fma(-a[j], sV[j][p], d);
-                e2[p] = fma(d, d, e2[p]);
-                f2[p] = fma(rp[p], rp[p], f2[p]);
+                e2[i] = fma(d, d, e2[i]);
+                f2[i] = fma(rp, rp, f2[i]);
             }
         }
+        __syncthreads();
     }
-    // sums over the workgroup in a fixed order: xor butterflies in each wave, then the 4 waves
+    // wave sums (xor butterflies: fixed order), lane 0 writes this wave's four probes
 #pragma unroll
-    for (int p = 0; p < PNP; ++p) {
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int sh = 1; sh < 64; sh <<= 1) {
-            e2[p] += __shfl_xor(e2[p], sh, 64);
-            f2[p] += __shfl_xor(f2[p], sh, 64);
+            e2[i] += __shfl_xor(e2[i], sh, 64);
+            f2[i] += __shfl_xor(f2[i], sh, 64);
         }
-    }
     if (lane == 0)
 #pragma unroll
-        for (int p = 0; p < PNP; ++p) {
-            red[wave][p] = e2[p];
-            red[wave][PNP + p] = f2[p];
+        for (int i = 0; i < 4; ++i) {
+            g.part[(int64_t)blockIdx.x * 2 * PNP + 4 * wave + i] = e2[i];
+            g.part[(int64_t)blockIdx.x * 2 * PNP + PNP + 4 * wave + i] = f2[i];
         }
-    __syncthreads();
-    if (tid < 2 * PNP)
-        g.part[(int64_t)blockIdx.x * 2 * PNP + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
 }
 
 int cp_grid(qk_ctx* ctx, int64_t N) {
-    const int64_t tiles = (N + CP_T - 1) / CP_T;
-    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 4;
+    const int64_t tiles = (N + CP_C - 1) / CP_C;
+    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 2;
     return (int)(tiles < cap ? (tiles > 0 ? tiles : 1) : cap);
 }
 

@@ -398,10 +398,10 @@ class KnitPipeline:
         self._pending = []  # device (rank, accepted) of steps not yet read back
         # slice mode, fused preparation: every rank factors the same all-reduced Grams with the same
         # deterministic kernel, so no broadcast of the factors; each rank checks the rows of R in its
-        # A column block against every probe and the squared errors are all-reduced (16 doubles), so
-        # one decision covers all of R and every rank takes it (the exact-slice fallback's
-        # collectives then match across ranks). Factors that differed between ranks would mix
-        # compressed columns and fail the summed check. QKNIT_SLICE_SYNC=1: rank 0's factors broadcast.
+        # A column block against every probe, and a MIN all-reduce of the accepted ranks gives one
+        # decision for all ranks (the A blocks cover all of R; a rejection anywhere sends every rank
+        # to the exact slice, so its collectives match). Factors that differed between ranks would mix
+        # compressed columns and fail some rank's check. QKNIT_SLICE_SYNC=1: rank 0's factors broadcast.
         self.slice_sync = os.environ.get("QKNIT_SLICE_SYNC", "0") == "1"
         self.last_kernel = None  # kernel of the last compressed contraction (None: qk_gemm_keyed)
         self.last_prep = None  # data-rank preparation of the last step: "fused" (qk_prep_operands) or "torch"
@@ -849,12 +849,12 @@ class KnitPipeline:
         """Slice mode (multi-GPU), the preparation of this rank's write: ``qs`` hold every instance
         row of this rank's column block of each operand (the sweep's all_to_all). Collectives (fused
         preparation): one all_reduce of the two Grams + the B side against the probes, one
-        all_gather of the compressed column blocks (rmax x 2^m per fragment), one all_reduce of the
-        16 squared probe errors; every rank factors the identical all-reduced Grams with the same
-        deterministic kernel (no broadcast unless QKNIT_SLICE_SYNC=1) and takes the same decision
-        from the summed errors. The write itself is local. A rejected compression (read back after
-        the write is queued) makes every rank take the exact contraction of its slice from
-        all-gathered operands. The torch preparation broadcasts rank 0's factors instead."""
+        all_gather of the compressed column blocks (rmax x 2^m per fragment), one MIN all_reduce of
+        the ranks' accepted ranks (each checks its rows of R); every rank factors the identical
+        all-reduced Grams with the same deterministic kernel (no broadcast unless QKNIT_SLICE_SYNC=1).
+        The write itself is local. A rejected compression on any rank (read back after the write is
+        queued) makes every rank take the exact contraction of its slice from all-gathered operands.
+        The torch preparation broadcasts rank 0's factors instead."""
         import torch.distributed as dist
 
         T, be, P = self.T, self.be, self.world
@@ -907,23 +907,19 @@ class KnitPipeline:
         A2 = gat[:, :R8 * bwA].view(P, R8, bwA).permute(1, 0, 2).reshape(R8, P * bwA).contiguous()
         B2 = gat[:, R8 * bwA:].view(P, R8, bwB).permute(1, 0, 2).reshape(R8, P * bwB).contiguous()
         if self._fused_prep(qs):
-            # this rank's A columns against all probes (B2 / probes: every column), summed over ranks:
-            # the summed e2 covers every row of R, and every rank takes the same decision from it, so
-            # the exact-slice fallback's collectives (_slice_exact) run on all ranks or on none
+            # this rank's A columns (its rows of R) against all probes (B2 / probes: every column)
             e2, _, _ = be.probe_errors(XA, A2, U, B2, x_full.contiguous(), a2_cols=(self.rank * bwA, bwA))
-            dist.all_reduce(e2, group=self.group)
             k_eff, _ = be.probe_accept(e2, r, self.rank_tol, self.rank_tol_rel)
             self._pending.append((r, k_eff))
         else:
             # rows of R in this rank's A column block, against all probes
             ref_rows = XA.T @ Bx
             cmp_rows = A2[:, self.rank * bwA:(self.rank + 1) * bwA].T @ _mm_nt(B2, x_full)
-
-            def reduce_err(e2):
-                dist.all_reduce(e2, group=self.group)
-                return e2
-
-            k_eff, _ = self._accept(None, None, None, None, None, r, ref_rows, cmp_rows, reduce_err)
+            k_eff, _ = self._accept(None, None, None, None, None, r, ref_rows, cmp_rows)
+        # one decision for every rank: the accepted rank only if every rank's rows of R passed (the A
+        # column blocks cover all of R; the ranks' factors are identical, so the local ranks are r or 0).
+        # A rejection anywhere makes every rank take the exact slice, whose collectives then match.
+        dist.all_reduce(k_eff, op=dist.ReduceOp.MIN, group=self.group)
         on_gpu = k_eff.device.type == "cuda"
         pinned = T.empty(1, dtype=T.int32, pin_memory=on_gpu)
         pinned.copy_(k_eff, non_blocking=on_gpu)

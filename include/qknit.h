@@ -334,7 +334,7 @@ int qk_probe_accept(qk_ctx* ctx, const double* e2, int n, const int32_t* r_dev, 
 
 /* Single GPU (every column of both operands on this device): qk_compress_operands + qk_probe_errors (with
  * k_out) — the B side's compression carries the V = B'' P^T partial sums, the A side's the probe rows, so
- * each operand is read once (row-contiguous, a thread per column); one-workgroup kernels fold the partials
+ * each operand is read once (a lane per column, K split over a workgroup's waves); one-workgroup kernels fold the partials
  * in a fixed order. Same outputs: A2 [rmax][NA], B2 [rmax][NB], e2 [32], *k_out, *err_out (DEVICE).
  * work: qk_compress_probe_workspace_bytes. */
 int qk_compress_probe_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes);

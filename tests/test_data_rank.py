@@ -61,7 +61,7 @@ def test_pipeline_data_rank_matches_oracle(case, force_fallback):
     pipe = KnitPipeline(VirtualCircuit(cut), factored=True, backend=CpuBackend(), data_rank=True)
     assert pipe.data_rank
     if force_fallback:
-        pipe.rank_tol = pipe.rank_tol_rel = -1.0  # every probe check fails
+        pipe.rank_tol = pipe.rank_tol_rel = float("nan")  # every probe check fails
     ref = dense.run_dense(cut)
     for _ in range(2):  # host path: gives up after RANK_GIVE_UP (3) rejections in a row; device path: per step
         res = pipe.step().numpy().copy()

@@ -106,7 +106,7 @@ def test_multi_rank_pipeline_matches_oracle(case, mode, factored, world):
     np.testing.assert_allclose(res, ref, atol=1e-12, rtol=0)
 
 
-def _slice_worker(rank, world, port, case, data_rank, q):
+def _slice_worker(rank, world, port, case, data_rank, q, veto_rank=None):
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -124,6 +124,8 @@ def _slice_worker(rank, world, port, case, data_rank, q):
         pipe = KnitPipeline(VirtualCircuit(cut), rank=rank, world=world, factored=True, backend=CpuBackend(),
                             data_rank=data_rank)
         assert pipe.mode == "slice"
+        if veto_rank == rank:  # this rank's probe check rejects every compression
+            pipe.rank_tol = pipe.rank_tol_rel = float("nan")
         outs = []
         for _ in range(2):
             res = pipe.step().clone()
@@ -238,3 +240,28 @@ def test_run_virtual_circuit_sharded_api(case, world):
         assert shards[0] == (0, n) and all(s == (0, 0) for s in shards[1:])
     else:
         assert shards == [(r * n // world, n // world) for r in range(world)]
+
+
+def test_slice_mode_one_rank_rejects():
+    """A probe check that rejects on ONE rank only (that rank's tolerance forced below zero): the MIN
+    all-reduce of the accepted ranks sends every rank to the exact slice together (their
+    collectives match: no hang), and the slices still concatenate to the oracle's knit."""
+    from oracle import dense
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_slice_worker, args=(r, world, port, "hwe_p2", True, q, 1)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs, sl, last_rank, fallbacks, incompressible, dev, prep = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sys.path.insert(0, HERE)
+    _, cut = _slice_case("hwe_p2")
+    ref = dense.run_dense(cut)
+    for got in outs:
+        np.testing.assert_allclose(got, ref, atol=1e-12, rtol=0)
+    assert dev and fallbacks == 2 and last_rank is None  # rank 0 accepted locally, yet took the exact path

@@ -1121,8 +1121,8 @@ def test_knit_lowrank_c_entry_matches_oracle(T, case, reject):
         circ, cut = CASES[case]()
     pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
     qs = pipe.sweep()
-    out, rank = engine.knit_lowrank_c(engine.get_context(0), pipe, qs, rank_tol=-1.0 if reject else None,
-                                      rank_tol_rel=-1.0 if reject else None)
+    out, rank = engine.knit_lowrank_c(engine.get_context(0), pipe, qs, rank_tol=float("nan") if reject else None,
+                                      rank_tol_rel=float("nan") if reject else None)
     np.testing.assert_allclose(out.cpu().numpy(), dense.run_dense(cut), atol=TOL, rtol=0)
     r = int(rank.item())
     assert (r == 0) if reject else (0 <= r <= 8)

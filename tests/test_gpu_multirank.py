@@ -64,7 +64,7 @@ def _watchdog(rank, tag, after=100):
     return log
 
 
-def _worker(rank, world, port, case, mode, factored, q):
+def _worker(rank, world, port, case, mode, factored, q, overlap=False, veto_rank=None):
     log = _watchdog(rank, f"{case}_{mode}_{world}")
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
@@ -83,10 +83,18 @@ def _worker(rank, world, port, case, mode, factored, q):
         pipe = KnitPipeline(VirtualCircuit(cut), device=0, rank=rank, world=world, mode=mode, factored=factored,
                             data_rank=factored)
         assert pipe.be.dev.type == "cuda"
+        if overlap:  # pipelined steps (the multi-GPU bench default): a non-default caller stream
+            torch.cuda.set_stream(torch.cuda.Stream())
+            pipe.overlap = pipe.overlap_ok()
+            assert pipe.overlap
+        if veto_rank == rank:
+            pipe.rank_tol = pipe.rank_tol_rel = float("nan")
         log(f"planned: mode {pipe.mode}")
         outs = []
         for it in range(2):
-            res = pipe.step().cpu().clone()
+            res = pipe.step()
+            torch.cuda.synchronize()
+            res = res.cpu().clone()
             log(f"step {it}")
             if pipe.mode == "slice":
                 parts = [torch.empty_like(res) for _ in range(world)]
@@ -115,11 +123,11 @@ def _worker(rank, world, port, case, mode, factored, q):
         dist.destroy_process_group()
 
 
-def _run(target, world, *args, timeout=300):
+def _run(target, world, *args, timeout=300, **kw):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, q), kwargs=kw) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -158,6 +166,32 @@ def test_multi_rank_hip_matches_oracle(case, mode, factored, world):
         assert incompressible == 2 and last_rank is None
     if case == "cx_3cuts" and mode == "gather":
         assert last_rank is not None and last_rank < terms  # the gather-mode data-rank branch ran
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("case,world,veto", [("hwe_p2", 8, None), ("cx_8x8", 4, None), ("hwe_p2", 4, 2)])
+def test_multi_rank_hip_overlapped_steps_match_oracle(case, world, veto):
+    """Pipelined steps (step i+1's sweep, preparation and collectives on a CU-masked stream under step
+    i's write: the multi-GPU bench default) in slice mode on 4-8 ranks sharing the GPU, twice in a
+    row, against the oracle at 1e-12: hwe (compressed every step), cx_8x8 (rank > 8: the exact slice
+    with its all-gathers), and a probe check rejecting on one rank only (every rank takes the exact
+    slice together)."""
+    sys.path.insert(0, HERE)
+    from oracle import dense
+
+    got_mode, outs, last_rank, fallbacks, incompressible, dev, kernel, terms = _run(
+        _worker, world, case, "slice", True, timeout=360, overlap=True, veto_rank=veto)
+    assert got_mode == "slice" and dev
+    _, cut = _case(case)
+    ref = dense.run_dense(cut)
+    for full in outs:
+        np.testing.assert_allclose(full, ref, atol=TOL, rtol=0)
+    if veto is not None:
+        assert fallbacks == 2 and last_rank is None
+    elif case == "hwe_p2":
+        assert fallbacks == 0 and last_rank is not None
+    else:
+        assert incompressible == 2
 
 
 def _syc_worker(rank, world, port, q):
