@@ -210,8 +210,8 @@ int qk_knit(qk_ctx* ctx, const qk_knit_plan* plan, const double* const* q, void*
 // Steps, all on ctx->stream with no host synchronisation (DESIGN.md §2 "Data-rank compression"):
 //   1. qk_prep_operands   X_A = Wt_A^T q_A, X_B = Wt_B^T q_B, G_A, G_B, U = X_B P^T
 //   2. qk_rank_factors    T_A, T_B, r from the Grams (r = 0: no factorisation of rank <= 8)
-//   3.-4. qk_compress_probe  A'' = T_A X_A, B'' = T_B X_B (8 rows) and the probe check: accepted rank
-//                         k = r when every probe error is <= max(rank_tol, rank_tol_rel ||R p||), else 0
+//   3. qk_compress_operands  A'' = T_A X_A, B'' = T_B X_B  (8 rows)
+//   4. qk_probe_errors    accepted rank k = r when every probe error is <= max(rank_tol, rank_tol_rel ||R p||)
 //   5. qk_knit_outer_stream_range  the write-bound knit of A'', B'' with K = k (k = 0: nothing)
 //   6. qk_gemm_keyed_pred the exact K-term contraction of X_A, X_B, predicated on k == 0
 namespace {
@@ -243,7 +243,7 @@ int lowrank_layout(qk_ctx* ctx, const qk_lowrank_plan* p, LowrankLayout& L, std:
     const int64_t K = p->terms;
     int64_t prep = 0, probe = 0;
     int rc = qk_prep_workspace_bytes(ctx, NA, NB, &prep);
-    if (!rc) rc = qk_compress_probe_workspace_bytes(ctx, NA, NB, &probe);
+    if (!rc) rc = qk_probe_workspace_bytes(ctx, NA, &probe);
     if (rc) {
         why = "qk_knit_lowrank: workspace queries failed";
         return rc;
@@ -308,9 +308,10 @@ int qk_knit_lowrank(qk_ctx* ctx, const qk_lowrank_plan* p, const double* q_a, co
     rc = qk_prep_operands(ctx, K, (int)p->rows_a, p->wt_a, q_a, NA, NA, XA, (int)p->rows_b, p->wt_b, q_b, NB, NB, XB,
                           p->probes, G, G + K * K, U, D(L.prep), L.prep_bytes);
     if (!rc) rc = qk_rank_factors(ctx, K, G, G + K * K, p->lam_tol, p->s_tol, p->s_abs, LR_RMAX, D(L.ta), D(L.tb), r);
+    if (!rc) rc = qk_compress_operands(ctx, K, LR_RMAX, D(L.ta), XA, NA, D(L.a2), D(L.tb), XB, NB, D(L.b2));
     if (!rc)
-        rc = qk_compress_probe(ctx, K, LR_RMAX, D(L.ta), XA, NA, D(L.a2), D(L.tb), XB, NB, D(L.b2), U, p->probes, r,
-                               p->rank_tol, p->rank_tol_rel, D(L.e2), k, D(L.err), D(L.probe), L.probe_bytes);
+        rc = qk_probe_errors(ctx, K, LR_RMAX, XA, NA, NA, D(L.a2), NA, U, D(L.b2), NB, NB, p->probes, NB, D(L.e2), r,
+                             p->rank_tol, p->rank_tol_rel, k, D(L.err), D(L.probe), L.probe_bytes);
     if (!rc)
         rc = qk_knit_outer_stream_range(ctx, p->nbits, LR_RMAX, D(L.a2), NA, D(L.b2), NB, p->mask_a, p->mask_b, 0,
                                         int64_t(1) << p->nbits, k, out);

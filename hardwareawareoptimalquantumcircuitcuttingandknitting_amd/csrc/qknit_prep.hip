@@ -450,188 +450,6 @@ __global__ __launch_bounds__(256) void qk_probe_accept_kernel(const double* __re
     }
 }
 
-// ---- single-GPU tail of the data-rank step (qk_compress_probe) --------------------------------------------
-// Replaces qk_compress_operands + qk_probe_errors where one GPU holds every column: the V partial sums
-// ride on the B side's compression and the probe rows on the A side's, so each operand X is read once
-// (128 MB of reads -> 80 MB for syc 32 5). A workgroup takes 64-column tiles, a lane one column, the four
-// waves a quarter of K each (16 loads in flight per lane, one 512-B row segment per wave load); the
-// quarters meet in LDS. Per-workgroup partials are folded in workgroup order by one-workgroup kernels
-// (deterministic; a last-workgroup fold inside the launch needs a device-scope release per workgroup,
-// an L2 write-back on gfx950, measured slower).
-//   qk_cp_b_kernel: B'' = T_B X_B; V partial = B''_tile P_tile^T
-//   qk_cp_vsum_kernel: V [8][16]
-//   qk_cp_a_kernel: A'' = T_A X_A; (R p)_c = X_A[:, c]^T U, d_c = (R p)_c - A''[:, c]^T V; partials of
-//                   e2 = sum d^2 and f2 = sum (R p)_c^2
-//   qk_probe_accept_kernel: e2 / f2 [32], err and the accepted rank
-constexpr int CP_C = 64;      // columns per workgroup tile (a lane per column, the 4 waves split K in quarters)
-constexpr int CP_T = 256;     // threads
-
-struct CpArgs {
-    int K, rmax;
-    const double* T;     // [rmax][K]
-    const double* X;     // [K][N]
-    int64_t N;
-    double* out;         // [rmax][N]
-    const double* P;     // B side: probes [16][N]
-    const double* U;     // A side: [K][16]
-    double* V;           // [8][16]: summed by qk_cp_vsum_kernel, read by the A side
-    double* part;        // [gridDim.x][128 (B) or 32 (A)]
-};
-
-// Lane l of wave q: the partial sums over k in [16q, 16q + 16) of this tile's column c0 + l — a[j] of
-// T X (j < 8) and, with sU, r[p] of X^T U (p < 16) — into the LDS partial planes. The 16 loads of a lane
-// are in flight together; each is one 512-B row segment per wave.
-template <bool PROBE>
-__device__ __forceinline__ void cp_partials(const CpArgs& g, const double (*sTt)[8], const double (*sU)[PNP],
-                                            int64_t c0, double (*pa)[8][CP_C], double (*pr)[PNP][CP_C]) {
-    const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
-    const int64_t c = c0 + lane;
-    const bool live = c < g.N;
-    double xv[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int k = 16 * q + u;
-        xv[u] = (live && k < g.K) ? g.X[(int64_t)k * g.N + c] : 0.0;
-    }
-    double a[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] = 0.0;
-    double r[PROBE ? PNP : 1];
-#pragma unroll
-    for (int p = 0; p < (PROBE ? PNP : 1); ++p) r[p] = 0.0;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int k = 16 * q + u;  // rows >= K: T / U are zero there (and xv is 0)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = fma(sTt[k][j], xv[u], a[j]);
-        if (PROBE)
-#pragma unroll
-            for (int p = 0; p < PNP; ++p) r[p] = fma(xv[u], sU[k][p], r[p]);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) pa[q][j][lane] = a[j];
-    if (PROBE)
-#pragma unroll
-        for (int p = 0; p < PNP; ++p) pr[q][p][lane] = r[p];
-}
-
-__global__ __launch_bounds__(CP_T, 2) void qk_cp_b_kernel(CpArgs g) {
-    __shared__ double sTt[PK][8];       // T^T (rows >= rmax / K zero)
-    __shared__ double pa[4][8][CP_C];   // per-wave partials of B'' = T X
-    __shared__ double sB2[8][CP_C];
-    __shared__ double sP[PNP][CP_C];
-    __shared__ double vh[2][128];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int e = tid; e < 8 * PK; e += CP_T) {
-        const int k = e >> 3, j = e & 7;
-        sTt[k][j] = (j < g.rmax && k < g.K) ? g.T[j * g.K + k] : 0.0;
-    }
-    __syncthreads();
-    const int jp = tid & 127, half = tid >> 7;   // V partial: pair (j, p) = (jp >> 4, jp & 15), column half
-    double v = 0.0;
-    const int64_t tiles = (g.N + CP_C - 1) / CP_C;
-    for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
-        const int64_t c0 = t * CP_C, c = c0 + lane;
-        cp_partials<false>(g, sTt, nullptr, c0, pa, nullptr);
-        // the probes' tile (wave w: probes 4w..4w+3), loaded while the partials land
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sP[4 * wave + i][lane] = c < g.N ? g.P[(int64_t)(4 * wave + i) * g.N + c] : 0.0;
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {  // wave w owns rows 2w, 2w + 1 of B''
-            const int j = 2 * wave + i;
-            const double b = (pa[0][j][lane] + pa[1][j][lane]) + (pa[2][j][lane] + pa[3][j][lane]);
-            sB2[j][lane] = b;
-            if (j < g.rmax && c < g.N) g.out[(int64_t)j * g.N + c] = b;
-        }
-        __syncthreads();
-        const int j = jp >> 4, p = jp & 15;
-#pragma unroll 8
-        for (int l = 32 * half; l < 32 * half + 32; ++l) v = fma(sB2[j][l], sP[p][l], v);
-        __syncthreads();  // the next tile's partials / probes overwrite the planes
-    }
-    vh[half][jp] = v;
-    __syncthreads();
-    if (tid < 128) g.part[(int64_t)blockIdx.x * 128 + tid] = vh[0][tid] + vh[1][tid];
-}
-
-// V [8][16] = sum of the n per-workgroup partials of qk_cp_b_kernel, in workgroup order (one workgroup,
-// 128 threads: thread t owns entry t, eight independent chains, combined in a fixed order).
-__global__ __launch_bounds__(128) void qk_cp_vsum_kernel(const double* __restrict__ part, int n, double* __restrict__ V) {
-    const int tid = threadIdx.x;
-    double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int b = 0;
-    for (; b + 8 <= n; b += 8)
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s8[u] += part[(int64_t)(b + u) * 128 + tid];
-    for (; b < n; ++b) s8[0] += part[(int64_t)b * 128 + tid];
-    V[tid] = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
-}
-
-__global__ __launch_bounds__(CP_T, 2) void qk_cp_a_kernel(CpArgs g) {
-    __shared__ double sTt[PK][8];
-    __shared__ double sU[PK][PNP];
-    __shared__ double sV[8][PNP];
-    __shared__ double pa[4][8][CP_C];
-    __shared__ double pr[4][PNP][CP_C];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int e = tid; e < 8 * PK; e += CP_T) {
-        const int k = e >> 3, j = e & 7;
-        sTt[k][j] = (j < g.rmax && k < g.K) ? g.T[j * g.K + k] : 0.0;
-    }
-    for (int e = tid; e < PK * PNP; e += CP_T) sU[e / PNP][e % PNP] = e / PNP < g.K ? g.U[e] : 0.0;
-    if (tid < 8 * PNP) sV[tid >> 4][tid & 15] = g.V[tid];
-    __syncthreads();
-    double e2[4] = {0, 0, 0, 0}, f2[4] = {0, 0, 0, 0};  // wave w: probes 4w..4w+3
-    const int64_t tiles = (g.N + CP_C - 1) / CP_C;
-    for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
-        const int64_t c0 = t * CP_C, c = c0 + lane;
-        cp_partials<true>(g, sTt, sU, c0, pa, pr);
-        __syncthreads();
-        double a[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = (pa[0][j][lane] + pa[1][j][lane]) + (pa[2][j][lane] + pa[3][j][lane]);
-        if (c < g.N) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {  // wave w stores rows 2w, 2w + 1 of A''
-                const int j = 2 * wave + i;
-                if (j < g.rmax) g.out[(int64_t)j * g.N + c] = a[j];
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int p = 4 * wave + i;
-                const double rp = (pr[0][p][lane] + pr[1][p][lane]) + (pr[2][p][lane] + pr[3][p][lane]);
-                double d = rp;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) d = fma(-a[j], sV[j][p], d);
-                e2[i] = fma(d, d, e2[i]);
-                f2[i] = fma(rp, rp, f2[i]);
-            }
-        }
-        __syncthreads();
-    }
-    // wave sums (xor butterflies: fixed order), lane 0 writes this wave's four probes
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int sh = 1; sh < 64; sh <<= 1) {
-            e2[i] += __shfl_xor(e2[i], sh, 64);
-            f2[i] += __shfl_xor(f2[i], sh, 64);
-        }
-    if (lane == 0)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            g.part[(int64_t)blockIdx.x * 2 * PNP + 4 * wave + i] = e2[i];
-            g.part[(int64_t)blockIdx.x * 2 * PNP + PNP + 4 * wave + i] = f2[i];
-        }
-}
-
-int cp_grid(qk_ctx* ctx, int64_t N) {
-    const int64_t tiles = (N + CP_C - 1) / CP_C;
-    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 2;
-    return (int)(tiles < cap ? (tiles > 0 ? tiles : 1) : cap);
-}
-
 int probe_grid_d(qk_ctx* ctx, int64_t NA) {
     const int64_t blocks = (NA + 63) / 64;  // 4 waves x 16 columns
     const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 2;
@@ -739,41 +557,6 @@ int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx,
                        k_out, err_out);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_probe_errors: ") + hipGetErrorString(e)).c_str());
-    return QK_OK;
-}
-
-int qk_compress_probe_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes) {
-    if (!ctx || !bytes) return QK_EARG;
-    // V [8][16] + the two launches' partials
-    *bytes = (int64_t)(128 + (int64_t)cp_grid(ctx, NB) * 128 + (int64_t)cp_grid(ctx, NA) * 2 * PNP) * 8;
-    return QK_OK;
-}
-
-int qk_compress_probe(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, double* A2,
-                      const double* TB, const double* XB, int64_t NB, double* B2, const double* U, const double* probes,
-                      const int32_t* r_dev, double tol, double rel_tol, double* e2, int32_t* k_out, double* err_out,
-                      void* work, int64_t work_bytes) {
-    if (!ctx) return QK_EARG;
-    if (K < 1 || K > PK || rmax < 1 || rmax > 8 || NA < 1 || NB < 1)
-        return fail(ctx, QK_EARG, "qk_compress_probe: need 1 <= K <= 64, 1 <= rmax <= 8, N >= 1");
-    if (!TA || !XA || !A2 || !TB || !XB || !B2 || !U || !probes || !r_dev || !work)
-        return fail(ctx, QK_EARG, "qk_compress_probe: null buffer");
-    int64_t need = 0;
-    qk_compress_probe_workspace_bytes(ctx, NA, NB, &need);
-    if (work_bytes < need) return fail(ctx, QK_EARG, "qk_compress_probe: workspace too small (qk_compress_probe_workspace_bytes)");
-    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_compress_probe: hipSetDevice");
-    double* V = static_cast<double*>(work);
-    double* part = V + 128;
-    const int gb = cp_grid(ctx, NB), ga = cp_grid(ctx, NA);
-    CpArgs b{K, rmax, TB, XB, NB, B2, probes, nullptr, V, part};
-    hipLaunchKernelGGL(qk_cp_b_kernel, dim3(gb), dim3(CP_T), 0, ctx->stream, b);
-    hipLaunchKernelGGL(qk_cp_vsum_kernel, dim3(1), dim3(128), 0, ctx->stream, part, gb, V);
-    CpArgs a{K, rmax, TA, XA, NA, A2, nullptr, U, V, part};
-    hipLaunchKernelGGL(qk_cp_a_kernel, dim3(ga), dim3(CP_T), 0, ctx->stream, a);
-    hipLaunchKernelGGL(qk_probe_accept_kernel, dim3(1), dim3(256), 0, ctx->stream, part, ga, r_dev, tol, rel_tol, e2,
-                       k_out, err_out);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_compress_probe: ") + hipGetErrorString(e)).c_str());
     return QK_OK;
 }
 

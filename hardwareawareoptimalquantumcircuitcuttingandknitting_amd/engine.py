@@ -881,38 +881,6 @@ def compress_operands(ctx: Context, TA, XA, TB, XB):
 
 
 _PROBE_WORK: dict = {}
-_CP_WORK: dict = {}
-
-
-def compress_probe(ctx: Context, TA, XA, TB, XB, U, probes, r, tol: float, rel_tol: float = 0.0):
-    """``qk_compress_probe`` (single GPU, every column of both operands here): the compressed operands
-    ``A2 = TA XA``, ``B2 = TB XB`` and the probe check of ``qk_probe_errors`` + ``qk_probe_accept`` in two
-    launches. Returns ``(A2, B2, e2 [32], k, err)``, all on the device."""
-    T = torch()
-    rmax, K = TA.shape
-    NA, NB = XA.shape[1], XB.shape[1]
-    assert TB.shape == (rmax, K) and XA.shape[0] == K and XB.shape[0] == K and U.shape == (K, N_PROBES)
-    assert probes.shape == (N_PROBES, NB) and all(t.is_contiguous() for t in (TA, XA, TB, XB, U, probes))
-    dev = XA.device
-    ab = T.empty(rmax * (NA + NB), dtype=T.float64, device=dev)
-    A2, B2 = ab[:rmax * NA].view(rmax, NA), ab[rmax * NA:].view(rmax, NB)
-    need = ctypes.c_int64()
-    ctx.check(ctx.lib.qk_compress_probe_workspace_bytes(ctx.handle, NA, NB, ctypes.byref(need)),
-              "qk_compress_probe_workspace_bytes")
-    key = (str(dev), T.cuda.current_stream(dev).cuda_stream)
-    work = _CP_WORK.get(key)
-    if work is None or work.numel() < need.value:
-        work = _CP_WORK[key] = T.empty(max(need.value, 8), dtype=T.uint8, device=dev)
-    e2 = T.empty(2 * N_PROBES, dtype=T.float64, device=dev)
-    k = T.empty(1, dtype=T.int32, device=dev)
-    err = T.empty(1, dtype=T.float64, device=dev)
-    ctx.check(ctx.lib.qk_compress_probe(ctx.handle, K, rmax, TA.data_ptr(), XA.data_ptr(), NA, A2.data_ptr(),
-                                        TB.data_ptr(), XB.data_ptr(), NB, B2.data_ptr(), U.data_ptr(),
-                                        probes.data_ptr(), r.data_ptr(), tol, rel_tol, e2.data_ptr(), k.data_ptr(),
-                                        err.data_ptr(), work.data_ptr(), work.numel()), "qk_compress_probe")
-    return A2, B2, e2, k, err
-
-
 def probe_errors(ctx: Context, XA, A2, U, B2, probes, r=None, tol: float = 0.0, a2_cols: tuple | None = None,
                  rel_tol: float = 0.0):
     """``qk_probe_errors``: ``e2`` ([32]) = the squared probe errors of the compressed knit ([:16]) and the

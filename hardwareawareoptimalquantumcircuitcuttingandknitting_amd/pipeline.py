@@ -308,9 +308,6 @@ class HipBackend:
     def compress(self, TA, XA, TB, XB):
         return engine.compress_operands(self.ctx, TA, XA, TB, XB)
 
-    def compress_probe(self, TA, XA, TB, XB, U, probes, r, tol, rel_tol):
-        return engine.compress_probe(self.ctx, TA, XA, TB, XB, U, probes, r, tol, rel_tol)
-
     def knit_select(self, A, B, clbits_a, clbits_b, nbits, accuracy, k_dev=None):
         return engine.knit_select(self.ctx, A, B, clbits_a, clbits_b, nbits, accuracy, k_dev=k_dev)
 
@@ -813,14 +810,9 @@ class KnitPipeline:
             x = self._probes(qs[ib].shape[1], qs[ib].device)
             mats, G, U = self._prep_fused(qs, x)
             TA, TB, r = self.be.rank_factors(G[0], G[1])
-            if hasattr(self.be, "compress_probe") and os.environ.get("QKNIT_COMPRESS_PROBE", "1") == "1":
-                # two launches: compression + V partials, compression + probe rows + acceptance
-                A2, B2, _, k_eff, _ = self.be.compress_probe(TA, mats[ia], TB, mats[ib], U, x, r, self.rank_tol,
-                                                             self.rank_tol_rel)
-            else:
-                A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib])
-                _, k_eff, _ = self.be.probe_errors(mats[ia], A2, U, B2, x, r=r, tol=self.rank_tol,
-                                                   rel_tol=self.rank_tol_rel)
+            A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib])
+            _, k_eff, _ = self.be.probe_errors(mats[ia], A2, U, B2, x, r=r, tol=self.rank_tol,
+                                               rel_tol=self.rank_tol_rel)
             self._pending.append((r, k_eff))
             return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
         mats = self.operands(qs)

@@ -247,7 +247,7 @@ int qk_knit(qk_ctx* ctx, const qk_knit_plan* plan, const double* const* q, void*
 
 /* ---- plan-level low-rank knit: the benched single-GPU step's knit in one call (qknit_plan.hip) ----
  * KnitPipeline's device data rank for a two-fragment knit, chained on the context's
- * stream with no host synchronisation: qk_prep_operands -> qk_rank_factors -> qk_compress_probe ->
+ * stream with no host synchronisation: qk_prep_operands -> qk_rank_factors -> qk_compress_operands ->
  * qk_probe_errors -> qk_knit_outer_stream_range (write-bound, K = accepted rank) -> qk_gemm_keyed_pred
  * (the exact terms-wide contraction, runs only when the check rejected). Same result as qk_knit on the
  * same transforms within the probe tolerance. q_a / q_b: the swept rows ([rows][2^popcount(mask)]).
@@ -331,17 +331,6 @@ int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx,
                     double* err_out, double* work, int64_t work_bytes);
 int qk_probe_accept(qk_ctx* ctx, const double* e2, int n, const int32_t* r_dev, double tol, double rel_tol,
                     int32_t* k_out, double* err_out);
-
-/* Single GPU (every column of both operands on this device): qk_compress_operands + qk_probe_errors (with
- * k_out) — the B side's compression carries the V = B'' P^T partial sums, the A side's the probe rows, so
- * each operand is read once (a lane per column, K split over a workgroup's waves); one-workgroup kernels fold the partials
- * in a fixed order. Same outputs: A2 [rmax][NA], B2 [rmax][NB], e2 [32], *k_out, *err_out (DEVICE).
- * work: qk_compress_probe_workspace_bytes. */
-int qk_compress_probe_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes);
-int qk_compress_probe(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, double* A2,
-                      const double* TB, const double* XB, int64_t NB, double* B2, const double* U, const double* probes,
-                      const int32_t* r_dev, double tol, double rel_tol, double* e2, int32_t* k_out, double* err_out,
-                      void* work, int64_t work_bytes);
 
 /* ---- post-processing (reference-shaped results; quasi_distr.py:3-43, run.py:71) ---------- */
 

@@ -1171,35 +1171,3 @@ def ctypes_size(ctx, comm):
     n, r = ctypes.c_int(), ctypes.c_int()
     ctx.check(ctx.lib.qk_comm_size(comm.handle, ctypes.byref(n), ctypes.byref(r)), "qk_comm_size")
     return n.value, r.value
-
-
-@pytest.mark.parametrize("K,NA,NB,r,noise", [(64, 65536, 65536, 2, 0.0), (64, 4096, 1000, 4, 0.0), (24, 320, 8192, 3, 0.0),
-                                             (64, 65536, 65536, 2, 1e-9)])
-def test_compress_probe_matches_separate_kernels(T, K, NA, NB, r, noise):
-    """qk_compress_probe (two launches: B'' with the V partials, A'' with the probe rows and the
-    acceptance, partials folded by each launch's last workgroup) == qk_compress_operands +
-    qk_probe_errors (four launches): the compressed operands to 1e-13 relative, the probe errors and
-    reference products to the fp64 floor of the products, the same accepted rank; deterministic."""
-    ctx = engine.get_context(0)
-    rng = np.random.default_rng(K + NA + NB + r)
-    core = rng.standard_normal((8, r)) @ rng.standard_normal((r, 8))
-    PA = rng.standard_normal((K, 8))
-    PB = np.linalg.pinv(PA.T) @ core
-    XA = T.from_numpy(PA @ rng.standard_normal((8, NA))).cuda()
-    XB = T.from_numpy(PB @ rng.standard_normal((8, NB)) + noise * rng.standard_normal((K, NB))).cuda()
-    x = T.from_numpy(np.random.default_rng(1234).standard_normal((16, NB))).cuda()
-    U = (XB @ x.T).contiguous()
-    TA, TB, rd = engine.rank_factors_device(ctx, (XA @ XA.T).contiguous(), (XB @ XB.T).contiguous())
-    A2, B2 = engine.compress_operands(ctx, TA, XA, TB, XB)
-    tol = 1e-12 * float((XA.T @ U).norm(dim=0).max())
-    e2, k, err = engine.probe_errors(ctx, XA, A2, U, B2, x, r=rd, tol=tol)
-    A2f, B2f, e2f, kf, errf = engine.compress_probe(ctx, TA, XA, TB, XB, U, x, rd, tol)
-    A2g, B2g, e2g, kg, _ = engine.compress_probe(ctx, TA, XA, TB, XB, U, x, rd, tol)
-    T.cuda.synchronize()
-    for got, ref in ((A2f, A2), (B2f, B2)):
-        assert float((got - ref).abs().max()) <= 1e-13 * float(ref.abs().max())
-    floor = 1e-13 * float((XA.T @ U).norm(dim=0).max())
-    assert float((e2f[:16].sqrt() - e2[:16].sqrt()).abs().max()) <= floor
-    assert float((e2f[16:].sqrt() - e2[16:].sqrt()).abs().max()) <= 1e-12 * float(e2[16:].sqrt().max())
-    assert int(kf.item()) == int(k.item()) == (0 if noise else r)
-    assert T.equal(A2f, A2g) and T.equal(B2f, B2g) and T.equal(e2f, e2g) and int(kg.item()) == int(kf.item())

@@ -48,7 +48,6 @@ def main():
     A2, B2 = engine.compress_operands(ctx, TA, XA, TB, XB)
     timed("compress_operands", lambda: engine.compress_operands(ctx, TA, XA, TB, XB))
     timed("probe_errors (v, d, accept)", lambda: engine.probe_errors(ctx, XA, A2, U, B2, P, r=r, tol=1e-14))
-    timed("compress_probe (fused tail)", lambda: engine.compress_probe(ctx, TA, XA, TB, XB, U, P, r, 1e-14))
     timed("rank_factors", lambda: engine.rank_factors_device(ctx, GA, GB))
     # the same compress on a non-power-of-two row length (row stride N + 64 doubles): a much lower
     # time per byte would point at HBM channel camping of the 2^19-byte row stride
