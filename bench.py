@@ -50,9 +50,10 @@ def parse():
     ap.add_argument("--no-general", action="store_true",
                     help="skip knit_general (the same step without data-rank compression)")
     ap.add_argument("--pipeline", action="store_true",
-                    help="pipelined steps: the next step's sweep + data-rank preparation on a CU-masked stream "
-                         "under the current step's write (DESIGN.md §4; measured box-dependent, off by default)")
-    ap.add_argument("--no-pipeline", action="store_true", help=argparse.SUPPRESS)
+                    help="one GPU: pipelined steps, the next step's sweep + data-rank preparation on a CU-masked "
+                         "stream under the current step's write (DESIGN.md §4; off by default on one GPU)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="several GPUs: plain steps instead of the default pipelined ones")
     return ap.parse_args()
 
 
@@ -540,9 +541,13 @@ def main():
     torch.cuda.set_stream(torch.cuda.Stream())
     pipe = KnitPipeline(virt, device=local, factored=not args.direct, rank=rank, world=world,
                         light_cone=not args.no_light_cone, data_rank=False if args.no_data_rank else None)
-    # pipelined steps (single GPU): step i+1's sweep + data-rank preparation run on a CU-masked stream
-    # while step i's write streams on the other CUs; every step still does all of its work
-    pipe.overlap = bool(world == 1 and args.pipeline and not args.no_pipeline and pipe.overlap_ok())
+    # pipelined steps: step i+1's sweep + data-rank preparation (+ its collectives) run on a CU-masked
+    # stream while step i's write streams on the other CUs; every step still does all of its work.
+    # Default on several GPUs (rank_sim with modelled xGMI, 8 ranks: 0.96 ms vs 1.17 ms per step,
+    # profiles/r03_rank_sim.jsonl), opt-in (--pipeline) on one (measured 6.28 vs 6.20 ms: the write
+    # loses more on 160 CUs than the 0.37 ms of sweep + preparation it hides)
+    want = args.pipeline if world == 1 else not args.no_pipeline
+    pipe.overlap = bool(want and pipe.overlap_ok())
     counts = pipe.instance_counts()
 
     def barrier():

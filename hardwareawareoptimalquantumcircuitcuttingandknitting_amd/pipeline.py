@@ -948,7 +948,10 @@ class KnitPipeline:
         return bool(self.dev_rank and self.mode in ("single", "slice") and getattr(self.be, "dev", None) is not None
                     and self.be.dev.type == "cuda")
 
-    PREP_CUS = 32  # CUs of the preparation stream in a pipelined step (QKNIT_PREP_CUS; 0: no CU split)
+    # CUs of the preparation stream in a pipelined step (QKNIT_PREP_CUS; 0: no CU split). rank_sim, 8
+    # ranks, modelled xGMI: 48 / 64 / 96 CUs -> 1.20 / 1.02 / 0.96 ms per step (the sweep on 32 CUs took
+    # 0.7 ms); one GPU: 64 and 96 alike (6.27 / 6.28 ms), 128 slower (6.59: the write on 128 CUs)
+    PREP_CUS = 96
 
     def _overlap_streams(self):
         """(prep stream, write stream) of pipelined steps. With ``QKNIT_PREP_CUS`` = c > 0 (default
