@@ -933,6 +933,214 @@ __global__ __launch_bounds__(256, 2) void qk_gemm_glds_kernel(GemmArgs g) {
 }
 
 // ------------------------------------------------------------------------------------------
+// knit contraction, wave-private LDS ring (full tiles, K = 4 * NKS, beta = 0)
+// ------------------------------------------------------------------------------------------
+// No barrier: each wave streams its own 64-row A slice and 64-column B slice of the k-step into
+// its own LDS ring (global_load_lds_dwordx4, DW k-steps deep), so the four waves of a workgroup
+// never wait for each other and a wave in its store epilogue leaves the SIMD's matrix pipe to its
+// partner (the shared-ring kernel above stalls every wave at each stage's barrier). The price is
+// that the two waves of a tile row both fetch its A slice (L2 traffic, not HBM).
+// Fragment rows are permuted so every LDS read is a conflict-free ds_read_b128: MFMA fragment i
+// holds tile rows m = 4 rho + i (rho: the A operand's row, lane & 15), fragment j of B holds
+// columns n = 2 rho + (j & 1) + 32 (j >> 1). In the C layout (row rho_r = (lane >> 4) + 4 r,
+// column rho) a lane then holds output columns n, n + 1 of fragments 2 jp, 2 jp + 1: one 16-B
+// store per (i, r, jp), no lane swap. The tile's 64 row and 64 column keys ride in the ring as
+// one more global_load_lds. Waits are counted by hand (the compiler does not count the stores
+// in flight and would wait for them at every tile start): see the vmcnt comment in the loop.
+#ifndef QK_GEMM_WAVE
+#define QK_GEMM_WAVE 1  // K in {16, 32, 64} full-tile contractions take the wave-ring kernel
+#endif
+#ifndef QK_WAVE_WG_PER_CU
+#define QK_WAVE_WG_PER_CU 2  // LDS: 4 waves x (4 x 4 KiB ring + 1 KiB keys) = 68 KiB per workgroup
+#endif
+constexpr int DW = 4;  // ring depth in k-steps (DW - 1 in flight while one is read)
+
+struct WaveRing {
+    double a[DW][4][64];  // k-step slot: 4 k-rows of the wave's 64 A columns (chunk-permuted)
+    double b[DW][4][64];  // 4 k-rows of its 64 B columns
+    int64_t key[2][64];   // row keys, column keys of the wave's 64 x 64 block
+};
+
+__device__ __forceinline__ void glds16_at(const void* src, void* lds_base) {
+    __builtin_amdgcn_global_load_lds(src,
+                                     reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                         reinterpret_cast<uintptr_t>(lds_base)),
+                                     16, 0, 0);
+}
+
+template <int NKS>
+__global__ __launch_bounds__(256, 2) void qk_gemm_wave_kernel(GemmArgs g) {
+    __shared__ __attribute__((aligned(16))) WaveRing rings[4];
+    if (gemm_skipped(g)) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    WaveRing& ring = rings[__builtin_amdgcn_readfirstlane(wave)];
+    const int64_t nblk = g.tiles_m * g.tiles_n;
+    const int64_t G = gridDim.x;
+    const bool xcd = nblk % 8 == 0 && G % 8 == 0;
+    const int64_t per_xcd = xcd ? nblk / 8 : nblk, stride = xcd ? G / 8 : G;
+    const int64_t base = xcd ? (blockIdx.x % 8) * per_xcd : 0;
+    int64_t li = xcd ? blockIdx.x / 8 : blockIdx.x;
+    if (li >= per_xcd) return;
+    const int64_t lda = g.lda, ldb = g.ldb;
+    // load side: lane t carries k-row (t >> 5) (+2 in the second load) and 16-B chunk position
+    // p = t & 31 of it; A positions hold chunks 0, 2, .., 30, 1, 3, .., 31 (so a lane's two reads
+    // are chunks 2 rho and 2 rho + 1), B positions the chunks in order
+    const int p = lane & 31;
+    const int chunkA = p < 16 ? 2 * p : 2 * (p - 16) + 1;
+    const int64_t offA = (int64_t)(lane >> 5) * lda + wm * 64 + 2 * chunkA;
+    const int64_t offB = (int64_t)(lane >> 5) * ldb + wn * 64 + 2 * p;
+    // key load: lanes 0-31 two row keys each, lanes 32-63 two column keys (an unkeyed side reads
+    // an in-bounds dummy and its keys are computed at the store)
+    const int64_t* tabA = g.keyA ? g.keyA : reinterpret_cast<const int64_t*>(g.A);
+    const int64_t* tabB = g.keyB ? g.keyB : reinterpret_cast<const int64_t*>(g.B);
+    const int64_t keyOff = 2 * (lane & 31);
+
+    int64_t bm, bn;
+    gemm_tile_coords(base + li, g.tiles_m, g.tiles_n, bm, bn);
+    const double* pa = g.A + bm * GT + offA;
+    const double* pb = g.B + bn * GT + offB;
+    const double* na = pa;
+    const double* nb = pb;
+    if (li + stride < per_xcd) {
+        int64_t tbm, tbn;
+        gemm_tile_coords(base + li + stride, g.tiles_m, g.tiles_n, tbm, tbn);
+        na = g.A + tbm * GT + offA;
+        nb = g.B + tbn * GT + offB;
+    }
+    // k-step ks of this tile into ring slot `slot` (ks >= NKS: the next tile's; the last tile's
+    // overrun re-reads its own first k-steps: in bounds, never read back). Four VMEM ops.
+    auto issue = [&](int slot, int ks) {
+        const double* a = ks < NKS ? pa + (int64_t)(4 * ks) * lda : na + (int64_t)(4 * (ks - NKS)) * lda;
+        const double* b = ks < NKS ? pb + (int64_t)(4 * ks) * ldb : nb + (int64_t)(4 * (ks - NKS)) * ldb;
+        glds16_at(a, &ring.a[slot][0][0]);
+        glds16_at(a + 2 * lda, &ring.a[slot][2][0]);
+        glds16_at(b, &ring.b[slot][0][0]);
+        glds16_at(b + 2 * ldb, &ring.b[slot][2][0]);
+    };
+#pragma unroll
+    for (int s = 0; s < DW - 1; ++s) issue(s, s);
+
+    // stores of the previous tile's epilogue still counted by vmcnt at this tile's first k-steps
+    int prev_stores = 0;
+    const int rho = lane & 15, kk = lane >> 4;
+    auto tile = [&]() -> bool {
+        d4_t acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = (d4_t){0.0, 0.0, 0.0, 0.0};
+        static_assert(NKS % DW == 0, "k-steps per tile must be a multiple of the ring depth");
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            issue((ks + DW - 1) % DW, ks + DW - 1);
+            if (ks == 0) {
+                const int64_t* t = lane < 32 ? tabA + (g.keyA ? bm * GT + wm * 64 : 0) + keyOff
+                                             : tabB + (g.keyB ? bn * GT + wn * 64 : 0) + keyOff;
+                glds16_at(t, &ring.key[0][0]);
+            }
+            // vmcnt: VMEM ops of this wave issued after slot ks's four: the later slots still
+            // in flight, this k-step's refill, the key load (issued at k-step 0 after slot 3's
+            // refill) and, for the slots filled during the previous tile, its epilogue stores
+            //   ks = 0, 1, 2: 13 + prev_stores; ks = 3: 13; ks >= 4: 12 (DW = 4)
+            static_assert(DW == 4, "wait counts below are for a 4-deep ring");
+            if (ks <= DW - 2) {  // 13 + 0 / 32 / 64 (clamped to the field's 63: waits longer, safe)
+                if (prev_stores == 0) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+                else if (prev_stores == 32) asm volatile("s_waitcnt vmcnt(45)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+            } else if (ks == DW - 1) {
+                asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            }
+            const int s = ks % DW;
+            const d2_t a0 = *reinterpret_cast<const d2_t*>(&ring.a[s][kk][2 * rho]);
+            const d2_t a1 = *reinterpret_cast<const d2_t*>(&ring.a[s][kk][32 + 2 * rho]);
+            const d2_t b0 = *reinterpret_cast<const d2_t*>(&ring.b[s][kk][2 * rho]);
+            const d2_t b1 = *reinterpret_cast<const d2_t*>(&ring.b[s][kk][32 + 2 * rho]);
+            const double fa[4] = {a0.x, a0.y, a1.x, a1.y};
+            const double fb[4] = {b0.x, b0.y, b1.x, b1.y};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            // the next k-step's refill overwrites this slot's neighbour: keep program order
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // keys: issued at k-step 0, followed by 4 (NKS - 1) refills
+        static_assert(4 * (NKS - 1) <= 63, "vmcnt field");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NKS - 1)) : "memory");
+        const int64_t* keyR = &ring.key[0][0];  // row keys: [0, 64)
+        const int64_t* keyC = &ring.key[0][0] + 64;
+        // lane's rows m = 4 kk + 16 r + i, columns c_j = 2 rho + (j & 1) + 32 (j >> 1)
+        int64_t kr[4][4], kc[4];
+        if (g.keyA) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) kr[r][i] = keyR[4 * kk + 16 * r + i];
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) kr[r][i] = (bm * GT + wm * 64 + 4 * kk + 16 * r + i) * g.strideA;
+        }
+        if (g.keyB) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) kc[j] = keyC[2 * rho + (j & 1) + 32 * (j >> 1)];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) kc[j] = (bn * GT + wn * 64 + 2 * rho + (j & 1) + 32 * (j >> 1)) * g.strideB;
+        }
+        int64_t odd = (kc[0] | kc[2]) & 1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) odd |= kr[r][i] & 1;
+        // wave-uniform; out is 16-B aligned (host)
+        const bool pair = __all(kc[1] == kc[0] + 1 && kc[3] == kc[2] + 1 && odd == 0);
+        if (pair) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int jp = 0; jp < 2; ++jp) {
+                        d2_t v;
+                        v.x = acc[i][2 * jp][r];
+                        v.y = acc[i][2 * jp + 1][r];
+                        gemm_store_pair(g.out + kr[r][i] + kc[2 * jp], v);
+                    }
+            prev_stores = 32;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) gemm_store_out(g.out + kr[r][i] + kc[j], acc[i][j][r]);
+            prev_stores = 64;
+        }
+        li += stride;
+        if (li >= per_xcd) return false;
+        gemm_tile_coords(base + li, g.tiles_m, g.tiles_n, bm, bn);
+        pa = na;
+        pb = nb;
+        if (li + stride < per_xcd) {
+            int64_t tbm, tbn;
+            gemm_tile_coords(base + li + stride, g.tiles_m, g.tiles_n, tbm, tbn);
+            na = g.A + tbm * GT + offA;
+            nb = g.B + tbn * GT + offB;
+        }
+        return true;
+    };
+    while (tile()) {
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the overrun refills land before the wave ends
+}
+
+// ------------------------------------------------------------------------------------------
 // small-K contraction (K <= 8): output-write bound — syc 32 1's uncut knit is a K = 1 outer
 // product that writes 34 GB from 1 MB of operands. A workgroup takes one output row at a time:
 // the row's K values of A are read once (wave-uniform), each lane forms two adjacent outputs from
@@ -1447,6 +1655,19 @@ int qk_gemm_keyed_pred(qk_ctx* ctx, int64_t M, int64_t N, int64_t K, const doubl
         const int cus = ctx->cus;
         const int64_t G = M < (int64_t)cus * 8 ? M : (int64_t)cus * 8;
         hipLaunchKernelGGL(qk_gemm_smallk_kernel<false>, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
+        QK_HIP(ctx, hipGetLastError());
+        return QK_OK;
+    }
+    if (QK_GEMM_WAVE && !beta && M % GT == 0 && N % GT == 0 && (K == 16 || K == 32 || K == 64) && aligned16 &&
+        ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(keyA) | reinterpret_cast<uintptr_t>(keyB)) &
+         15) == 0) {
+        const int cus = ctx->cus;
+        int64_t G = (int64_t)cus * QK_WAVE_WG_PER_CU;
+        G = G < 8 ? 8 : G - G % 8;
+        if (G > nblk) G = nblk;
+        if (K == 16) hipLaunchKernelGGL(qk_gemm_wave_kernel<4>, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
+        else if (K == 32) hipLaunchKernelGGL(qk_gemm_wave_kernel<8>, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
+        else hipLaunchKernelGGL(qk_gemm_wave_kernel<16>, dim3((unsigned)G), dim3(256), 0, ctx->stream, g);
         QK_HIP(ctx, hipGetLastError());
         return QK_OK;
     }

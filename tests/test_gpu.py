@@ -50,24 +50,36 @@ def test_gemm_keyed_matches_numpy(T):
 @pytest.mark.parametrize("K,M,N,keyed", [
     (16, 128, 128, False), (16, 4096, 4096, False), (32, 4096, 4096, True), (272, 4096, 2048, False),
     (48, 8192, 1024, True), (256, 1024, 8192, False), (8, 4096, 4096, True),  # K % 16: register kernel
+    (64, 128, 256, False), (64, 8192, 8192, False), (64, 2048, 4096, True), (32, 1024, 2048, False),
+    (64, 4096, 2048, "odd"), (64, 8192, 4096, "rowkeys"),
 ])
 def test_gemm_keyed_full_tile_pipeline_matches_torch(T, K, M, N, keyed):
-    """Full-tile shapes take the LDS-DMA ring kernel (qk_gemm_glds_kernel): one or several tiles
-    per workgroup, stage rings that wrap across tile ends (K = 16: an epilogue every stage), the
-    paired-store and (transposing keys) the per-element epilogue, against torch's fp64 GEMM."""
+    """Full-tile shapes take the LDS-DMA kernels: K in {16, 32, 64} the wave-private ring
+    (qk_gemm_wave_kernel), other multiples of 16 the shared ring (qk_gemm_glds_kernel). One or
+    several tiles per workgroup, rings that wrap across tile ends, the paired-store epilogue, the
+    per-element epilogue (transposing keys; odd output offsets that break 16-B pairs) and keyed
+    rows with paired columns, against torch's fp64 GEMM."""
     ctx = engine.get_context(0)
     g = T.Generator(device="cuda").manual_seed(K + M + N)
     A = T.randn(K, M, dtype=T.float64, device="cuda", generator=g)
     B = T.randn(K, N, dtype=T.float64, device="cuda", generator=g)
     ref = A.T @ B
-    out = T.full((M * N,), float("nan"), dtype=T.float64, device="cuda")
-    if keyed:  # out[j * M + i]: column keys step by M, so no paired stores
+    out = T.full((M * N + 2,), float("nan"), dtype=T.float64, device="cuda")
+    if keyed == "odd":  # out[1 + i * N + j]: every pair start odd -> per-element stores
+        engine.gemm_keyed(ctx, A, B, keyA=T.arange(M, dtype=T.int64, device="cuda") * N + 1,
+                          keyB=T.arange(N, dtype=T.int64, device="cuda"), out=out)
+        got = out[1:1 + M * N].view(M, N)
+    elif keyed == "rowkeys":  # rows reversed through keys, columns paired
+        rows = T.arange(M, dtype=T.int64, device="cuda").flip(0) * N
+        engine.gemm_keyed(ctx, A, B, keyA=rows, keyB=T.arange(N, dtype=T.int64, device="cuda"), out=out)
+        got = out[:M * N].view(M, N).flip(0)
+    elif keyed:  # out[j * M + i]: column keys step by M, so no paired stores
         engine.gemm_keyed(ctx, A, B, keyA=T.arange(M, dtype=T.int64, device="cuda"),
                           keyB=T.arange(N, dtype=T.int64, device="cuda") * M, out=out)
-        got = out.view(N, M).T
+        got = out[:M * N].view(N, M).T
     else:
         engine.gemm_keyed(ctx, A, B, out=out, strideA=N)
-        got = out.view(M, N)
+        got = out[:M * N].view(M, N)
     T.cuda.synchronize()
     err = float((got - ref).abs().max())
     assert err <= 1e-12 * K, err
