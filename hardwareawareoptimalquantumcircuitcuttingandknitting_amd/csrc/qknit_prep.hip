@@ -60,7 +60,12 @@ struct PrepArgs {
 // global -> LDS by global_load_lds (16 B per lane, no staging VGPRs); PNS stages in flight per
 // workgroup (2 x 28.7 KiB) and two workgroups per CU cover the HBM latency. The ring and the X tile
 // share the LDS (66.5 KiB per workgroup).
-constexpr int PRS = 16;          // instance rows per stage (4 MFMA k-steps)
+#ifndef QK_PREP_RS
+#define QK_PREP_RS 16
+#endif
+constexpr int PRS = QK_PREP_RS;  // instance rows per stage (PRS / 4 MFMA k-steps; PRS / 8 rows loaded per wave)
+constexpr int PRPW = PRS / 8;
+static_assert(PRS % 8 == 0 && PRS >= 8, "stage rows: a multiple of 8 (8 waves)");
 // tools/prep_bench.py, syc 32 5 shapes: 2 stages x 2 workgroups per CU 134 us; 1 workgroup per CU with
 // 3 / 4 / 5 stages 167 / 160 / 160 us (the wider ring does not help: latency hiding needs more waves)
 #ifndef QK_PREP_NS
@@ -68,6 +73,9 @@ constexpr int PRS = 16;          // instance rows per stage (4 MFMA k-steps)
 #endif
 #ifndef QK_PREP_WG_PER_CU
 #define QK_PREP_WG_PER_CU 2  // 512-thread workgroups per CU (2 needs QK_PREP_NS <= 2: the LDS)
+#endif
+#ifndef QK_PREP_EXP
+#define QK_PREP_EXP 0  // tools/ timing experiments only: 1 skips the Gram phase, 2 the X store, 4 the transform
 #endif
 constexpr int PNS = QK_PREP_NS;  // stages in flight
 constexpr int QLD = PCT + 16;    // q stage row stride (doubles): rows 32 banks apart, a k-step's reads conflict-free
@@ -98,7 +106,7 @@ __device__ __forceinline__ void prep_vmwait(int n) {
     }
 }
 
-__global__ __launch_bounds__(PTH, QK_PREP_WG_PER_CU) void qk_prep_operands_kernel(PrepArgs a) {
+__global__ __launch_bounds__(PTH, 2 * QK_PREP_WG_PER_CU) void qk_prep_operands_kernel(PrepArgs a) {
     __shared__ __attribute__((aligned(16))) PrepLds L;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, l4 = lane >> 4;
@@ -113,15 +121,15 @@ __global__ __launch_bounds__(PTH, QK_PREP_WG_PER_CU) void qk_prep_operands_kerne
         d4_t g0 = {0, 0, 0, 0}, g1 = {0, 0, 0, 0}, u = {0, 0, 0, 0};
         for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
             const int64_t c0 = t * PCT;
-            // stage loads: this wave moves q rows 2w, 2w+1 (one 1-KiB wave-instruction each) and Wt
-            // rows 2w, 2w+1 (lanes < K/2: 16 B each); rows >= R are not loaded (masked at use)
+            // stage loads: this wave moves q rows PRPW w + h (one 1-KiB wave-instruction each) and the
+            // same Wt rows (lanes < K/2: 16 B each); rows >= R are not loaded (masked at use)
             int nload[PNS];  // loads this wave issued per ring slot (for the vmcnt accounting)
             auto issue = [&](int st) {
                 PrepStage& P = L.st[st % PNS];
                 int n = 0;
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int rl = 2 * wave_s + h, r = st * PRS + rl;
+                for (int h = 0; h < PRPW; ++h) {
+                    const int rl = PRPW * wave_s + h, r = st * PRS + rl;
                     if (r < R) {
                         prep_glds(S.q + (int64_t)r * S.ldq + c0 + 2 * lane, &P.q[rl][0]);
                         ++n;
@@ -131,65 +139,98 @@ __global__ __launch_bounds__(PTH, QK_PREP_WG_PER_CU) void qk_prep_operands_kerne
                 }
                 nload[st % PNS] = n;
             };
-            __syncthreads();  // the previous tile's X readers are done with the LDS
+            // the previous tile's X readers are done with the LDS (bare barrier: a __syncthreads()
+            // would wait for the previous tile's X stores as well)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
             for (int st = 0; st < PNS - 1 && st < nst; ++st) issue(st);
             d4_t x[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) x[i] = (d4_t){0, 0, 0, 0};
-            for (int st = 0; st < nst; ++st) {
+            for (int st = 0; st < ((QK_PREP_EXP & 4) ? 0 : nst); ++st) {
                 int after = 0;  // loads of this wave issued after stage st's
                 for (int d = st + 1; d < st + PNS - 1 && d < nst; ++d) after += nload[d % PNS];
                 prep_vmwait(after);
-                __syncthreads();  // stage st landed for every wave; stage st - 1 fully read
-                if (st + PNS - 1 < nst) issue(st + PNS - 1);
+                // stage st landed for every wave; stage st - 1 fully read. A bare s_barrier: the
+                // release fence of __syncthreads() makes the compiler wait vmcnt(0) — for the
+                // prefetched stages too — which serialised every stage's loads (round 3)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                // this stage's fragments into registers BEFORE the refill is issued: an LDS read
+                // after a global_load_lds makes the compiler wait for that load (vmcnt(0)), which
+                // serialised every refill with the stage's MFMAs (round 3)
                 const PrepStage& P = L.st[st % PNS];
+                double qb[PRS / 4], wa[PRS / 4][4];
 #pragma unroll
                 for (int kk = 0; kk < PRS / 4; ++kk) {
                     const int rl = 4 * kk + l4;
                     const bool rv = st * PRS + rl < R;
-                    const double qb = rv ? P.q[rl][16 * wave + l16] : 0.0;
+                    qb[kk] = rv ? P.q[rl][16 * wave + l16] : 0.0;
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int k = 16 * i + l16;
-                        const double wa = (rv && k < K) ? P.w[rl][k] : 0.0;
-                        x[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa, qb, x[i], 0, 0, 0);
+                        wa[kk][i] = (rv && k < K) ? P.w[rl][k] : 0.0;
                     }
                 }
+                if (st + PNS - 1 < nst) issue(st + PNS - 1);
+#pragma unroll
+                for (int kk = 0; kk < PRS / 4; ++kk)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[kk][i], qb[kk], x[i], 0, 0, 0);
             }
-            __syncthreads();  // every wave is done with the ring: the X tile takes its place
+            // probe columns of the tile (B side, waves 0-3): software-pipelined batches of PPB loads,
+            // the first batch in flight across the X tile's LDS write (round 2 loaded one per k-step,
+            // each waited for at once: 32 dependent global loads per tile)
+            const bool probes = S.P != nullptr && wave < 4;
+            constexpr int PPB = 8;
+            const double* pp = probes ? S.P + (int64_t)l16 * S.N + c0 + l4 : nullptr;
+            double pxn[PPB];
+#pragma unroll
+            for (int j = 0; j < PPB; ++j) pxn[j] = probes ? pp[4 * j] : 0.0;
+            // bare barriers (no vmcnt(0): the probe batch stays in flight); every stage's LDS-DMA
+            // landed at the last stage's wait
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // every wave is done with the ring: the X tile takes its place
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) L.x[16 * i + l4 + 4 * rr][16 * wave + l16] = x[i][rr];
-            __syncthreads();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
             // ---- Gram blocks and (B side) probe products over the tile's 128 columns
-            const bool probes = S.P != nullptr && wave < 4;
-#pragma unroll 4
-            for (int s4 = 0; s4 < PCT / 4; ++s4) {
-                const int c = 4 * s4 + l4;
-                const double av = L.x[16 * bi + l16][c];
-                const double b0 = L.x[16 * bj0 + l16][c];
-                const double b1 = L.x[16 * (bj0 + 1) + l16][c];
-                g0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0, g0, 0, 0, 0);
-                g1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b1, g1, 0, 0, 0);
-                if (probes) {  // wave-uniform; waves 0-3: bi == wave
-                    const double px = S.P[(int64_t)l16 * S.N + c0 + c];
-                    u = __builtin_amdgcn_mfma_f64_16x16x4f64(av, px, u, 0, 0, 0);
-                }
-            }
-            // ---- X tile to HBM: row tid >> 3, 16 columns per thread (8 x 16-B stores)
-            const int row = tid >> 3, col = (tid & 7) * 16;
-            if (row < K) {
-                double* dst = S.X + (int64_t)row * S.N + c0 + col;
+            for (int s8 = 0; s8 < ((QK_PREP_EXP & 1) ? 0 : PCT / 4); s8 += PPB) {
+                double px[PPB];
 #pragma unroll
-                for (int v = 0; v < 8; ++v) {
-                    d2_t z;
-                    z.x = L.x[row][col + 2 * v];
-                    z.y = L.x[row][col + 2 * v + 1];
-                    *reinterpret_cast<d2_t*>(dst + 2 * v) = z;
+                for (int j = 0; j < PPB; ++j) px[j] = pxn[j];
+                if (probes && s8 + PPB < PCT / 4) {
+#pragma unroll
+                    for (int j = 0; j < PPB; ++j) pxn[j] = pp[4 * (s8 + PPB + j)];
+                }
+#pragma unroll
+                for (int j = 0; j < PPB; ++j) {
+                    const int c = 4 * (s8 + j) + l4;
+                    const double av = L.x[16 * bi + l16][c];
+                    const double b0 = L.x[16 * bj0 + l16][c];
+                    const double b1 = L.x[16 * (bj0 + 1) + l16][c];
+                    g0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0, g0, 0, 0, 0);
+                    g1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b1, g1, 0, 0, 0);
+                    if (probes) u = __builtin_amdgcn_mfma_f64_16x16x4f64(av, px[j], u, 0, 0, 0);  // waves 0-3: bi == wave
                 }
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's load accounting starts at 0
+            // ---- X tile to HBM: wave w stores rows 8w .. 8w+7, one contiguous 1-KiB row per
+            // wave-instruction (16 B per lane). Round 2 gave each thread 16 consecutive columns of one
+            // row — every store instruction scattered 64 x 16 B at a 128-B stride — and then waited
+            // for the stores (vmcnt(0)); the two cost 30 of the kernel's 126 us (tools/prep_bench.py)
+            if (!(QK_PREP_EXP & 2)) {
+                d2_t z[8];  // all eight rows read first: distinct registers, no store-data waits
+#pragma unroll
+                for (int v = 0; v < 8; ++v) z[v] = *reinterpret_cast<const d2_t*>(&L.x[8 * wave_s + v][2 * lane]);
+#pragma unroll
+                for (int v = 0; v < 8; ++v)
+                    if (8 * wave_s + v < K) *reinterpret_cast<d2_t*>(S.X + (int64_t)(8 * wave_s + v) * S.N + c0 + 2 * lane) = z[v];
+            }
+            // no vmcnt(0) here: the stores are older than every load of the next tile, and vector
+            // memory operations complete in issue order, so the next tile's counted waits cover them
         }
         // ---- this workgroup's partial sums (zero if it took no tile)
         double* p = a.part + ((int64_t)sd * gridDim.x + blockIdx.x) * PPART;
@@ -250,10 +291,11 @@ __global__ __launch_bounds__(64 * PRW) void qk_prep_reduce_kernel(const double* 
     }
 }
 
-// out[j][c] = sum_k T[j][k] X[k][c] for j < rmax, both sides (blockIdx.y). A workgroup takes 64 columns;
-// its four waves split K in quarters (16 rows each: every load of a thread in flight at once) and sum
-// their partial products through LDS in a fixed order. 31 us for syc 32 5's two 64 x 2^16 operands (72 MB:
-// ~2.3 TB/s, linear in the column count); two columns per lane with 16-B loads measured slower (35 us)
+// out[j][c] = sum_k T[j][k] X[k][c] for j < rmax, both sides (blockIdx.y). A workgroup takes 64 columns
+// per iteration; its four waves split K in quarters (16 rows each: every load of a thread in flight at
+// once) and sum their partial products through LDS in a fixed order. Round 3: the X loads are issued
+// before T is staged, and the grid is one 64-column block per workgroup (4 per CU per side: every
+// load of the kernel in flight at once, no second round trip)
 __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const double* __restrict__ TA,
                                                           const double* __restrict__ XA, int64_t NA,
                                                           double* __restrict__ A2, const double* __restrict__ TB,
@@ -266,23 +308,28 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
     const double* X = bs ? XB : XA;
     double* out = bs ? B2 : A2;
     const int64_t N = bs ? NB : NA;
-    const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
-    {  // T (at most 8 x 64): both loads of a thread in flight together (a load-wait loop here cost a
-       // memory latency per iteration in every workgroup)
+    const int l = threadIdx.x & 63;
+    const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR row bases
+    auto load = [&](int64_t c0, double (&xv)[16]) {
+        const int64_t c = c0 + l;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int k = 16 * q + u;
+            const double* row = X + (int64_t)k * N;  // uniform
+            xv[u] = (k < K && c < N) ? row[c] : 0.0;
+        }
+    };
+    double xv[16];
+    int64_t c0 = (int64_t)blockIdx.x * 64;
+    if (c0 < N) load(c0, xv);  // in flight while T is staged
+    {  // T (at most 8 x 64): both loads of a thread in flight together
         const int n = rmax * K, e0 = threadIdx.x, e1 = threadIdx.x + 256;
         const double t0 = e0 < n ? Tg[e0] : 0.0, t1 = e1 < n ? Tg[e1] : 0.0;
         if (e0 < n) T[e0 / K][e0 % K] = t0;
         if (e1 < n) T[e1 / K][e1 % K] = t1;
     }
     __syncthreads();
-    for (int64_t c0 = (int64_t)blockIdx.x * 64; c0 < N; c0 += (int64_t)gridDim.x * 64) {
-        const int64_t c = c0 + l;
-        double xv[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int k = 16 * q + u;
-            xv[u] = (k < K && c < N) ? X[(int64_t)k * N + c] : 0.0;
-        }
+    for (; c0 < N; c0 += (int64_t)gridDim.x * 64) {
         double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int u = 0; u < 16; ++u)
@@ -298,10 +345,12 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
                 out[(int64_t)j * N + c0 + cc] = (part[0][j][cc] + part[1][j][cc]) + (part[2][j][cc] + part[3][j][cc]);
         }
         __syncthreads();
+        if (c0 + (int64_t)gridDim.x * 64 < N) load(c0 + (int64_t)gridDim.x * 64, xv);
     }
 }
 
-constexpr int PV_GRID = 64;  // workgroups of the V = B'' P^T partial sums (probe_d sums their partials)
+constexpr int PV_GRID = 128;  // workgroups of the V = B'' P^T partial sums (probe_d sums their partials)
+constexpr int PV_PART = 8 * 16;  // doubles per V partial: rows j < 8 (rmax <= 8), 16 probes
 
 // V partials: vpart[b][j][p] = sum over this workgroup's columns c of B2[j][c] P[p][c] (j < rmax), on the
 // VALU: a lane takes one column per iteration (every load a coalesced 512-B row segment), wave w the
@@ -339,17 +388,17 @@ __global__ __launch_bounds__(256) void qk_probe_v_kernel(int rmax, const double*
             for (int s = 1; s < 64; s <<= 1) v += __shfl_xor(v, s, 64);
             acc[jj][q] = v;
         }
-    // vpart layout [b][j][p] with j < 16 (rows >= rmax zero): lane j16 * 4 + q of wave w writes (j16, 4w + q)
-    double* out = vpart + (int64_t)blockIdx.x * 256;
-    if (lane < 64) {
-        const int j16 = lane >> 2, q = lane & 3;
+    // vpart layout [b][j][p], j < 8 (rows >= rmax zero): lane j * 4 + q (< 32) of wave w writes (j, 4w + q)
+    double* out = vpart + (int64_t)blockIdx.x * PV_PART;
+    if (lane < 32) {
+        const int j8 = lane >> 2, q = lane & 3;
         double v = 0.0;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj)
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq)
-                if (jj == j16 && qq == q) v = acc[jj][qq];
-        out[j16 * 16 + 4 * wave + q] = v;
+                if (jj == j8 && qq == q) v = acc[jj][qq];
+        out[j8 * 16 + 4 * wave + q] = v;
     }
 }
 
@@ -363,14 +412,16 @@ __global__ __launch_bounds__(256) void qk_probe_d_kernel(int K, int rmax, const 
     __shared__ double Vs[16][PNP];
     __shared__ double ep[4][2 * PNP];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, l4 = lane >> 4;
-    {
+    if (tid < PV_PART) {  // V rows 0..7 (fixed-order fold of the partials); rows 8..15 stay zero
         double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         int b = 0;
         for (; b + 8 <= gv; b += 8)
 #pragma unroll
-            for (int u = 0; u < 8; ++u) t[u] += vpart[(int64_t)(b + u) * 256 + tid];
-        for (; b < gv; ++b) t[0] += vpart[(int64_t)b * 256 + tid];
+            for (int u = 0; u < 8; ++u) t[u] += vpart[(int64_t)(b + u) * PV_PART + tid];
+        for (; b < gv; ++b) t[0] += vpart[(int64_t)b * PV_PART + tid];
         Vs[tid / 16][tid % 16] = -(((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7])));
+    } else {
+        Vs[tid / 16][tid % 16] = 0.0;
     }
     for (int e = tid; e < PK * PNP; e += 256) Us[e / PNP][e % PNP] = (e / PNP) < K ? U[e] : 0.0;
     __syncthreads();
@@ -517,7 +568,7 @@ int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const d
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_compress_operands: hipSetDevice");
     const int64_t N = NA > NB ? NA : NB;
     int64_t gx = (N + 63) / 64;
-    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 2;  // x 2 sides: 4 workgroups per CU
+    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 4;  // x 2 sides: up to 8 workgroups per CU
     gx = gx < cap ? gx : cap;
     hipLaunchKernelGGL(qk_compress_kernel, dim3((unsigned)gx, 2), dim3(256), 0, ctx->stream, K, rmax, TA, XA, NA, A2,
                        TB, XB, NB, B2);
@@ -529,7 +580,7 @@ int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const d
 
 int qk_probe_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t* bytes) {
     if (!ctx || !bytes) return QK_EARG;
-    *bytes = (int64_t)(PV_GRID * 256 + probe_grid_d(ctx, NA) * PE) * (int64_t)sizeof(double);
+    *bytes = (int64_t)(PV_GRID * PV_PART + probe_grid_d(ctx, NA) * PE) * (int64_t)sizeof(double);
     return QK_OK;
 }
 
@@ -544,11 +595,11 @@ int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx,
         return fail(ctx, QK_EARG, "qk_probe_errors: null buffer");
     if (ldx < NA || ldb2 < NB || ldp < NB) return fail(ctx, QK_EARG, "qk_probe_errors: leading dimension");
     const int gd = probe_grid_d(ctx, NA);
-    if (work_bytes < (int64_t)(PV_GRID * 256 + gd * PE) * (int64_t)sizeof(double))
+    if (work_bytes < (int64_t)(PV_GRID * PV_PART + gd * PE) * (int64_t)sizeof(double))
         return fail(ctx, QK_EARG, "qk_probe_errors: workspace too small (qk_probe_workspace_bytes)");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_probe_errors: hipSetDevice");
     double* vpart = work;
-    double* epart = work + PV_GRID * 256;
+    double* epart = work + PV_GRID * PV_PART;
     hipLaunchKernelGGL(qk_probe_v_kernel, dim3(PV_GRID), dim3(256), 0, ctx->stream, rmax, B2, ldb2, NB, probes, ldp,
                        vpart);
     hipLaunchKernelGGL(qk_probe_d_kernel, dim3(gd), dim3(256), 0, ctx->stream, K, rmax, XA, ldx, NA, A2, lda2, U, vpart,

@@ -63,3 +63,30 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def read_patterns(reps: int = 20):
+    """How fast can the [64, 2^16] operand be read at all? Sequential full-buffer reduction, the torch
+    (hipBLASLt) T @ X product the compress kernel computes, and a column-sum over the rows."""
+    import torch
+
+    g = torch.Generator(device="cuda").manual_seed(1)
+    X = torch.randn(64, 65536, dtype=torch.float64, device="cuda", generator=g)
+    T = torch.randn(8, 64, dtype=torch.float64, device="cuda", generator=g)
+    for name, fn in (("X.sum() (sequential 32 MB)", lambda: X.sum()),
+                     ("X.sum(dim=0) (column sums)", lambda: X.sum(dim=0)),
+                     ("torch.mm(T, X) [8,64]x[64,2^16]", lambda: torch.mm(T, X))):
+        fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) / reps * 1e3
+        print(f"{name:34s} {us:8.1f} us per call ({32 * 2**20 / us / 1e6:.2f} TB/s)", flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("QK_READ_PATTERNS"):
+    read_patterns()
