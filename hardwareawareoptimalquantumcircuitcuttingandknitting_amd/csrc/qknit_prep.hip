@@ -74,6 +74,9 @@ static_assert(PRS % 8 == 0 && PRS >= 8, "stage rows: a multiple of 8 (8 waves)")
 #ifndef QK_PREP_WG_PER_CU
 #define QK_PREP_WG_PER_CU 2  // 512-thread workgroups per CU (2 needs QK_PREP_NS <= 2: the LDS)
 #endif
+#ifndef QK_COMPRESS_COLS
+#define QK_COMPRESS_COLS 1  // qk_compress_cols_kernel where the shapes allow (0: the K-split kernel)
+#endif
 #ifndef QK_PREP_EXP
 #define QK_PREP_EXP 0  // tools/ timing experiments only: 1 skips the Gram phase, 2 the X store, 4 the transform
 #endif
@@ -349,6 +352,82 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
     }
 }
 
+// Column form (round 3, the default when N is even and the rows 16-B aligned): one wave per 128
+// columns, a lane takes two adjacent columns (16-B loads: every wave-instruction a contiguous 1-KiB row
+// segment) over all K rows, T read as wave-uniform (scalar) operands, no LDS and no cross-wave sum.
+// syc 32 5's two 64 x 2^16 operands are 1024 waves — one per SIMD — so each wave keeps its loads
+// in flight in 16-row chunks, the next chunk issued before the current one is summed.
+constexpr int PCW = 16;  // rows per load chunk
+__global__ __launch_bounds__(64) void qk_compress_cols_kernel(int K, int rmax, const double* __restrict__ TA,
+                                                              const double* __restrict__ XA, int64_t NA,
+                                                              double* __restrict__ A2, const double* __restrict__ TB,
+                                                              const double* __restrict__ XB, int64_t NB,
+                                                              double* __restrict__ B2) {
+    const bool bs = blockIdx.y == 1;
+    const double* Tg = bs ? TB : TA;
+    const double* X = bs ? XB : XA;
+    double* out = bs ? B2 : A2;
+    const int64_t N = bs ? NB : NA;
+    const int64_t c = ((int64_t)blockIdx.x * 64 + threadIdx.x) * 2;
+    if (c >= N) return;
+    d2_t acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = (d2_t){0.0, 0.0};
+    // T^T [PK][8] in LDS, zero beyond (K, rmax): the body is branch-free (rows k >= K re-read row K - 1
+    // times a zero coefficient) — uniform-condition scalar T loads became branches, and the compiler
+    // then waited vmcnt(0) at each of them
+    __shared__ __attribute__((aligned(16))) double Tt[PK][8];
+    d2_t buf[2][PCW];
+    auto load = [&](int ch, d2_t (&b)[PCW]) {
+#pragma unroll
+        for (int u = 0; u < PCW; ++u) {
+            const int k = min(ch * PCW + u, K - 1);
+            b[u] = *reinterpret_cast<const d2_t*>(X + (int64_t)k * N + c);
+        }
+    };
+    const int nch = (K + PCW - 1) / PCW;
+    {
+        // T first: loads complete in issue order, so its wait below does not wait for the X chunk
+        double tv[PK * 8 / 64];  // clamped indices: every load unconditional, all in flight together
+#pragma unroll
+        for (int i = 0; i < PK * 8 / 64; ++i) {
+            const int e = threadIdx.x + 64 * i, k = e >> 3, j = e & 7;
+            tv[i] = Tg[min(j, rmax - 1) * K + min(k, K - 1)];
+        }
+        load(0, buf[0]);
+#pragma unroll
+        for (int i = 0; i < PK * 8 / 64; ++i) {
+            const int e = threadIdx.x + 64 * i, k = e >> 3, j = e & 7;
+            Tt[k][j] = (k < K && j < rmax) ? tv[i] : 0.0;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ch = 0; ch < PK / PCW; ++ch) {
+        if (ch >= nch) break;
+        if (ch + 1 < nch) load(ch + 1, buf[(ch + 1) & 1]);
+#pragma unroll
+        for (int u = 0; u < PCW; ++u) {
+            const int k = ch * PCW + u;
+            double t[8];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const d2_t tv = *reinterpret_cast<const d2_t*>(&Tt[k][2 * h]);
+                t[2 * h] = tv.x;
+                t[2 * h + 1] = tv.y;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                acc[j].x = fma(t[j], buf[ch & 1][u].x, acc[j].x);
+                acc[j].y = fma(t[j], buf[ch & 1][u].y, acc[j].y);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (j < rmax) *reinterpret_cast<d2_t*>(out + (int64_t)j * N + c) = acc[j];
+}
+
 constexpr int PV_GRID = 128;  // workgroups of the V = B'' P^T partial sums (probe_d sums their partials)
 constexpr int PV_PART = 8 * 16;  // doubles per V partial: rows j < 8 (rmax <= 8), 16 probes
 
@@ -567,11 +646,19 @@ int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const d
     if (!TA || !XA || !A2 || !TB || !XB || !B2) return fail(ctx, QK_EARG, "qk_compress_operands: null buffer");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_compress_operands: hipSetDevice");
     const int64_t N = NA > NB ? NA : NB;
-    int64_t gx = (N + 63) / 64;
-    const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 4;  // x 2 sides: up to 8 workgroups per CU
-    gx = gx < cap ? gx : cap;
-    hipLaunchKernelGGL(qk_compress_kernel, dim3((unsigned)gx, 2), dim3(256), 0, ctx->stream, K, rmax, TA, XA, NA, A2,
-                       TB, XB, NB, B2);
+    const bool cols = QK_COMPRESS_COLS && NA % 2 == 0 && NB % 2 == 0 &&
+                      !((reinterpret_cast<uintptr_t>(XA) | reinterpret_cast<uintptr_t>(XB) |
+                         reinterpret_cast<uintptr_t>(A2) | reinterpret_cast<uintptr_t>(B2)) & 15);
+    if (cols) {
+        hipLaunchKernelGGL(qk_compress_cols_kernel, dim3((unsigned)((N + 127) / 128), 2), dim3(64), 0, ctx->stream, K,
+                           rmax, TA, XA, NA, A2, TB, XB, NB, B2);
+    } else {
+        int64_t gx = (N + 63) / 64;
+        const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 4;  // x 2 sides: up to 8 workgroups per CU
+        gx = gx < cap ? gx : cap;
+        hipLaunchKernelGGL(qk_compress_kernel, dim3((unsigned)gx, 2), dim3(256), 0, ctx->stream, K, rmax, TA, XA, NA,
+                           A2, TB, XB, NB, B2);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return fail(ctx, QK_EHIP, (std::string("qk_compress_operands: ") + hipGetErrorString(e)).c_str());
