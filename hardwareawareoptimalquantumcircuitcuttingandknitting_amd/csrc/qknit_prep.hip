@@ -439,6 +439,8 @@ constexpr int PV_PART = 8 * 16;  // doubles per V partial: rows j < 8 (rmax <= 8
 __global__ __launch_bounds__(256) void qk_probe_v_kernel(int rmax, const double* __restrict__ B2, int64_t ldb2,
                                                          int64_t NB, const double* __restrict__ P, int64_t ldp,
                                                          double* __restrict__ vpart) {
+    // loads are unconditional (rows >= rmax re-read row rmax - 1, zeroed at the end): conditional loads
+    // became branches with a vmcnt(0) wait each (round 3)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double acc[8][4];
 #pragma unroll
@@ -449,7 +451,7 @@ __global__ __launch_bounds__(256) void qk_probe_v_kernel(int rmax, const double*
     for (int64_t c = (int64_t)blockIdx.x * 64 + lane; c < NB; c += (int64_t)gridDim.x * 64) {
         double b[8], pv[4];
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) b[jj] = jj < rmax ? B2[(int64_t)jj * ldb2 + c] : 0.0;
+        for (int jj = 0; jj < 8; ++jj) b[jj] = B2[(int64_t)min(jj, rmax - 1) * ldb2 + c];
 #pragma unroll
         for (int q = 0; q < 4; ++q) pv[q] = P[(int64_t)(4 * wave + q) * ldp + c];
 #pragma unroll
@@ -465,7 +467,7 @@ __global__ __launch_bounds__(256) void qk_probe_v_kernel(int rmax, const double*
             double v = acc[jj][q];
 #pragma unroll
             for (int s = 1; s < 64; s <<= 1) v += __shfl_xor(v, s, 64);
-            acc[jj][q] = v;
+            acc[jj][q] = jj < rmax ? v : 0.0;
         }
     // vpart layout [b][j][p], j < 8 (rows >= rmax zero): lane j * 4 + q (< 32) of wave w writes (j, 4w + q)
     double* out = vpart + (int64_t)blockIdx.x * PV_PART;
@@ -491,16 +493,31 @@ __global__ __launch_bounds__(256) void qk_probe_d_kernel(int K, int rmax, const 
     __shared__ double Vs[16][PNP];
     __shared__ double ep[4][2 * PNP];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, l4 = lane >> 4;
-    if (tid < PV_PART) {  // V rows 0..7 (fixed-order fold of the partials); rows 8..15 stay zero
-        double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        int b = 0;
-        for (; b + 8 <= gv; b += 8)
+    {  // V rows 0..7, a fixed-order fold of the partials: thread t takes entry t % 128 over the partials
+       // b = t / 128 (mod 2), 16 loads in flight per batch (batches of 8 on half the threads took one
+       // memory latency each); rows 8..15 stay zero
+        __shared__ double vh[PV_PART];
+        const int e = tid & (PV_PART - 1), h = tid >> 7;
+        double t[16];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) t[u] += vpart[(int64_t)(b + u) * PV_PART + tid];
-        for (; b < gv; ++b) t[0] += vpart[(int64_t)b * PV_PART + tid];
-        Vs[tid / 16][tid % 16] = -(((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7])));
-    } else {
-        Vs[tid / 16][tid % 16] = 0.0;
+        for (int u = 0; u < 16; ++u) t[u] = 0.0;
+        int b = h;
+        for (; b + 30 < gv; b += 32) {
+            double v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = vpart[(int64_t)(b + 2 * u) * PV_PART + e];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) t[u] += v[u];
+        }
+        for (; b < gv; b += 2) t[0] += vpart[(int64_t)b * PV_PART + e];
+#pragma unroll
+        for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+            for (int u = 0; u < w; ++u) t[u] += t[u + w];
+        if (h == 1) vh[e] = t[0];
+        __syncthreads();
+        if (h == 0) Vs[e / 16][e % 16] = -(t[0] + vh[e]);
+        else Vs[8 + e / 16][e % 16] = 0.0;
     }
     for (int e = tid; e < PK * PNP; e += 256) Us[e / PNP][e % PNP] = (e / PNP) < K ? U[e] : 0.0;
     __syncthreads();
@@ -544,6 +561,7 @@ __global__ __launch_bounds__(256) void qk_probe_d_kernel(int K, int rmax, const 
 // itself (||R p|| ~ ||R||_F) above the absolute floor tol.
 // 256 threads: thread t sums rows b = t / 32, + 8, ... of entry t % 32, then a fixed-order LDS tree.
 constexpr int PE = 2 * PNP;
+
 __global__ __launch_bounds__(256) void qk_probe_accept_kernel(const double* __restrict__ epart, int n,
                                                               const int32_t* __restrict__ r_dev, double tol,
                                                               double rel_tol, double* __restrict__ e2_out,
