@@ -1323,15 +1323,6 @@ __global__ __launch_bounds__(256) void qk_knit_outer_stream_kernel(OuterStreamAr
 #ifndef QK_OB_NT
 #define QK_OB_NT 0
 #endif
-#ifndef QK_OB_ROT
-#define QK_OB_ROT 0
-#endif
-#ifndef QK_OB_EXP
-#define QK_OB_EXP 0
-#endif
-#ifndef QK_OB_NV
-#define QK_OB_NV 1
-#endif
 struct OuterBlockedArgs {
     int K, TB;
     const double* __restrict__ A;
@@ -1387,56 +1378,11 @@ __global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlocked
         __syncthreads();
         const double* Bg = a.B + bh;
         double* o = a.out + ((int64_t)base - a.o_begin);
-        // QK_OB_ROT (tuning): the workgroup starts its task at iteration (t * QK_OB_ROT) mod iters, so
-        // the resident workgroups, one 2^TB-output task each, do not all write the same offset of their
-        // power-of-two-strided tasks at once
-#if QK_OB_NV > 1
-        if (iters >= QK_OB_NV) {
-            // QK_OB_NV (tuning): each lane writes NV 16-B vectors per iteration, lane-interleaved over an
-            // NV-KiB run per wave (lane l: bytes 16 (NV l + v)), the pattern of a vectorised fill
-            constexpr int NV = QK_OB_NV;
-#pragma unroll 2
-            for (int it = 0; it < iters / NV; ++it) {
-                d2_t acc[NV];
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    const uint32_t off = (uint32_t)(512 * NV * it + 2 * (NV * threadIdx.x + v));
-                    const uint32_t row = tab[0][0][off & 255] + tab[0][1][(off >> 8) & 255];
-                    const uint32_t col = tab[1][0][off & 255] + tab[1][1][(off >> 8) & 255];
-                    acc[v] = (d2_t){0.0, 0.0};
-#if QK_OB_EXP & 1
-                    acc[v].x = (double)row;
-                    acc[v].y = (double)col;
-#else
-#pragma unroll
-                    for (int k = 0; k < SK_MAX; ++k)
-                        if (k < K) {
-                            const double av = sA[k * na + row];
-                            const d2_t bv = BG ? *reinterpret_cast<const d2_t*>(Bg + k * a.ldb + col)
-                                               : *reinterpret_cast<const d2_t*>(sB + k * nb + col);
-                            acc[v].x = fma(av, bv.x, acc[v].x);
-                            acc[v].y = fma(av, bv.y, acc[v].y);
-                        }
-#endif
-                }
-#pragma unroll
-                for (int v = 0; v < NV; ++v)
-                    *reinterpret_cast<d2_t*>(o + 512 * NV * it + 2 * (NV * threadIdx.x + v)) = acc[v];
-            }
-            continue;
-        }
-#endif
-        const int rot = (int)((t * QK_OB_ROT) & (iters - 1));
 #pragma unroll 4
-        for (int it0 = 0; it0 < iters; ++it0) {
-            const int it = (it0 + rot) & (iters - 1);
+        for (int it = 0; it < iters; ++it) {
             const uint32_t hi = (uint32_t)(2 * it + (threadIdx.x >> 7));  // byte 1 of the task offset
             const uint32_t row = r0 + tab[0][1][hi], col = c0 + tab[1][1][hi];
             d2_t acc = {0.0, 0.0};
-#if QK_OB_EXP & 1  // tuning only: stores without the operand reads (the store pattern's own rate)
-            acc.x = (double)row;
-            acc.y = (double)col;
-#else
 #pragma unroll
             for (int k = 0; k < SK_MAX; ++k)
                 if (k < K) {
@@ -1446,7 +1392,6 @@ __global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlocked
                     acc.x = fma(av, bv.x, acc.x);
                     acc.y = fma(av, bv.y, acc.y);
                 }
-#endif
 #if QK_OB_NT
             __builtin_nontemporal_store(acc, reinterpret_cast<d2_t*>(o + 512 * it + 2 * threadIdx.x));
 #else
@@ -1454,34 +1399,6 @@ __global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlocked
 #endif
         }
     }
-}
-
-// Chunk form (round 3 experiment, QKNIT_OB_CHUNK=1): no persistent grid and no LDS — one workgroup per
-// 512-output chunk, dispatched in output order, which is the store pattern a plain fill writes fastest
-// with (tools/fill_probe.hip: one 4-KiB chunk per workgroup 6.9-7.0 TB/s against 5.9-6.2 for 512-KiB
-// blocks per workgroup, the blocked kernel's pattern). pext(o, m) = pext(chunk base, m) (uniform) +
-// pext(lane offset, m & 511) (a lane's 9 low bits); operands come from L1 / L2 (2 x K x 2^16 doubles).
-__global__ __launch_bounds__(256) void qk_knit_outer_chunk_kernel(OuterBlockedArgs a) {
-    int K = a.K;
-    if (a.kdev) {
-        const int kd = *a.kdev;
-        if (kd <= 0) return;
-        K = kd < K ? kd : K;
-    }
-    const uint32_t o0 = (uint32_t)(a.task_begin * 512 + (int64_t)blockIdx.x * 512);  // absolute chunk base
-    const uint32_t ah = pext32(o0, a.maskA), bh = pext32(o0, a.maskB);               // uniform
-    const uint32_t lo = 2u * threadIdx.x;
-    const uint32_t ia = ah + pext32(lo, a.maskA & 511u), ib = bh + pext32(lo, a.maskB & 511u);
-    d2_t acc = {0.0, 0.0};
-#pragma unroll
-    for (int k = 0; k < SK_MAX; ++k)
-        if (k < K) {
-            const double av = a.A[k * a.lda + ia];
-            const d2_t bv = *reinterpret_cast<const d2_t*>(a.B + k * a.ldb + ib);
-            acc.x = fma(av, bv.x, acc.x);
-            acc.y = fma(av, bv.y, acc.y);
-        }
-    *reinterpret_cast<d2_t*>(a.out + ((int64_t)o0 - a.o_begin) + lo) = acc;
 }
 
 constexpr int64_t OB_STAGE_BYTES = 24 * 1024;  // LDS budget of the blocked kernel's operand stage
@@ -1831,14 +1748,6 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
     const int align = __builtin_ctzll((uint64_t)(o_begin | o_count));
     bool bg = false;
     const int tb = outer_blocked_tile(nbits, K, maskA, maskB, align, &bg);
-    static const int chunk_form = getenv("QKNIT_OB_CHUNK") ? atoi(getenv("QKNIT_OB_CHUNK")) : 0;
-    if (chunk_form && tb && nbits <= 32 && (o_count % 512) == 0 && (o_begin % 512) == 0) {
-        OuterBlockedArgs b{(int)K, 9, A, lda, B, ldb, (uint32_t)maskA, (uint32_t)maskB, o_begin >> 9,
-                           (o_begin + o_count) >> 9, o_begin, k_dev, out};
-        hipLaunchKernelGGL(qk_knit_outer_chunk_kernel, dim3((unsigned)(o_count >> 9)), dim3(256), 0, ctx->stream, b);
-        QK_HIP(ctx, hipGetLastError());
-        return QK_OK;
-    }
     if (tb) {
         const uint64_t low = (uint64_t(1) << tb) - 1;
         const size_t stage = 8 * (size_t)K * ((size_t(1) << __builtin_popcountll(maskA & low)) +
