@@ -373,6 +373,11 @@ def drop_in_timing(cut, ref_out, steps: int, device: int) -> dict:
         del out
     # the reference-shaped result (run.py:71): entries above ACCURACY + NPD, thresholded knit
     dict_times, entries = [], 0
+    # the first dict call allocates the select / NPD buffers of this plan (reported apart, as the dense
+    # API's first call is); steady state = the calls after it
+    t0 = time.perf_counter()
+    run_virtual_circuit(VirtualCircuit(cut), device=device)
+    dict_first = time.perf_counter() - t0
     for _ in range(max(steps, 3)):
         virt = VirtualCircuit(cut)
         t0 = time.perf_counter()
@@ -385,6 +390,7 @@ def drop_in_timing(cut, ref_out, steps: int, device: int) -> dict:
 
     return {"api": "run_virtual_circuit(virt, dense=True)", "first_call_ms": first * 1e3,
             "dict_api": "run_virtual_circuit(virt): qk_knit_select (entries above ACCURACY only) + qk_npd_pairs",
+            "dict_first_ms": dict_first * 1e3,
             "dict_steady_ms": float(sum(dict_times) / len(dict_times)) * 1e3, "dict_min_ms": min(dict_times) * 1e3,
             "dict_entries": entries, "accuracy": quasi_distr.ACCURACY,
             "steady_ms": float(sum(times) / len(times)) * 1e3, "steady_min_ms": min(times) * 1e3,
