@@ -18,7 +18,8 @@ import glob
 import json
 import os
 
-CHAIN = ("qk_prep_operands_kernel", "qk_prep_reduce_kernel", "qk_rank_factors_kernel", "qk_compress_kernel", "qk_gemm_glds_kernel",
+CHAIN = ("qk_prep_operands_kernel", "qk_prep_reduce_kernel", "qk_rank_factors_kernel", "qk_compress_cols_kernel",
+         "qk_compress_kernel", "qk_gemm_glds_kernel", "qk_gemm_wave_kernel",
          "qk_probe_v_kernel", "qk_probe_d_kernel", "qk_probe_accept_kernel",
          "qk_knit_outer_blocked_kernel", "qk_select")
 
