@@ -862,13 +862,15 @@ def test_prep_operands_matches_torch(T, K, RA, RB, NA, NB):
             engine.prep_operands(ctx, WtA[:, :5].contiguous(), qA, WtB[:, :5].contiguous(), qB, P)
 
 
-@pytest.mark.parametrize("K,NA,NB", [(64, 4096, 1001), (24, 129, 8192), (64, 65536, 65536)])
-def test_compress_operands_matches_torch(T, K, NA, NB):
-    """qk_compress_operands against torch: even and odd column counts (rows not 16-B aligned), ragged
-    last column blocks, K below 64."""
+@pytest.mark.parametrize("K,NA,NB,rmax", [(64, 4096, 1001, 8), (24, 129, 8192, 8), (64, 65536, 65536, 8),
+                                          (24, 4096, 2048, 3), (17, 2050, 130, 8), (64, 2048, 4096, 1)])
+def test_compress_operands_matches_torch(T, K, NA, NB, rmax):
+    """qk_compress_operands against torch: odd column counts (rows not 16-B aligned: the K-split
+    kernel), even ones (the column kernel, qk_compress_cols_kernel) with K below 64, K not a multiple
+    of its 16-row load chunks, and fewer than 8 rows of T, ragged last column blocks."""
     ctx = engine.get_context(0)
-    g = T.Generator(device="cuda").manual_seed(K + NA + NB)
-    TA, TB = (T.randn(8, K, dtype=T.float64, device="cuda", generator=g) for _ in range(2))
+    g = T.Generator(device="cuda").manual_seed(K + NA + NB + rmax)
+    TA, TB = (T.randn(rmax, K, dtype=T.float64, device="cuda", generator=g) for _ in range(2))
     XA = T.randn(K, NA, dtype=T.float64, device="cuda", generator=g)
     XB = T.randn(K, NB, dtype=T.float64, device="cuda", generator=g)
     A2, B2 = engine.compress_operands(ctx, TA, XA, TB, XB)
