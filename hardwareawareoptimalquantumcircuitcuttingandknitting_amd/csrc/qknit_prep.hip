@@ -369,7 +369,8 @@ __global__ __launch_bounds__(64) void qk_compress_cols_kernel(int K, int rmax, c
     double* out = bs ? B2 : A2;
     const int64_t N = bs ? NB : NA;
     const int64_t c = ((int64_t)blockIdx.x * 64 + threadIdx.x) * 2;
-    if (c >= N) return;
+    if ((int64_t)blockIdx.x * 128 >= N) return;  // the whole wave past this side's columns
+    const int64_t cl = c < N ? c : N - 2;          // loads of lanes past the end: the last column pair
     d2_t acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = (d2_t){0.0, 0.0};
@@ -382,7 +383,7 @@ __global__ __launch_bounds__(64) void qk_compress_cols_kernel(int K, int rmax, c
 #pragma unroll
         for (int u = 0; u < PCW; ++u) {
             const int k = min(ch * PCW + u, K - 1);
-            b[u] = *reinterpret_cast<const d2_t*>(X + (int64_t)k * N + c);
+            b[u] = *reinterpret_cast<const d2_t*>(X + (int64_t)k * N + cl);
         }
     };
     const int nch = (K + PCW - 1) / PCW;
@@ -402,6 +403,7 @@ __global__ __launch_bounds__(64) void qk_compress_cols_kernel(int K, int rmax, c
         }
     }
     __syncthreads();
+    if (c >= N) return;  // after the T staging, which every lane of the wave takes part in
 #pragma unroll
     for (int ch = 0; ch < PK / PCW; ++ch) {
         if (ch >= nch) break;
