@@ -58,6 +58,21 @@ __global__ __launch_bounds__(256) void f_block_xcd(double* __restrict__ out, int
     }
 }
 
+// the XCD (XCC_ID hardware register, bits 3:0) each workgroup of a one16-shaped launch ran on
+__global__ __launch_bounds__(256) void f_xcc_map(int* __restrict__ xcc_of) {
+    if (threadIdx.x == 0) xcc_of[blockIdx.x] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15;
+}
+// one16 order, but a workgroup writes the chunks of its own XCD: the k-th workgroup to start on XCD x
+// (per-XCD counter) writes chunk 8 k + x
+__global__ __launch_bounds__(256) void f_one16_xcc(double* __restrict__ out, int* __restrict__ ctr) {
+    __shared__ int slot;
+    const int x = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7;
+    if (threadIdx.x == 0) slot = atomicAdd(&ctr[x], 1);
+    __syncthreads();
+    const int64_t c = 8 * (int64_t)slot + x;
+    reinterpret_cast<d2_t*>(out)[c * 256 + threadIdx.x] = (d2_t){(double)c, 1.0};
+}
+
 int main() {
     const int64_t total = int64_t(1) << 32;  // doubles
     double* out = nullptr;
@@ -114,6 +129,27 @@ int main() {
             if (cb < 8) continue;  // chunk below one 256-thread iteration: not expressible here
             run(nm, [&] { hipLaunchKernelGGL(f_block_xcd, dim3((unsigned)(n2 >> bb)), dim3(256), 0, 0, out, bb, cb); });
         }
+    {
+        const int nb = 4096;
+        int* d = nullptr;
+        CK(hipMalloc(&d, nb * sizeof(int)));
+        hipLaunchKernelGGL(f_xcc_map, dim3(nb), dim3(256), 0, 0, d);
+        std::vector<int> h(nb);
+        CK(hipMemcpy(h.data(), d, nb * sizeof(int), hipMemcpyDeviceToHost));
+        int rr = 0;
+        for (int b = 0; b < nb; ++b) rr += (h[b] == b % 8);
+        printf("xcc map: %d of %d workgroups on XCD blockIdx %% 8; first 16:", rr, nb);
+        for (int b = 0; b < 16; ++b) printf(" %d", h[b]);
+        printf("\n");
+        CK(hipFree(d));
+        int* ctr = nullptr;
+        CK(hipMalloc(&ctr, 8 * sizeof(int)));
+        run("one16, chunk = 8 k + own XCD", [&] {
+            (void)hipMemsetAsync(ctr, 0, 8 * sizeof(int), 0);
+            hipLaunchKernelGGL(f_one16_xcc, dim3((unsigned)(n2 / 256)), dim3(256), 0, 0, out, ctr);
+        });
+        CK(hipFree(ctr));
+    }
     CK(hipFree(out));
     return 0;
 }
