@@ -126,26 +126,18 @@ __global__ __launch_bounds__(RK_THREADS) void qk_rank_factors_kernel(RankArgs a)
 
     const int tid = threadIdx.x, lane = tid & 63, side = tid >> 6, K = a.K;
     RK_STAMP(0)
-    {  // raw copy, wave w on rows w*16.. of [GA; GB] (lane = column), 16 loads in flight per lane and no
-       // integer division in the index math (the divide-by-K form cost ~10 us); the symmetrisation
-       // 0.5 (G + G^T) happens where the Cholesky reads a column
-        const int wv = tid >> 6;
-        for (int r0 = wv * 16; r0 < 2 * K; r0 += 32) {
-            double v[16];
+    {  // raw copy: wave 0 loads GA, wave 1 GB (lane = column), all K rows of a lane in flight at once
+       // (round 3: unconditional loads with clamped indices; the round-2 loop of 16-row batches took one
+       // memory round trip per batch, ~10 of the kernel's 26 us in the step where the Grams are cold)
+       // — the symmetrisation 0.5 (G + G^T) happens where the Cholesky reads a column
+        const double* Gs = side ? a.GB : a.GA;
+        const int col = lane < K ? lane : K - 1;
+        double v[RK_K];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int rr = r0 + u;
-                v[u] = (rr < 2 * K && lane < K) ? (rr < K ? a.GA[rr * K + lane] : a.GB[(rr - K) * K + lane]) : 0.0;
-            }
+        for (int u = 0; u < RK_K; ++u) v[u] = Gs[(u < K ? u : K - 1) * K + col];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int rr = r0 + u;
-                if (rr < 2 * K && lane < K) {
-                    const int s = rr >= K ? 1 : 0;
-                    G[s][rr - s * K][lane] = v[u];
-                }
-            }
-        }
+        for (int u = 0; u < RK_K; ++u)
+            if (u < K && lane < K) G[side][u][lane] = v[u];
         __syncthreads();
         RK_STAMP(4)
     }
