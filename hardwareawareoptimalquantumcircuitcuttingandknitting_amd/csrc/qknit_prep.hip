@@ -272,11 +272,17 @@ __global__ __launch_bounds__(64 * PRW) void qk_prep_reduce_kernel(const double* 
     double s = 0.0;
     if (sd >= 0) {
         const double* p = part + (int64_t)sd * nblk * PPART + off;
-        double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // 8 loads in flight per thread, fixed summation order
+        // 32 loads in flight per thread (one memory round trip for 512 partials; batches of 8 took four),
+        // fixed summation order
+        double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         int b = grp;
-        for (; b + 7 * PRW < nblk; b += 8 * PRW)
+        for (; b + 31 * PRW < nblk; b += 32 * PRW) {
+            double v[32];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) t[u] += p[(int64_t)(b + PRW * u) * PPART];
+            for (int u = 0; u < 32; ++u) v[u] = p[(int64_t)(b + PRW * u) * PPART];
+#pragma unroll
+            for (int u = 0; u < 32; ++u) t[u & 7] += v[u];
+        }
         for (; b < nblk; b += PRW) t[0] += p[(int64_t)b * PPART];
         s = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
     }
@@ -449,17 +455,39 @@ __global__ __launch_bounds__(256) void qk_probe_v_kernel(int rmax, const double*
     for (int jj = 0; jj < 8; ++jj)
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[jj][q] = 0.0;
-#pragma unroll 4
-    for (int64_t c = (int64_t)blockIdx.x * 64 + lane; c < NB; c += (int64_t)gridDim.x * 64) {
+    // the next column's 12 loads in flight while the current one is multiplied (two named buffers,
+    // unconditional clamped prefetch: the round-2 loop waited for each iteration's loads in turn)
+    struct Col {
         double b[8], pv[4];
+    };
+    const int64_t step = (int64_t)gridDim.x * 64;
+    auto fetch = [&](int64_t c, Col& x) {
+        const int64_t cc = c < NB ? c : NB - 1;
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) b[jj] = B2[(int64_t)min(jj, rmax - 1) * ldb2 + c];
+        for (int jj = 0; jj < 8; ++jj) x.b[jj] = B2[(int64_t)min(jj, rmax - 1) * ldb2 + cc];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pv[q] = P[(int64_t)(4 * wave + q) * ldp + c];
+        for (int q = 0; q < 4; ++q) x.pv[q] = P[(int64_t)(4 * wave + q) * ldp + cc];
+    };
+    auto mac = [&](const Col& x) {
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) acc[jj][q] = fma(b[jj], pv[q], acc[jj][q]);
+            for (int q = 0; q < 4; ++q) acc[jj][q] = fma(x.b[jj], x.pv[q], acc[jj][q]);
+    };
+    int64_t c = (int64_t)blockIdx.x * 64 + lane;
+    if (c < NB) {
+        Col x0, x1;
+        fetch(c, x0);
+        for (;; c += 2 * step) {
+            fetch(c + step, x1);
+            __builtin_amdgcn_sched_barrier(0);  // keep the prefetch issued ahead of the multiplies
+            mac(x0);
+            if (c + step >= NB) break;
+            fetch(c + 2 * step, x0);
+            __builtin_amdgcn_sched_barrier(0);
+            mac(x1);
+            if (c + 2 * step >= NB) break;
+        }
     }
     // wave sums in a fixed order (xor butterfly: every lane ends with the total)
 #pragma unroll
@@ -524,23 +552,25 @@ __global__ __launch_bounds__(256) void qk_probe_d_kernel(int K, int rmax, const 
     for (int e = tid; e < PK * PNP; e += 256) Us[e / PNP][e % PNP] = (e / PNP) < K ? U[e] : 0.0;
     __syncthreads();
     double e2 = 0.0, f2 = 0.0;  // squared errors and squared reference products (R p)
-    const int ksteps = (K + 3) / 4;
+    // every operand load of a 16-column block in flight before its MFMAs (round 3: the k-loop waited
+    // for each load in turn, 18 memory round trips per block); rows k >= K re-read row K - 1 against
+    // the zero rows of Us, rows j >= rmax row rmax - 1 against the zero rows of Vs
     for (int64_t cb = (int64_t)blockIdx.x * 4 + wave; cb * 16 < NA; cb += (int64_t)gridDim.x * 4) {
         const int64_t c = cb * 16 + l16;
+        double av[PK / 4], a2[2];
+#pragma unroll
+        for (int kk = 0; kk < PK / 4; ++kk) av[kk] = XA[(int64_t)min(4 * kk + l4, K - 1) * ldx + c];  // A[c][k]
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) a2[jj] = A2[(int64_t)min(4 * jj + l4, rmax - 1) * lda2 + c];
         d4_t acc = {0, 0, 0, 0};
-        for (int kk = 0; kk < ksteps; ++kk) {
-            const int k = 4 * kk + l4;
-            const double av = k < K ? XA[(int64_t)k * ldx + c] : 0.0;  // A[c][k]
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Us[k][l16], acc, 0, 0, 0);
-        }
+#pragma unroll
+        for (int kk = 0; kk < PK / 4; ++kk)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kk], Us[4 * kk + l4][l16], acc, 0, 0, 0);
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) f2 = fma(acc[rr], acc[rr], f2);  // (X_A^T U)[c][p] = (R p)_c
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-            const int j = 4 * jj + l4;
-            const double av = j < rmax ? A2[(int64_t)j * lda2 + c] : 0.0;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Vs[j][l16], acc, 0, 0, 0);
-        }
+        for (int jj = 0; jj < 2; ++jj)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[jj], Vs[4 * jj + l4][l16], acc, 0, 0, 0);
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) e2 = fma(acc[rr], acc[rr], e2);  // d[cb*16 + l4 + 4rr][l16]
     }
@@ -574,9 +604,13 @@ __global__ __launch_bounds__(256) void qk_probe_accept_kernel(const double* __re
     constexpr int STEP = 256 / PE;
     double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int b = tid / PE;
-    for (; b + 7 * STEP < n; b += 8 * STEP)
+    for (; b + 31 * STEP < n; b += 32 * STEP) {  // 32 loads in flight per batch (batches of 8: a round trip each)
+        double v[32];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s8[u] += epart[(int64_t)(b + u * STEP) * PE + p];
+        for (int u = 0; u < 32; ++u) v[u] = epart[(int64_t)(b + u * STEP) * PE + p];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) s8[u & 7] += v[u];
+    }
     for (; b < n; b += STEP) s8[0] += epart[(int64_t)b * PE + p];
     const double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     acc[tid] = s;

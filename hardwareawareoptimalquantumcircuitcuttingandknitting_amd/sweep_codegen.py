@@ -76,7 +76,9 @@ def _lds_at(f: dict, r: int) -> str:
     is swizzled once per group (``sb``) and each access is one XOR with a constant (round 3: the
     per-access swizzle was ~20% of the FINAL pass's VALU instructions)."""
     c = int(f["cst"][r])
-    return f"sb ^ {_swz(c)}u" if c else "sb"
+    # byte offsets (sbb = 16 sb): the XOR lands on the address itself, no shift per access
+    off = f"(sbb ^ {16 * _swz(c)}u)" if c else "sbb"
+    return f"*reinterpret_cast<double2*>(reinterpret_cast<char*>(lds) + {off})"
 
 
 class _Emitter:
@@ -331,13 +333,13 @@ def _pass_kernel(enc: sp.EncodedProgram, ip: int, name: str, device_fn: bool = F
     for gi in gids:
         f = _fiber(enc, gi, TB, bitpos)
         e("{")
-        e(f"const unsigned sb = swz({f['base']});", 2)
+        e(f"const unsigned sbb = 16u * swz({f['base']});", 2)
         e("double2 v[16];", 2)
         for r in range(PER):
-            e(f"v[{r}] = lds[{_lds_at(f, r)}];", 2)
+            e(f"v[{r}] = {_lds_at(f, r)};", 2)
         _emit_group_ops(e, enc, gi, f, bitpos)
         for r in range(PER):
-            e(f"lds[{_lds_at(f, r)}] = v[{r}];", 2)
+            e(f"{_lds_at(f, r)} = v[{r}];", 2)
         e("__syncthreads();", 2)
         e("}")
     if zero_tile:
@@ -452,15 +454,15 @@ def _pass_body_direct(e: _Emitter, enc, ps, gids: list, TB: int, NT: int, n: int
         f = first if k == 0 else (last if k == len(gids) - 1 else _fiber(enc, gi, TB, bitpos))
         e("{")
         if k > 0:
-            e(f"const unsigned sb = swz({f['base']});", 2)
+            e(f"const unsigned sbb = 16u * swz({f['base']});", 2)
             for r in range(PER):
-                e(f"v[{r}] = lds[{_lds_at(f, r)}];", 2)
+                e(f"v[{r}] = {_lds_at(f, r)};", 2)
         _emit_group_ops(e, enc, gi, f, bitpos)
         if k < len(gids) - 1:
             if k == 0:
-                e(f"const unsigned sb = swz({f['base']});", 2)
+                e(f"const unsigned sbb = 16u * swz({f['base']});", 2)
             for r in range(PER):
-                e(f"lds[{_lds_at(f, r)}] = v[{r}];", 2)
+                e(f"{_lds_at(f, r)} = v[{r}];", 2)
             e("__syncthreads();", 2)
         e("}")
     if zero_tile:
