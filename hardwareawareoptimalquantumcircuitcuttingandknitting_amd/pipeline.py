@@ -416,6 +416,7 @@ class KnitPipeline:
         self.sweep_events = []  # (start, end) events around each step's sweep (all fragments)
         self.prep_events = []  # (sweep end, knit start): operand transforms + data-rank compression
         self.record_events = False
+        self.out_placement = None  # the output buffer's placement choice (_place_out), once per pipeline
         self._plan()
 
     def _stream_bits(self):
@@ -715,11 +716,14 @@ class KnitPipeline:
 
     def knit(self, qs: list):
         if self.dev_rank and self.mode in ("single", "slice"):
-            if self.out is None:
-                self.out = self._alloc_out(None)
             if self.mode == "slice":
+                if self.out is None:
+                    self.out = self._alloc_out(None)
                 return self._launch_slice(self._prep_slice(qs))
-            return self._launch_dev_rank(self._prep_dev_rank(qs))
+            p = self._prep_dev_rank(qs)
+            if self.out is None:
+                self.out = self._place_out(p)
+            return self._launch_dev_rank(p)
         mats = self.operands(qs)
         if self.out is None:
             self.out = self._alloc_out(mats)
@@ -1152,6 +1156,52 @@ class KnitPipeline:
         out = list(mats)
         out[ia], out[ib] = A, B
         return self._contract(out)
+
+    # Output placement (round 3): the write kernel's rate depends on the physical placement of the
+    # 2^N output buffer — bimodal on one box, 4.8 or 5.8 ms for the same kernel into different 34 GB
+    # allocations, while a plain fill runs at 5.1 ms into all of them (tools/alloc_probe.py,
+    # DESIGN.md §4). So the buffer the pipeline allocates itself is chosen once: up to
+    # OUT_CANDIDATES allocations held at the same time (distinct physical pages), the step's own write
+    # timed into each, the fastest kept and the others freed. QKNIT_OUT_CANDIDATES=1: no choice.
+    OUT_CANDIDATES = int(os.environ.get("QKNIT_OUT_CANDIDATES", "3"))
+
+    def _place_out(self, p: dict):
+        T = self.T
+        n = 1 << self.N
+        k = self.OUT_CANDIDATES
+        self._placed = True
+        dev = getattr(self.be, "dev", None)
+        if getattr(dev, "type", None) != "cuda":  # host backends (tests): nothing to place
+            k = 1
+        if k > 1:
+            free, _ = T.cuda.mem_get_info(dev)
+            k = min(k, int(free // (8 * n + (1 << 30))))  # leave 1 GiB
+        if k <= 1:
+            self.out_placement = None
+            return self._alloc_out(None)
+        ia, ib = self.order[0], self.order[-1]
+        cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
+        cands, times = [], []
+        for _ in range(k):
+            buf = T.empty(n, dtype=T.float64, device=self.be.dev)
+            ms = []
+            for _r in range(2):  # the first pass warms the page tables; the second is timed
+                s0, s1 = self.be.event(), self.be.event()
+                s0.record()
+                self.be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, buf, k_dev=p["k_eff"])
+                s1.record()
+                s1.synchronize()
+                ms.append(s0.elapsed_time(s1))
+            cands.append(buf)
+            times.append(ms[-1])
+        best = min(range(k), key=lambda i: times[i])
+        out = cands[best]
+        del cands
+        if not self.covers_outputs():  # outputs no kernel of the knit writes stay zero (as _alloc_out)
+            out.zero_()
+        T.cuda.empty_cache()  # the other candidates' blocks back to the device
+        self.out_placement = {"candidates": k, "write_ms": [round(t, 4) for t in times], "chosen": best}
+        return out
 
     def _alloc_out(self, mats):
         T = self.T

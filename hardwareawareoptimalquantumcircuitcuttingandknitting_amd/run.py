@@ -204,7 +204,11 @@ def _planned_dense(virt: VirtualCircuit, device: int, out):
     now = perf_counter()
     pipe = cached_plan(virt, device)
     pipe.be.bind()
-    if out is None:
+    # first call of a single-GPU data-rank plan: the pipeline places the output itself (the fastest of a
+    # few allocations for its write, pipeline._place_out); later calls get that block back from torch's
+    # caching allocator once the caller has dropped the previous result
+    place = out is None and pipe.mode == "single" and pipe.dev_rank and not getattr(pipe, "_placed", False)
+    if out is None and not place:
         n = pipe.slice[1] if pipe.mode == "slice" else 1 << pipe.N
         alloc = T.empty if pipe.covers_outputs() else T.zeros
         out = alloc(n, dtype=T.float64, device=T.device("cuda", device))
@@ -216,6 +220,7 @@ def _planned_dense(virt: VirtualCircuit, device: int, out):
         qs = pipe.sweep()
         e1.record()
         pipe.knit(qs)
+        out = pipe.out
     finally:
         pipe.out = None
     _sync(device)
