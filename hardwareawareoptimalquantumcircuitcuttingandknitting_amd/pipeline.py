@@ -725,6 +725,16 @@ class KnitPipeline:
                 self.out = self._place_out(p)
             return self._launch_dev_rank(p)
         mats = self.operands(qs)
+        small_k = self.mode == "single" and len(self.order) == 2 and mats[self.order[0]].shape[0] <= 8
+        if self.out is None and small_k and not self.data_rank and self.covers_outputs():
+            # the write-bound knit (syc 32 1: K = 1): its output placed like the data-rank write's
+            def write(buf):
+                keep, self.out = self.out, buf
+                try:
+                    self._contract_lowrank(mats)
+                finally:
+                    self.out = keep
+            self.out = self._place_out_with(write)
         if self.out is None:
             self.out = self._alloc_out(mats)
         if self.mode == "slice":
@@ -1166,6 +1176,13 @@ class KnitPipeline:
     OUT_CANDIDATES = int(os.environ.get("QKNIT_OUT_CANDIDATES", "3"))
 
     def _place_out(self, p: dict):
+        ia, ib = self.order[0], self.order[-1]
+        cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
+        return self._place_out_with(
+            lambda buf: self.be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, buf, k_dev=p["k_eff"]))
+
+    def _place_out_with(self, write):
+        """``write(buf)`` runs the step's write into ``buf``; returns the chosen output buffer."""
         T = self.T
         n = 1 << self.N
         k = self.OUT_CANDIDATES
@@ -1179,8 +1196,6 @@ class KnitPipeline:
         if k <= 1:
             self.out_placement = None
             return self._alloc_out(None)
-        ia, ib = self.order[0], self.order[-1]
-        cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
         cands, times = [], []
         for _ in range(k):
             buf = T.empty(n, dtype=T.float64, device=self.be.dev)
@@ -1188,7 +1203,7 @@ class KnitPipeline:
             for _r in range(2):  # the first pass warms the page tables; the second is timed
                 s0, s1 = self.be.event(), self.be.event()
                 s0.record()
-                self.be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, buf, k_dev=p["k_eff"])
+                write(buf)
                 s1.record()
                 s1.synchronize()
                 ms.append(s0.elapsed_time(s1))
