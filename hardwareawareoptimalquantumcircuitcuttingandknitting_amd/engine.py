@@ -63,8 +63,10 @@ class Context:
         self.handle = h
 
     def bind_stream(self) -> None:
-        s = torch().cuda.current_stream(self.device)
-        self.lib.qk_ctx_set_stream(self.handle, ctypes.c_void_p(s.cuda_stream))
+        s = torch().cuda.current_stream(self.device).cuda_stream
+        if s != getattr(self, "_bound", None):
+            self.lib.qk_ctx_set_stream(self.handle, ctypes.c_void_p(s))
+            self._bound = s
 
     def check(self, status: int, what: str) -> None:
         _lib.check(self.handle, status, what)

@@ -717,9 +717,15 @@ class KnitPipeline:
     def knit(self, qs: list):
         if self.dev_rank and self.mode in ("single", "slice"):
             if self.mode == "slice":
-                if self.out is None:
-                    self.out = self._alloc_out(None)
-                return self._launch_slice(self._prep_slice(qs))
+                p = self._prep_slice(qs)
+                if self.out is None:  # this rank's slice, placed like the single-GPU output (local writes only)
+                    o_begin, o_count = self.slice
+                    ia, ib = self.order[0], self.order[-1]
+                    cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
+                    self.out = self._place_out_with(
+                        lambda buf: self.be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, buf, o_begin=o_begin,
+                                                              o_count=o_count, k_dev=p["k_eff"]), n=o_count)
+                return self._launch_slice(p)
             p = self._prep_dev_rank(qs)
             if self.out is None:
                 self.out = self._place_out(p)
@@ -1008,6 +1014,10 @@ class KnitPipeline:
             # (here: the caller's wait for the write) would order the next step's preparation behind
             # this step's write and undo the overlap
             raise ValueError("pipelined steps need a non-default current stream (torch.cuda.stream(...))")
+        if self.out is None:
+            # the first step runs plain: it places the output (_place_out_with, timed writes on the
+            # whole chip); the pipelined steps after it write into that buffer
+            return self.knit(self.sweep())
         S, W = self._overlap_streams()
         W = W if W is not None else main
         with T.cuda.stream(S):
@@ -1172,8 +1182,13 @@ class KnitPipeline:
     # allocations, while a plain fill runs at 5.1 ms into all of them (tools/alloc_probe.py,
     # DESIGN.md §4). So the buffer the pipeline allocates itself is chosen once: up to
     # OUT_CANDIDATES allocations held at the same time (distinct physical pages), the step's own write
-    # timed into each, the fastest kept and the others freed. QKNIT_OUT_CANDIDATES=1: no choice.
-    OUT_CANDIDATES = int(os.environ.get("QKNIT_OUT_CANDIDATES", "3"))
+    # timed into each, the fastest kept and the others freed; the search stops at the first buffer
+    # written at OUT_FAST_GBS or more (the fast mode: 4.8-5.1 ms = 6.7-7.2 TB/s for 2^32 outputs; the
+    # slow one 5.8 ms = 5.9 TB/s). Outputs below OUT_MIN_BYTES (1 GiB) take one plain allocation. QKNIT_OUT_CANDIDATES=1:
+    # no choice.
+    OUT_CANDIDATES = int(os.environ.get("QKNIT_OUT_CANDIDATES", "6"))
+    OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "6500"))
+    OUT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_MIN_BYTES", str(1 << 30)))
 
     def _place_out(self, p: dict):
         ia, ib = self.order[0], self.order[-1]
@@ -1181,14 +1196,15 @@ class KnitPipeline:
         return self._place_out_with(
             lambda buf: self.be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, buf, k_dev=p["k_eff"]))
 
-    def _place_out_with(self, write):
-        """``write(buf)`` runs the step's write into ``buf``; returns the chosen output buffer."""
+    def _place_out_with(self, write, n=None):
+        """``write(buf)`` runs the step's write into ``buf`` (``n`` doubles, default 2^N); returns the
+        chosen output buffer."""
         T = self.T
-        n = 1 << self.N
+        n = (1 << self.N) if n is None else n
         k = self.OUT_CANDIDATES
         self._placed = True
         dev = getattr(self.be, "dev", None)
-        if getattr(dev, "type", None) != "cuda":  # host backends (tests): nothing to place
+        if getattr(dev, "type", None) != "cuda" or 8 * n < self.OUT_MIN_BYTES:  # host backends (tests), small outputs
             k = 1
         if k > 1:
             free, _ = T.cuda.mem_get_info(dev)
@@ -1209,13 +1225,15 @@ class KnitPipeline:
                 ms.append(s0.elapsed_time(s1))
             cands.append(buf)
             times.append(ms[-1])
-        best = min(range(k), key=lambda i: times[i])
+            if 8 * n / (ms[-1] * 1e6) >= self.OUT_FAST_GBS:
+                break
+        best = min(range(len(times)), key=lambda i: times[i])
         out = cands[best]
         del cands
         if not self.covers_outputs():  # outputs no kernel of the knit writes stay zero (as _alloc_out)
             out.zero_()
         T.cuda.empty_cache()  # the other candidates' blocks back to the device
-        self.out_placement = {"candidates": k, "write_ms": [round(t, 4) for t in times], "chosen": best}
+        self.out_placement = {"candidates": len(times), "write_ms": [round(t, 4) for t in times], "chosen": best}
         return out
 
     def _alloc_out(self, mats):
@@ -1336,6 +1354,9 @@ class KnitPipeline:
     PENDING_MAX = 32  # device-rank steps whose (rank, accepted) tensors are kept before a read-back
 
     def step(self):
+        bind = getattr(self.be, "bind", None)
+        if bind is not None:  # the caller may have switched torch's current stream since the last step
+            bind()
         if len(self._pending) >= self.PENDING_MAX:
             self.sync_stats()  # bounded: one host read every PENDING_MAX steps of a long loop
         if self.overlap and self.overlap_ok():

@@ -642,6 +642,8 @@ def test_syc_32_5_data_rank_step_matches_exact_step(T):
     assert pipe.dev_rank and pipe.last_kernel == "qk_knit_outer_blocked_kernel"
     assert pipe.rank_fallbacks == 0 and pipe.rank_incompressible == 0
     assert pipe.last_rank is not None and pipe.last_rank <= 8
+    pl = pipe.out_placement  # the output buffer was chosen among timed candidates
+    assert pl is not None and 1 <= pl["candidates"] <= pipe.OUT_CANDIDATES and len(pl["write_ms"]) == pl["candidates"]
     exact = KnitPipeline(VirtualCircuit(cut), factored=True, data_rank=False)
     ref = exact.step()
     T.cuda.synchronize()
@@ -649,6 +651,26 @@ def test_syc_32_5_data_rank_step_matches_exact_step(T):
     assert abs(float(got.sum()) - 1.0) <= 1e-10
     del pipe, exact, got, ref
     T.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("case", ["hwe_p2", "cx_8x8"])
+def test_output_placement_keeps_a_correct_buffer(T, case, monkeypatch):
+    """Output placement on small outputs (QKNIT_OUT_MIN_BYTES=0): the first step writes into every
+    candidate (none reaches the fast-write rate at this size), keeps one, and the steps after it
+    write the same values into that buffer (oracle, 1e-12)."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    monkeypatch.setattr(KnitPipeline, "OUT_MIN_BYTES", 0)
+    cut = {"hwe_p2": lambda: cutting.config_cut_circuit("hwe", 16, 1, 2)[1],
+           "cx_8x8": lambda: circuits.two_fragment("cx", 8, 8, n_cuts=4)[1]}[case]()
+    pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
+    ref = dense.run_dense(cut)
+    for _ in range(2):
+        got = pipe.step().cpu().numpy()
+        np.testing.assert_allclose(got, ref, atol=1e-12, rtol=0)
+    pl = pipe.out_placement
+    if pipe.dev_rank:
+        assert pl is not None and pl["candidates"] == pipe.OUT_CANDIDATES and 0 <= pl["chosen"] < pl["candidates"]
 
 
 @pytest.mark.slow
