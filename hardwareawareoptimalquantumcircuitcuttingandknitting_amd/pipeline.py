@@ -321,6 +321,25 @@ class HipBackend:
         return self.T.cuda.Event(enable_timing=True)
 
 
+def pick_output_buffer(alloc, timed_write, k: int, nbytes: int, fast_gbs: float):
+    """The output placement search (``KnitPipeline._place_out_with``): up to ``k`` buffers from
+    ``alloc()``, all held until the end (so each lands on different physical pages); ``timed_write(buf)``
+    runs the step's write and returns its ms — once to warm the page tables, once timed. Stops at the
+    first buffer written at ``fast_gbs`` GB/s or more (``nbytes`` per write). Returns (the fastest
+    buffer, the timed ms per candidate, its index); the other candidates are dropped on return."""
+    cands, times = [], []
+    for _ in range(max(1, k)):
+        buf = alloc()
+        timed_write(buf)
+        t = timed_write(buf)
+        cands.append(buf)
+        times.append(t)
+        if t > 0 and nbytes / (t * 1e6) >= fast_gbs:
+            break
+    best = min(range(len(times)), key=times.__getitem__)
+    return cands[best], times, best
+
+
 class KnitPipeline:
     def __init__(self, virt, device: int = 0, factored: bool = False, rank: int = 0, world: int = 1,
                  mode: str | None = None, group=None, backend=None, chunk_jobs: int | None = None,
@@ -1212,24 +1231,17 @@ class KnitPipeline:
         if k <= 1:
             self.out_placement = None
             return self._alloc_out(None)
-        cands, times = [], []
-        for _ in range(k):
-            buf = T.empty(n, dtype=T.float64, device=self.be.dev)
-            ms = []
-            for _r in range(2):  # the first pass warms the page tables; the second is timed
-                s0, s1 = self.be.event(), self.be.event()
-                s0.record()
-                write(buf)
-                s1.record()
-                s1.synchronize()
-                ms.append(s0.elapsed_time(s1))
-            cands.append(buf)
-            times.append(ms[-1])
-            if 8 * n / (ms[-1] * 1e6) >= self.OUT_FAST_GBS:
-                break
-        best = min(range(len(times)), key=lambda i: times[i])
-        out = cands[best]
-        del cands
+
+        def timed(buf):
+            s0, s1 = self.be.event(), self.be.event()
+            s0.record()
+            write(buf)
+            s1.record()
+            s1.synchronize()
+            return s0.elapsed_time(s1)
+
+        out, times, best = pick_output_buffer(lambda: T.empty(n, dtype=T.float64, device=self.be.dev), timed, k,
+                                              8 * n, self.OUT_FAST_GBS)
         if not self.covers_outputs():  # outputs no kernel of the knit writes stay zero (as _alloc_out)
             out.zero_()
         T.cuda.empty_cache()  # the other candidates' blocks back to the device
