@@ -81,8 +81,14 @@ static_assert(PRS % 8 == 0 && PRS >= 8, "stage rows: a multiple of 8 (8 waves)")
 #define QK_PREP_EXP 0  // tools/ timing experiments only: 1 skips the Gram phase, 2 the X store, 4 the transform
 #endif
 constexpr int PNS = QK_PREP_NS;  // stages in flight
-constexpr int QLD = PCT + 16;    // q stage row stride (doubles): rows 32 banks apart, a k-step's reads conflict-free
-constexpr int WLD = PK + 16;     // Wt stage row stride (same)
+#ifndef QK_PREP_QPAD
+#define QK_PREP_QPAD 16
+#endif
+#ifndef QK_PREP_WPAD
+#define QK_PREP_WPAD 16
+#endif
+constexpr int QLD = PCT + QK_PREP_QPAD;  // q stage row stride (doubles): rows 32 banks apart, a k-step's reads conflict-free
+constexpr int WLD = PK + QK_PREP_WPAD;   // Wt stage row stride (same)
 struct PrepStage {
     double q[PRS][QLD];
     double w[PRS][WLD];
