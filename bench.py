@@ -361,7 +361,7 @@ def drop_in_timing(cut, ref_out, steps: int, device: int) -> dict:
     first = time.perf_counter() - t0
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.run import cached_plan
 
-    placement = getattr(cached_plan(virt0, device), "out_placement", None)
+    placement = getattr(cached_plan(virt0, device), "out_alloc", None)
     diff = 0.0
     chunk = 1 << 28
     for i in range(0, out.numel(), chunk):
@@ -400,7 +400,7 @@ def drop_in_timing(cut, ref_out, steps: int, device: int) -> dict:
             "steady_ms": float(sum(times) / len(times)) * 1e3, "steady_min_ms": min(times) * 1e3,
             "run_time_ms": float(sum(i.run_time for i in infos) / len(infos)) * 1e3,
             "knit_time_ms": float(sum(i.knit_time for i in infos) / len(infos)) * 1e3,
-            "calls": len(times), "max_abs_diff_vs_step": diff, "out_placement": placement}
+            "calls": len(times), "max_abs_diff_vs_step": diff, "out_alloc": placement}
 
 
 def npd_timing(dense, accuracy: float) -> dict:
@@ -706,10 +706,9 @@ def main():
         for k in ("f64_issue_frac", "valu_busy_frac"):  # SIMD issue cycles over the counted run's step
             if k in c:
                 line["sweep"][k] = c[k]
-    if pipe.out_placement is not None:
-        # the output buffer: the fastest of a few allocations for this write (pipeline._place_out, at the
-        # first step, outside the timed region) — the write time of each candidate
-        line["out_placement"] = pipe.out_placement
+    if pipe.out_alloc is not None:
+        # the output buffer: one allocation, mapped from 1-GiB physical chunks (qk_out_alloc)
+        line["out_alloc"] = pipe.out_alloc
     prep = [s.elapsed_time(e) for s, e in pipe.prep_events]
     if prep:
         line["rank_compress_ms"] = sum(prep) / len(prep)  # sweep end -> knit start (transforms, factors, probes)

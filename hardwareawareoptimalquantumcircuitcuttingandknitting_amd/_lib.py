@@ -51,6 +51,9 @@ SIGNATURES = {
     "qk_stream_create_cu_masked": (c_i32, [ctypes.c_int, ctypes.POINTER(c_u32), ctypes.c_int, ctypes.POINTER(c_vp)]),
     "qk_stream_destroy": (c_i32, [c_vp]),
     "qk_stream_cu_count": (c_i32, [ctypes.c_int, c_vp, ctypes.POINTER(ctypes.c_int)]),
+    "qk_out_alloc": (c_i32, [c_vp, c_i64, ctypes.POINTER(c_vp)]),
+    "qk_out_free": (c_i32, [c_vp, c_vp]),
+    "qk_out_mapped_bytes": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),
     "qk_sweep_workspace_bytes": (c_i32, [ctypes.POINTER(QkProgram), c_i64, ctypes.POINTER(c_i64)]),
     "qk_sweep": (c_i32, [c_vp, ctypes.POINTER(QkProgram), c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "qk_module_compile": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
@@ -73,6 +76,8 @@ SIGNATURES = {
                                      c_vp, c_vp]),
     "qk_knit_outer_stream": (c_i32, [c_vp, ctypes.c_int, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.c_uint64,
                                      ctypes.c_uint64, c_vp]),
+    "qk_knit_outer_stream_kind": (c_i32, [ctypes.c_int, c_i64, c_u64, c_u64, c_i64, c_i64,
+                                          ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "qk_knit_outer_stream_range": (c_i32, [c_vp, ctypes.c_int, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.c_uint64,
                                            ctypes.c_uint64, c_i64, c_i64, c_vp, c_vp]),
     "qk_rank_factors": (c_i32, [c_vp, c_i64, c_vp, c_vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,

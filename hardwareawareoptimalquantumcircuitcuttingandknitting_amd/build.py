@@ -9,7 +9,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", f) for f in ("qknit.hip", "qknit_post.hip", "qknit_jit.hip",
                                                               "qknit_sample.hip", "qknit_rank.hip",
                                                               "qknit_plan.hip", "qknit_prep.hip",
-                                                              "qknit_select.hip", "qknit_comm.hip")]
+                                                              "qknit_select.hip", "qknit_comm.hip",
+                                                              "qknit_mem.hip")]
 DEPS = SRCS + [os.path.join(HERE, "csrc", h) for h in ("internal.h", "sweep_ops.h")]
 HEADER = os.path.join(os.path.dirname(HERE), "include", "qknit.h")
 OUT = os.path.join(HERE, "libqknit.so")
@@ -33,12 +34,28 @@ def build_library(force: bool = False, verbose: bool = False, out: str = OUT,
     if not (force or stale):
         return out
     tmp = out + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-result", *[f"-D{d}" for d in defines], *SRCS, "-lhiprtc", "-lrccl", "-o", tmp]
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
+             *[f"-D{d}" for d in defines]]
+    # one hipcc per translation unit, in parallel (the device code dominates: ~2 min serial), then link
+    objdir = os.path.join(os.path.dirname(out), "build", os.path.basename(out) + ".objs")
+    os.makedirs(objdir, exist_ok=True)
+    jobs = []
+    for src in SRCS:
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        cmd = [hipcc(), *flags, "-c", src, "-o", obj]
+        jobs.append((cmd, obj, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
+    errs = []
+    for cmd, obj, proc in jobs:
+        _, err = proc.communicate()
+        if proc.returncode != 0:
+            errs.append(f"{' '.join(cmd)}\n{err}")
+        elif verbose and err:
+            print(err)
+    if errs:
+        raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
+    cmd = [hipcc(), *flags, "-shared", *[obj for _, obj, _ in jobs], "-lhiprtc", "-lrccl", "-o", tmp]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
-        raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{res.stderr}")
-    if verbose and res.stderr:
-        print(res.stderr)
+        raise RuntimeError(f"hipcc link failed:\n{' '.join(cmd)}\n{res.stderr}")
     os.replace(tmp, out)
     return out

@@ -1778,6 +1778,16 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
     return QK_OK;
 }
 
+int qk_knit_outer_stream_kind(int nbits, int64_t K, uint64_t maskA, uint64_t maskB, int64_t o_begin,
+                              int64_t o_count, int* kind, int* task_bits) {
+    if (!kind || !task_bits || nbits < 2 || nbits > 32 || K < 1 || K > SK_MAX || o_count <= 0) return QK_EARG;
+    bool bg = false;
+    const int tb = outer_blocked_tile(nbits, K, maskA, maskB, __builtin_ctzll((uint64_t)(o_begin | o_count)), &bg);
+    *kind = tb ? (bg ? 2 : 1) : 0;
+    *task_bits = tb;
+    return QK_OK;
+}
+
 int qk_khatri_rao(qk_ctx* ctx, int64_t K, int64_t M, int64_t N, const double* A, int64_t lda,
                   const double* B, int64_t ldb, double* out) {
     if (!ctx) return QK_EARG;

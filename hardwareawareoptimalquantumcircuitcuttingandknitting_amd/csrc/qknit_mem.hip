@@ -1,0 +1,144 @@
+// qknit_mem.hip — output buffers mapped from 1-GiB physical allocations (gfx950).
+//
+// The knit's dominant kernel streams the 2^N output (syc 32: 2^32 fp64 = 34.4 GB per step) from
+// persistent workgroups, each writing its own 512-KiB task. Into a plain hipMalloc buffer that write
+// is bimodal: 4.83-4.87 ms into some allocations, 5.8-6.0 ms into others on the same box, while a
+// store order with one short-lived workgroup per 4 KiB is ~4.9 ms into every one of them
+// (tools/write_probe2..8). Composing the same 34 GB from 1-GiB physical allocations (hipMemCreate)
+// mapped at 1-GiB-aligned virtual addresses makes every buffer fast — 4.83-4.86 ms for 24 buffers
+// covering all 280 GB of the device in order, interleaved and permuted (tools/write_probe10) — so the
+// slow mode follows the virtual-to-physical mapping (the translation granularity a hipMalloc block
+// happens to get), not the physical memory. qk_out_alloc maps every large output this way; the
+// pipeline no longer times candidate allocations (round 3's placement search).
+//
+//   qk_out_alloc(ctx, bytes, &ptr)  device memory of at least `bytes`, 1-GiB physical chunks (the
+//                                   last rounded up to the allocation granularity) mapped
+//                                   read-write for ctx's device at a 1-GiB-aligned address;
+//                                   below 1 GiB one chunk at an alignment of its power-of-two size
+//   qk_out_free(ctx, ptr)           synchronizes the device, unmaps, releases
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "internal.h"
+
+namespace {
+
+struct OutMapping {
+    size_t bytes;  // reserved and mapped
+    int device;
+    std::vector<hipMemGenericAllocationHandle_t> chunks;
+};
+
+std::mutex g_mu;
+std::map<uintptr_t, OutMapping> g_maps;
+
+constexpr size_t OUT_CHUNK = size_t(1) << 30;
+
+int mem_fail(qk_ctx* ctx, int code, const char* what, hipError_t e) {
+    if (ctx) {
+        char buf[256];
+        snprintf(buf, sizeof buf, "%s: %s", what, e == hipSuccess ? "invalid argument" : hipGetErrorString(e));
+        ctx->err = buf;
+    }
+    return code;
+}
+
+void unmap_release(void* va, OutMapping& m) {
+    (void)hipMemUnmap(va, m.bytes);
+    for (auto h : m.chunks) (void)hipMemRelease(h);
+    (void)hipMemAddressFree(va, m.bytes);
+}
+
+}  // namespace
+
+extern "C" {
+
+int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr) {
+    if (!ctx || !ptr || bytes <= 0) return mem_fail(ctx, QK_EARG, "qk_out_alloc: need a context, bytes > 0", hipSuccess);
+    *ptr = nullptr;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_alloc: hipSetDevice", e);
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = ctx->device;
+    size_t gran = 0;
+    e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum);
+    if (e != hipSuccess || gran == 0) return mem_fail(ctx, QK_EHIP, "qk_out_alloc: allocation granularity", e);
+    size_t want = ((size_t)bytes + gran - 1) / gran * gran;
+    size_t chunk = OUT_CHUNK, align = OUT_CHUNK;
+    if (want < OUT_CHUNK) {  // one chunk, aligned to its power-of-two size
+        chunk = want;
+        align = gran;
+        while (align < want) align <<= 1;
+    }
+    const size_t n_chunks = (want + chunk - 1) / chunk;
+    OutMapping m{n_chunks * chunk, ctx->device, {}};
+    void* va = nullptr;
+    e = hipMemAddressReserve(&va, m.bytes, align, nullptr, 0);
+    if (e != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_alloc: hipMemAddressReserve", e);
+    size_t mapped = 0;
+    for (size_t i = 0; i < n_chunks; ++i) {
+        hipMemGenericAllocationHandle_t h;
+        e = hipMemCreate(&h, chunk, &prop, 0);
+        if (e == hipSuccess) {
+            e = hipMemMap((char*)va + i * chunk, chunk, 0, h, 0);
+            if (e != hipSuccess) (void)hipMemRelease(h);
+        }
+        if (e != hipSuccess) {
+            (void)hipMemUnmap(va, mapped);
+            for (auto hh : m.chunks) (void)hipMemRelease(hh);
+            (void)hipMemAddressFree(va, m.bytes);
+            return mem_fail(ctx, QK_EHIP, "qk_out_alloc: hipMemCreate / hipMemMap", e);
+        }
+        m.chunks.push_back(h);
+        mapped += chunk;
+    }
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    e = hipMemSetAccess(va, m.bytes, &acc, 1);
+    if (e != hipSuccess) {
+        unmap_release(va, m);
+        return mem_fail(ctx, QK_EHIP, "qk_out_alloc: hipMemSetAccess", e);
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_maps[(uintptr_t)va] = std::move(m);
+    }
+    *ptr = va;
+    return QK_OK;
+}
+
+int qk_out_free(qk_ctx* ctx, void* ptr) {
+    if (!ptr) return QK_OK;
+    OutMapping m;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_maps.find((uintptr_t)ptr);
+        if (it == g_maps.end()) return mem_fail(ctx, QK_EARG, "qk_out_free: not a qk_out_alloc pointer", hipSuccess);
+        m = std::move(it->second);
+        g_maps.erase(it);
+    }
+    (void)hipSetDevice(m.device);
+    // kernels on any stream may still write the buffer: the mapping goes only when they are done
+    hipError_t e = hipDeviceSynchronize();
+    unmap_release(ptr, m);
+    if (e != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_free: hipDeviceSynchronize", e);
+    return QK_OK;
+}
+
+int qk_out_mapped_bytes(const void* ptr, int64_t* bytes) {
+    if (!bytes) return QK_EARG;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_maps.find((uintptr_t)ptr);
+    *bytes = it == g_maps.end() ? 0 : (int64_t)it->second.bytes;
+    return it == g_maps.end() ? QK_EARG : QK_OK;
+}
+
+}  // extern "C"

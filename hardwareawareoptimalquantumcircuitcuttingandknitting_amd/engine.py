@@ -141,6 +141,69 @@ def get_context(device: int = 0) -> Context:
     return ctx
 
 
+class _Lease:
+    """What a tensor over a MappedOut holds (through ``__cuda_array_interface__``): one per
+    :meth:`MappedOut.tensor`, alive exactly as long as that tensor's storage (views included)."""
+
+    def __init__(self, owner):
+        self.owner = owner
+        self.__cuda_array_interface__ = owner.cai
+
+
+class MappedOut:
+    """Owner of one ``qk_out_alloc`` mapping (1-GiB physical chunks at a 1-GiB-aligned address,
+    csrc/qknit_mem.hip): the knit output the write kernels stream into at the same rate whichever
+    memory the device hands out (a plain allocation: 4.8 or 5.9 ms per 2^32 fp64, by block). Tensors
+    over it (:meth:`tensor`) keep it alive; the mapping is released (device synchronised first) when
+    the last of them and this object are gone."""
+
+    def __init__(self, ctx: Context, n: int):
+        self.lib, self.device, self.n = ctx.lib, ctx.device, int(n)
+        p = ctypes.c_void_p()
+        ctx.check(ctx.lib.qk_out_alloc(ctx.handle, 8 * self.n, ctypes.byref(p)), "qk_out_alloc")
+        self.ptr = p.value
+        self.cai = {"shape": (self.n,), "typestr": "<f8", "data": (self.ptr, False), "version": 2}
+        self._leases = []
+
+    def tensor(self):
+        """A float64 [n] tensor on the mapping (its storage holds this owner)."""
+        import weakref
+
+        T = torch()
+        lease = _Lease(self)
+        with T.cuda.device(self.device):
+            t = T.as_tensor(lease, device=T.device("cuda", self.device))
+        if t.data_ptr() != self.ptr:
+            raise _lib.QknitError("qk_out_alloc buffer was copied instead of shared")
+        self._leases = [w for w in self._leases if w() is not None] + [weakref.ref(lease)]
+        return t
+
+    def in_use(self) -> bool:
+        """Whether a tensor handed out by :meth:`tensor` (or a view of it) is still alive."""
+        return any(w() is not None for w in self._leases)
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            try:
+                self.lib.qk_out_free(None, ctypes.c_void_p(self.ptr))
+            except Exception:
+                pass
+            self.ptr = None
+
+
+OUT_MAPPED_MIN_BYTES = int(os.environ.get("QKNIT_OUT_MAPPED_MIN_BYTES", str(1 << 30)))  # below: torch allocation
+
+
+def out_buffer(ctx: Context, n: int):
+    """(tensor [n] float64, owner or None): a ``qk_out_alloc`` mapping for outputs of at least
+    OUT_MAPPED_MIN_BYTES, torch's allocator below that. Contents are undefined."""
+    T = torch()
+    if 8 * n < OUT_MAPPED_MIN_BYTES:
+        return T.empty(n, dtype=T.float64, device=T.device("cuda", ctx.device)), None
+    owner = MappedOut(ctx, n)
+    return owner.tensor(), owner
+
+
 # ----------------------------------------------------------------------------- fragments
 @dataclass
 class DeviceProgram:
@@ -512,6 +575,24 @@ def knit_outer_stream(ctx: Context, A, B, clbits_a: list, clbits_b: list, nbits:
                                                  o_begin, o_count, _ptr(k_dev), out.data_ptr()),
               "qk_knit_outer_stream_range")
     return out
+
+
+OUTER_STREAM_KERNELS = ("qk_knit_outer_stream_kernel", "qk_knit_outer_blocked_kernel",
+                        "qk_knit_outer_blocked_kernel<b_global>")
+
+
+def knit_outer_stream_kernel(K: int, clbits_a: list, clbits_b: list, nbits: int, o_begin: int = 0,
+                             o_count: int | None = None) -> str:
+    """Name of the kernel :func:`knit_outer_stream` launches for these arguments
+    (``qk_knit_outer_stream_kind``): the per-output gather, the blocked kernel with both operands
+    staged in LDS, or the blocked kernel reading B from global memory."""
+    mA, mB = sum(1 << c for c in clbits_a), sum(1 << c for c in clbits_b)
+    if o_count is None:
+        o_count = (1 << nbits) - o_begin
+    kind, tb = ctypes.c_int(), ctypes.c_int()
+    _lib.check(None, _lib.lib().qk_knit_outer_stream_kind(nbits, K, mA, mB, o_begin, o_count, ctypes.byref(kind),
+                                                          ctypes.byref(tb)), "qk_knit_outer_stream_kind")
+    return OUTER_STREAM_KERNELS[kind.value]
 
 
 def stream_knit_ok(clbits_a: list, clbits_b: list, nbits: int) -> bool:

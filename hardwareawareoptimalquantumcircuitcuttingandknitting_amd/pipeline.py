@@ -293,6 +293,9 @@ class HipBackend:
         return engine.knit_outer_stream(self.ctx, A, B, clbits_a, clbits_b, nbits, out, o_begin=o_begin,
                                         o_count=o_count, k_dev=k_dev)
 
+    def outer_stream_kernel(self, K, clbits_a, clbits_b, nbits, o_begin=0, o_count=None):
+        return engine.knit_outer_stream_kernel(K, clbits_a, clbits_b, nbits, o_begin, o_count)
+
     def rank_factors(self, GA, GB):
         return engine.rank_factors_device(self.ctx, GA, GB)
 
@@ -317,27 +320,12 @@ class HipBackend:
     def npd_dense(self, dense, accuracy):
         return engine.nearest_probability_distribution(self.ctx, dense, accuracy)
 
+    def out_buffer(self, n: int):
+        """(tensor [n] float64, owner): the knit output, 1-GiB-mapped when large (engine.out_buffer)."""
+        return engine.out_buffer(self.ctx, n)
+
     def event(self):
         return self.T.cuda.Event(enable_timing=True)
-
-
-def pick_output_buffer(alloc, timed_write, k: int, nbytes: int, fast_gbs: float):
-    """The output placement search (``KnitPipeline._place_out_with``): up to ``k`` buffers from
-    ``alloc()``, all held until the end (so each lands on different physical pages); ``timed_write(buf)``
-    runs the step's write and returns its ms — once to warm the page tables, once timed. Stops at the
-    first buffer written at ``fast_gbs`` GB/s or more (``nbytes`` per write). Returns (the fastest
-    buffer, the timed ms per candidate, its index); the other candidates are dropped on return."""
-    cands, times = [], []
-    for _ in range(max(1, k)):
-        buf = alloc()
-        timed_write(buf)
-        t = timed_write(buf)
-        cands.append(buf)
-        times.append(t)
-        if t > 0 and nbytes / (t * 1e6) >= fast_gbs:
-            break
-    best = min(range(len(times)), key=times.__getitem__)
-    return cands[best], times, best
 
 
 class KnitPipeline:
@@ -435,7 +423,7 @@ class KnitPipeline:
         self.sweep_events = []  # (start, end) events around each step's sweep (all fragments)
         self.prep_events = []  # (sweep end, knit start): operand transforms + data-rank compression
         self.record_events = False
-        self.out_placement = None  # the output buffer's placement choice (_place_out), once per pipeline
+        self.out_alloc = None  # how the last output buffer was allocated (new_out)
         self._plan()
 
     def _stream_bits(self):
@@ -737,29 +725,14 @@ class KnitPipeline:
         if self.dev_rank and self.mode in ("single", "slice"):
             if self.mode == "slice":
                 p = self._prep_slice(qs)
-                if self.out is None:  # this rank's slice, placed like the single-GPU output (local writes only)
-                    o_begin, o_count = self.slice
-                    ia, ib = self.order[0], self.order[-1]
-                    cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
-                    self.out = self._place_out_with(
-                        lambda buf: self.be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, buf, o_begin=o_begin,
-                                                              o_count=o_count, k_dev=p["k_eff"]), n=o_count)
+                if self.out is None:
+                    self.out = self._alloc_out(None)
                 return self._launch_slice(p)
             p = self._prep_dev_rank(qs)
             if self.out is None:
-                self.out = self._place_out(p)
+                self.out = self._alloc_out(None)
             return self._launch_dev_rank(p)
         mats = self.operands(qs)
-        small_k = self.mode == "single" and len(self.order) == 2 and mats[self.order[0]].shape[0] <= 8
-        if self.out is None and small_k and not self.data_rank and self.covers_outputs():
-            # the write-bound knit (syc 32 1: K = 1): its output placed like the data-rank write's
-            def write(buf):
-                keep, self.out = self.out, buf
-                try:
-                    self._contract_lowrank(mats)
-                finally:
-                    self.out = keep
-            self.out = self._place_out_with(write)
         if self.out is None:
             self.out = self._alloc_out(mats)
         if self.mode == "slice":
@@ -863,13 +836,18 @@ class KnitPipeline:
         k_eff, _ = self._accept(A, B, A2, B2, self._probes(B.shape[1], B.device), r)
         return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
 
+    def _kernel_name(self, K, cA, cB, o_begin=0, o_count=None):
+        """The write kernel knit_outer_stream launches (the backend's answer; its class name otherwise)."""
+        name = getattr(self.be, "outer_stream_kernel", None)
+        return name(K, cA, cB, self.N, o_begin, o_count) if name else type(self.be).__name__
+
     def _launch_dev_rank(self, p: dict):
         ia, ib = self.order[0], self.order[-1]
         cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
         if self.record_events:
             start, end = self.be.event(), self.be.event()
             start.record()
-        self.last_kernel = "qk_knit_outer_blocked_kernel"
+        self.last_kernel = self._kernel_name(p["A2"].shape[0], cA, cB)
         self.be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, self.out, k_dev=p["k_eff"])
         if self.record_events:
             end.record()
@@ -968,7 +946,7 @@ class KnitPipeline:
         if self.record_events:
             start, end = be.event(), be.event()
             start.record()
-        self.last_kernel = "qk_knit_outer_blocked_kernel"
+        self.last_kernel = self._kernel_name(p["A2"].shape[0], cA, cB, o_begin, o_count)
         be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, self.out, o_begin=o_begin, o_count=o_count,
                              k_dev=p["k_eff"])
         if self.record_events:
@@ -1034,8 +1012,8 @@ class KnitPipeline:
             # this step's write and undo the overlap
             raise ValueError("pipelined steps need a non-default current stream (torch.cuda.stream(...))")
         if self.out is None:
-            # the first step runs plain: it places the output (_place_out_with, timed writes on the
-            # whole chip); the pipelined steps after it write into that buffer
+            # the first step runs plain (it allocates the output); the pipelined steps after it write
+            # into that buffer
             return self.knit(self.sweep())
         S, W = self._overlap_streams()
         W = W if W is not None else main
@@ -1179,7 +1157,7 @@ class KnitPipeline:
         cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
         stream = os.environ.get("QKNIT_OUTER", "stream") == "stream"  # "paired": keyed kernel (A/B timing)
         if stream and r <= 8 and engine.stream_knit_ok(cA, cB, self.N) and hasattr(self.be, "knit_outer_stream"):
-            self.last_kernel = "qk_knit_outer_stream_kernel"
+            self.last_kernel = self._kernel_name(r, cA, cB)
             return self.be.knit_outer_stream(A, B, cA, cB, self.N, self.out)
         if r <= 8 and engine.paired_keys(cB) and hasattr(self.be, "gemm_outer_paired"):
             st = engine._affine_stride(cA)
@@ -1196,67 +1174,55 @@ class KnitPipeline:
         out[ia], out[ib] = A, B
         return self._contract(out)
 
-    # Output placement (round 3): the write kernel's rate depends on the physical placement of the
-    # 2^N output buffer — bimodal on one box, 4.8 or 5.8 ms for the same kernel into different 34 GB
-    # allocations, while a plain fill runs at 5.1 ms into all of them (tools/alloc_probe.py,
-    # DESIGN.md §4). So the buffer the pipeline allocates itself is chosen once: up to
-    # OUT_CANDIDATES allocations held at the same time (distinct physical pages), the step's own write
-    # timed into each, the fastest kept and the others freed; the search stops at the first buffer
-    # written at OUT_FAST_GBS or more (the fast mode: 4.8-5.1 ms = 6.7-7.2 TB/s for 2^32 outputs; the
-    # slow one 5.8 ms = 5.9 TB/s). Outputs below OUT_MIN_BYTES (1 GiB) take one plain allocation. QKNIT_OUT_CANDIDATES=1:
-    # no choice.
-    OUT_CANDIDATES = int(os.environ.get("QKNIT_OUT_CANDIDATES", "6"))
-    OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "6500"))
-    OUT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_MIN_BYTES", str(1 << 30)))
-
-    def _place_out(self, p: dict):
-        ia, ib = self.order[0], self.order[-1]
-        cA, cB = self.ops.clbits[ia], self.ops.clbits[ib]
-        return self._place_out_with(
-            lambda buf: self.be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, buf, k_dev=p["k_eff"]))
-
-    def _place_out_with(self, write, n=None):
-        """``write(buf)`` runs the step's write into ``buf`` (``n`` doubles, default 2^N); returns the
-        chosen output buffer."""
-        T = self.T
-        n = (1 << self.N) if n is None else n
-        k = self.OUT_CANDIDATES
-        self._placed = True
-        dev = getattr(self.be, "dev", None)
-        if getattr(dev, "type", None) != "cuda" or 8 * n < self.OUT_MIN_BYTES:  # host backends (tests), small outputs
-            k = 1
-        if k > 1:
-            free, _ = T.cuda.mem_get_info(dev)
-            k = min(k, int(free // (8 * n + (1 << 30))))  # leave 1 GiB
-        if k <= 1:
-            self.out_placement = None
-            return self._alloc_out(None)
-
-        def timed(buf):
-            s0, s1 = self.be.event(), self.be.event()
-            s0.record()
-            write(buf)
-            s1.record()
-            s1.synchronize()
-            return s0.elapsed_time(s1)
-
-        out, times, best = pick_output_buffer(lambda: T.empty(n, dtype=T.float64, device=self.be.dev), timed, k,
-                                              8 * n, self.OUT_FAST_GBS)
-        if not self.covers_outputs():  # outputs no kernel of the knit writes stay zero (as _alloc_out)
-            out.zero_()
-        T.cuda.empty_cache()  # the other candidates' blocks back to the device
-        self.out_placement = {"candidates": len(times), "write_ms": [round(t, 4) for t in times], "chosen": best}
-        return out
+    # The output buffer (round 4): the write kernel's rate depended on the 2^N buffer's placement — 4.8
+    # or 5.9 ms for the same kernel into different 34 GB hipMalloc blocks — and round 3 timed up to six
+    # candidate allocations to keep a fast one. The slow mode follows the virtual-to-physical mapping, not
+    # the memory: the same writes into buffers mapped from 1-GiB physical allocations at 1-GiB-aligned
+    # addresses run at 4.83-4.86 ms whichever of the device's memory backs them (tools/write_probe10,
+    # DESIGN.md §4). Large outputs are therefore allocated that way (qk_out_alloc, engine.out_buffer);
+    # small ones (< 1 GiB) from torch.
 
     def _alloc_out(self, mats):
-        T = self.T
+        """This rank's output buffer: 2^N entries (single / reduce), its slice (slice mode), or its block
+        of output rows (gather mode, zeroed). Zero-filled unless every output is written by the knit."""
         if self.mode == "slice":
-            return self.be.zeros((self.slice[1],), T.float64)
-        if self.mode != "gather":
-            return self.be.zeros((1 << self.N,), T.float64)
-        lo, hi = self.row_block
-        width_b = mats[self.order[-1]].shape[1]
-        return self.be.zeros((max(hi - lo, 1) * width_b,), T.float64)
+            n = self.slice[1]
+        elif self.mode != "gather":
+            n = 1 << self.N
+        else:
+            lo, hi = self.row_block
+            n = max(hi - lo, 1) * mats[self.order[-1]].shape[1]
+        return self.new_out(n, zero=self.mode == "gather" or not self.covers_outputs())
+
+    def new_out(self, n: int, zero: bool = False):
+        """A fresh [n] fp64 device buffer for the knit output (engine.out_buffer: 1-GiB-mapped when
+        large; a host backend's own allocation in the CPU tests). ``self.out_alloc`` records how."""
+        alloc = getattr(self.be, "out_buffer", None)
+        if alloc is None:
+            self.out_alloc = "backend"
+            return self.be.zeros((n,), self.T.float64) if zero else self.be.empty((n,), self.T.float64)
+        out, owner = alloc(n)
+        self.out_alloc = "qk_out_alloc (1-GiB mapped chunks)" if owner is not None else "torch"
+        self._last_owner = owner
+        if zero:
+            out.zero_()
+        return out
+
+    def take_out(self):
+        """The output buffer of one drop-in call (run.run_virtual_circuit): the previous call's mapping
+        again once the caller has dropped every tensor over it (the reference returns a fresh result
+        per call, and mapping 34 GB costs milliseconds), else a new buffer."""
+        n = self.slice[1] if self.mode == "slice" else 1 << self.N
+        zero = not self.covers_outputs()
+        own = getattr(self, "_call_owner", None)
+        if own is not None and own.n == n and not own.in_use():
+            out = own.tensor()
+            if zero:
+                out.zero_()
+            return out
+        out = self.new_out(n, zero=zero)
+        self._call_owner = self._last_owner
+        return out
 
     def _contract(self, mats, skip=None):
         if self.mode != "gather":

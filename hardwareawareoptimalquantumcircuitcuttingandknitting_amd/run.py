@@ -110,27 +110,27 @@ _PLANS: OrderedDict = OrderedDict()
 _PLANS_LOCK = threading.Lock()
 
 
+def _param_key(p):
+    """A parameter as hashed by circuit_fingerprint: arrays by dtype, shape and bytes (their repr
+    rounds to 8 digits and elides long arrays), everything else by repr."""
+    if isinstance(p, np.ndarray):
+        return ("nd", p.dtype.str, p.shape, hashlib.sha1(np.ascontiguousarray(p).tobytes()).hexdigest())
+    return repr(p)
+
+
 def circuit_fingerprint(virt: VirtualCircuit) -> str:
     """Content hash of a cut circuit as the sweep and knit see it: every fragment circuit's
     operations (name, parameters, qubit and global clbit positions; for virtual-gate endpoints the
     gate type, its parameters and the endpoint side) and the output width. Two ``VirtualCircuit``
     objects built from the same cut share it, so a repeated ``run_virtual_circuit`` reuses the
-    compiled plan. Cached on the ``VirtualCircuit`` per mutation generation (``_generation``) and on
-    the caller's cut circuit object while its instruction list is the same length (the reference
-    rebuilds a ``VirtualCircuit`` from the same cut circuit on every call, ``Utilities.py:74-79``)."""
+    compiled plan. Cached on the ``VirtualCircuit`` per mutation generation (``_generation``) only:
+    the caller's circuit can be edited in place between calls (``cut.data[i] = ...`` keeps the list
+    and its length), so every new ``VirtualCircuit`` hashes its fragments again (syc 32 5: ~2 ms,
+    against the ~0.3 s the reference spends rebuilding it per call, ``Utilities.py:74-79``)."""
     gen = getattr(virt, "_generation", 0)
     cached = getattr(virt, "_qk_fingerprint", None)
     if cached is not None and cached[0] == gen:
         return cached[1]
-    src = getattr(virt, "_source", None)
-    data = getattr(src, "data", None)
-    stamp = (id(data), len(data)) if isinstance(data, list) else None
-    if stamp is None or stamp != getattr(virt, "_source_stamp", None):
-        stamp = None  # the source changed since this VirtualCircuit was built: hash the fragments only
-    on_src = getattr(src, "_qk_fingerprint", None) if stamp is not None else None
-    if on_src is not None and on_src[0] == stamp:
-        virt._qk_fingerprint = (gen, on_src[1])
-        return on_src[1]
     h = hashlib.sha1()
     circ = virt.circuit
     h.update(repr((circ.num_qubits, circ.num_clbits, len(virt.vgate_instructions))).encode())
@@ -138,20 +138,15 @@ def circuit_fingerprint(virt: VirtualCircuit) -> str:
         h.update(repr(("frag", frag.name, len(frag))).encode())
         for instr in fcirc:
             op = instr.operation
-            item = [op.name, tuple(repr(p) for p in getattr(op, "params", ())),
+            item = [op.name, tuple(_param_key(p) for p in getattr(op, "params", ())),
                     tuple(fcirc.find_qubit(q) for q in instr.qubits), tuple(fcirc.find_clbit(c) for c in instr.clbits)]
             vg = getattr(op, "_virtual_gate", None)
             if vg is not None:
                 item += [op.vgate_idx, op.qubit_idx, type(vg).__name__,
-                         tuple(repr(p) for p in getattr(vg, "_params", getattr(vg, "params", ())))]
+                         tuple(_param_key(p) for p in getattr(vg, "_params", getattr(vg, "params", ())))]
             h.update(repr(item).encode())
     fp = h.hexdigest()
     virt._qk_fingerprint = (gen, fp)
-    if stamp is not None:
-        try:  # the next VirtualCircuit of this same (unmodified) circuit object reuses it
-            src._qk_fingerprint = (stamp, fp)
-        except AttributeError:
-            pass
     return fp
 
 
@@ -204,14 +199,8 @@ def _planned_dense(virt: VirtualCircuit, device: int, out):
     now = perf_counter()
     pipe = cached_plan(virt, device)
     pipe.be.bind()
-    # first call of a single-GPU data-rank plan: the pipeline places the output itself (the fastest of a
-    # few allocations for its write, pipeline._place_out); later calls get that block back from torch's
-    # caching allocator once the caller has dropped the previous result
-    place = out is None and pipe.mode == "single" and pipe.dev_rank and not getattr(pipe, "_placed", False)
-    if out is None and not place:
-        n = pipe.slice[1] if pipe.mode == "slice" else 1 << pipe.N
-        alloc = T.empty if pipe.covers_outputs() else T.zeros
-        out = alloc(n, dtype=T.float64, device=T.device("cuda", device))
+    if out is None:  # 1-GiB-mapped when large; the previous call's mapping once the caller dropped it
+        out = pipe.take_out()
     e0, e1 = T.cuda.Event(enable_timing=True), T.cuda.Event(enable_timing=True)
     host = perf_counter() - now
     e0.record()

@@ -46,11 +46,6 @@ class VirtualCircuit:
     def __init__(self, circuit: QuantumCircuit) -> None:
         from .ingest import adopt_with_map
 
-        # the caller's circuit object: run_virtual_circuit's plan cache keeps the content hash on it,
-        # so VirtualCircuits rebuilt from the same cut per call (Utilities.py:74-79) skip re-hashing
-        self._source = circuit
-        data = getattr(circuit, "data", None)
-        self._source_stamp = (id(data), len(data)) if isinstance(data, list) else None
         # a foreign (qiskit) cut circuit is rebuilt in this IR; its registers stay valid keys
         circuit, self._frag_alias = adopt_with_map(circuit)
         self._vgate_instrs = [instr for instr in circuit if _is_vgate(instr.operation)]
@@ -131,7 +126,6 @@ class VirtualCircuit:
     def replace_fragment_circuit(self, fragment, circuit: QuantumCircuit) -> None:
         self._frag_circs[self._frag(fragment)] = circuit
         self._generation += 1
-        self._source = None  # the fragments no longer follow from the source circuit alone
 
     def get_backend(self, fragment):
         fragment = self._frag(fragment)

@@ -104,6 +104,17 @@ int qk_stream_destroy(void* stream);
 int qk_stream_cu_count(int device, void* stream, int* cus);
 const char* qk_version(void);
 
+/* Output buffers for the write-bound knit kernels (qknit_mem.hip): at least `bytes` of device memory
+ * built from 1-GiB physical allocations (hipMemCreate) mapped read-write at a 1-GiB-aligned virtual
+ * address (below 1 GiB: one allocation at its power-of-two alignment). The 2^32-entry knit writes at
+ * 4.83-4.86 ms into every such buffer and at 4.8 or 5.9 ms into plain hipMalloc blocks, depending
+ * on the block. Replaces the output dict the reference allocates per merge
+ * (quasi_distr.py:55-60): the caller owns the buffer; qk_out_free synchronizes the device and
+ * unmaps it. qk_out_mapped_bytes: the mapped size of a qk_out_alloc pointer (QK_EARG otherwise). */
+int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr);
+int qk_out_free(qk_ctx* ctx, void* ptr);
+int qk_out_mapped_bytes(const void* ptr, int64_t* bytes);
+
 /* Workspace (bytes) qk_sweep needs for n_jobs jobs of prog (0 in PACKED mode). */
 int qk_sweep_workspace_bytes(const qk_program* prog, int64_t n_jobs, int64_t* bytes);
 
@@ -215,6 +226,12 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
                                const int32_t* k_dev, double* out);
 
 /* out[k][i + j*M] = A[k*lda + i] * B[k*ldb + j] */
+/* The kernel qk_knit_outer_stream_range launches for these arguments (no launch): *kind = 0 the
+ * per-output gather kernel (qk_knit_outer_stream_kernel), 1 the blocked kernel with A and B staged in
+ * LDS (qk_knit_outer_blocked_kernel<false>), 2 the blocked kernel reading B from global memory
+ * (<true>); *task_bits = log2 outputs per blocked task (0 for kind 0). */
+int qk_knit_outer_stream_kind(int nbits, int64_t K, uint64_t maskA, uint64_t maskB, int64_t o_begin,
+                              int64_t o_count, int* kind, int* task_bits);
 int qk_khatri_rao(qk_ctx* ctx, int64_t K, int64_t M, int64_t N, const double* A, int64_t lda,
                   const double* B, int64_t ldb, double* out);
 

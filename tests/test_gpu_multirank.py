@@ -175,9 +175,9 @@ def test_multi_rank_hip_overlapped_steps_match_oracle(case, world, veto, monkeyp
     i's write: the multi-GPU bench default) in slice mode on 4-8 ranks sharing the GPU, twice in a
     row, against the oracle at 1e-12: hwe (compressed every step), cx_8x8 (rank > 8: the exact slice
     with its all-gathers), and a probe check rejecting on one rank only (every rank takes the exact
-    slice together). Every rank places its slice among several output buffers (QKNIT_OUT_MIN_BYTES=0:
-    the first, plain step times the write into each candidate and keeps one)."""
-    monkeypatch.setenv("QKNIT_OUT_MIN_BYTES", "0")
+    slice together). Every rank's slice is a qk_out_alloc mapping (QKNIT_OUT_MAPPED_MIN_BYTES=0: small
+    outputs mapped too)."""
+    monkeypatch.setenv("QKNIT_OUT_MAPPED_MIN_BYTES", "0")
     sys.path.insert(0, HERE)
     from oracle import dense
 

@@ -434,16 +434,39 @@ def test_circuit_fingerprint_keys_the_plan_cache():
     _, angle = circuits.two_fragment("rzz", angle=0.3)
     _, angle2 = circuits.two_fragment("rzz", angle=0.4)
     assert circuit_fingerprint(VirtualCircuit(angle)) != circuit_fingerprint(VirtualCircuit(angle2))
-    assert getattr(cut, "_qk_fingerprint", None) is not None  # kept on the caller's circuit object
     grown = VirtualCircuit(cut)
     cut.h(cut.qubits[0])  # the same object, one instruction more: hashed again
     assert circuit_fingerprint(VirtualCircuit(cut)) != circuit_fingerprint(grown)
+    # an in-place edit of the same length (same list object): a new VirtualCircuit hashes again
+    i = next(j for j, ins in enumerate(cut.data) if ins.operation.name == "h")
+    before_edit = circuit_fingerprint(VirtualCircuit(cut))
+    ins = cut.data[i]
+    cut.data[i] = ins.replace(operation=type(ins.operation)("x", 1, []))
+    assert circuit_fingerprint(VirtualCircuit(cut)) != before_edit
+    cut.data[i] = ins
+    assert circuit_fingerprint(VirtualCircuit(cut)) == before_edit
     before = circuit_fingerprint(a)
     frag = next(f for f in a.fragment_circuits if len(f))
     fc = a.fragment_circuits[frag].copy()
     fc.h(fc.qubits[0])
     a.replace_fragment_circuit(frag, fc)
     assert circuit_fingerprint(a) != before
+
+
+def test_circuit_fingerprint_hashes_array_params_by_content():
+    """Matrix-valued parameters are hashed by dtype, shape and bytes: two unitaries that repr() prints
+    alike (8 digits; long arrays elided) still get different fingerprints (plan-cache key)."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.run import _param_key
+
+    a = np.eye(2) * (1 + 1e-12)
+    b = np.eye(2)
+    assert repr(a) == repr(b) and _param_key(a) != _param_key(b)
+    big = np.zeros(4096)
+    big2 = big.copy()
+    big2[2000] = 1e-9
+    assert repr(big) == repr(big2) and _param_key(big) != _param_key(big2)
+    assert _param_key(np.float32(1.0).reshape(())) != _param_key(np.float64(1.0).reshape(()))
+    assert _param_key(0.5) == repr(0.5)
 
 
 def test_traced_qubits_beyond_final_tile_widen_and_fold():
@@ -473,31 +496,3 @@ def test_traced_qubits_beyond_final_tile_widen_and_fold():
         ref, _ = dense.fragment_q(view, list(frag))
         np.testing.assert_allclose(q, ref, atol=1e-12, rtol=0)
     assert seen
-
-
-def test_output_placement_search_stops_at_first_fast_buffer():
-    """pick_output_buffer (the pipeline's output placement): every candidate is written
-    twice (warm, then timed), all are held until the search ends, it stops at the first buffer
-    written at the fast rate, and returns the fastest one seen."""
-    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import pick_output_buffer
-
-    nbytes = 8 << 32  # 2^32 fp64 outputs: 6.5 TB/s is 5.29 ms
-    for script, k, want_n, want_best in (
-            ([5.8, 5.9, 4.9, 4.8], 6, 3, 2),      # third candidate fast: stop there
-            ([5.8, 5.85, 5.9], 3, 3, 0),          # none fast: all k tried, the fastest kept
-            ([4.85], 6, 1, 0),                    # first fast
-            ([5.9, 5.7, 5.8, 5.95, 5.75, 5.72], 6, 6, 1)):
-        held, calls = [], []
-
-        def alloc():
-            held.append(object())
-            return held[-1]
-
-        def timed(buf, it=iter([t for t in script for _ in (0, 1)])):
-            calls.append(buf)
-            return next(it)
-
-        out, times, best = pick_output_buffer(alloc, timed, k, nbytes, 6500.0)
-        assert len(times) == want_n and len(held) == want_n and best == want_best
-        assert out is held[best] and times == script[:want_n]
-        assert calls == [b for b in held for _ in (0, 1)]  # each written twice, in order

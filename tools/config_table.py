@@ -73,8 +73,8 @@ def run(key, steps):
     row["light_cone_terms"] = counts.get("labels")
     row["rank_fallbacks"] = getattr(pipe, "rank_fallbacks", None)
     row["knit_kernel"] = pipe.last_kernel or "qk_gemm_keyed (smallk / glds / keyed by shape)"
-    if getattr(pipe, "out_placement", None):  # output placement (pipeline._place_out_with): write ms per candidate
-        row["out_placement"] = pipe.out_placement
+    if getattr(pipe, "out_alloc", None):  # how the output buffer was allocated (pipeline.new_out)
+        row["out_alloc"] = pipe.out_alloc
     if K > 8:
         row["knit_mfma_frac"] = 2.0 * M * N * K / (knit_ms * 1e-3) / 1e12 / MFMA
     else:
