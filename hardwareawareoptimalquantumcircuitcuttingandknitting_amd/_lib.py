@@ -99,6 +99,9 @@ SIGNATURES = {
     "qk_npd_workspace_bytes": (c_i32, [c_i64, c_i64, ctypes.POINTER(c_i64)]),
     "qk_threshold_count": (c_i32, [c_vp, c_i64, c_vp, ctypes.c_double, c_vp, c_i64, c_vp]),
     "qk_npd": (c_i32, [c_vp, c_i64, c_vp, ctypes.c_double, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "qk_qd_from_rows": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, ctypes.c_double, c_vp]),
+    "qk_qd_merge": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, ctypes.c_double, c_i64, c_vp]),
+    "qk_qd_axpby": (c_i32, [c_vp, c_i64, ctypes.c_double, c_vp, ctypes.c_double, c_vp, ctypes.c_double, c_vp]),
     "qk_hellinger": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     "qk_knit_lowrank_workspace_bytes": (c_i32, [c_vp, c_vp, ctypes.POINTER(c_i64)]),
     "qk_knit_lowrank": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),

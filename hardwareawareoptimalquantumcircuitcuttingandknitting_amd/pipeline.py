@@ -929,14 +929,10 @@ class KnitPipeline:
         # column blocks cover all of R; the ranks' factors are identical, so the local ranks are r or 0).
         # A rejection anywhere makes every rank take the exact slice, whose collectives then match.
         dist.all_reduce(k_eff, op=dist.ReduceOp.MIN, group=self.group)
-        on_gpu = k_eff.device.type == "cuda"
-        pinned = T.empty(1, dtype=T.int32, pin_memory=on_gpu)
-        pinned.copy_(k_eff, non_blocking=on_gpu)
-        ready = T.cuda.Event() if on_gpu else None
-        if on_gpu:
-            ready.record()
-        return {"A2": A2, "B2": B2, "k_eff": k_eff, "XA": XA, "XB": XB, "pinned": pinned, "ready": ready,
-                "mats": mats}
+        # the exact slice's operands, gathered every step (the same collectives on every rank whatever
+        # the verdict; the contraction itself is predicated on the device, _launch_slice)
+        ex = self._slice_exact_operands(XA, XB)
+        return {"A2": A2, "B2": B2, "k_eff": k_eff, "exact": ex, "mats": mats}
 
     def _launch_slice(self, p: dict):
         be = self.be
@@ -952,10 +948,10 @@ class KnitPipeline:
         if self.record_events:
             end.record()
             self.events.append((start, end))
-        if p["ready"] is not None:
-            p["ready"].synchronize()  # the check only, not the knit queued behind it
-        if int(p["pinned"][0]) == 0:
-            self._slice_exact(p["XA"], p["XB"], cA, cB)
+        # exact contraction of this slice, predicated on the device: runs only when the (MIN-reduced)
+        # accepted rank is 0 — no host round trip, the verdict is read later by sync_stats
+        A, kA, B, kB = p["exact"]
+        be.gemm_keyed(A, B, keyA=kA, keyB=kB, out=self.out, skip=p["k_eff"])
         return self.out
 
     # ------------------------------------------------------------------ overlapped steps
@@ -1038,7 +1034,7 @@ class KnitPipeline:
             be.bind()
             for k in ("A2", "B2", "k_eff"):
                 p[k].record_stream(W)
-            for m in p["mats"]:
+            for m in list(p["mats"]) + list(p.get("exact", ())):
                 if m is not None:
                     m.record_stream(W)
             out = self._launch_slice(p) if self.mode == "slice" else self._launch_dev_rank(p)
@@ -1052,30 +1048,51 @@ class KnitPipeline:
 
         return 0 if self.group is None else dist.get_global_rank(self.group, 0)
 
-    def _slice_exact(self, XA, XB, cA, cB):
-        """Exact contraction of this rank's output slice (K terms) from all-gathered operand blocks."""
+    def _slice_exact_plan(self):
+        """Per side of the exact slice contraction: (the output bits' column range [base, base + n) of
+        that side this rank's slice reads, whether it is the rank's own column block, device keys of
+        those columns relative to the slice start). Built once."""
+        if getattr(self, "_exact_plan", None) is None:
+            from .knit_plan import deposit_keys
+
+            o_begin, o_count = self.slice
+            plan = []
+            for i in (self.order[0], self.order[-1]):
+                cl = self.ops.clbits[i]
+                m = sum(1 << c for c in cl)
+                n = 1 << bin(m & (o_count - 1)).count("1")
+                base = _pext(o_begin, m)
+                w = 1 << len(cl)
+                local = n == w // self.world and base == self.rank * n
+                keys = deposit_keys(list(cl))[base:base + n] - (o_begin & m)
+                plan.append((base, n, local, self.be.to_device(np.ascontiguousarray(keys))))
+            self._exact_plan = plan
+        return self._exact_plan
+
+    def _slice_exact_operands(self, XA, XB):
+        """(A, keyA, B, keyB) of this rank's exact slice from the transformed column blocks ``XA`` /
+        ``XB`` [K, w / P]: a side whose columns are this rank's own block is used as it is, the other
+        side is all-gathered (syc 32 at 2-8 ranks: the slice's fixed output bits are A's top bits, so
+        only B travels, K x 2^16 doubles per step)."""
         import torch.distributed as dist
 
-        from .knit_plan import deposit_keys
+        T, P = self.T, self.world
+        out = []
+        for X, (base, n, local, keys) in zip((XA, XB), self._slice_exact_plan()):
+            if not local:
+                K, bw = X.shape
+                g = T.empty((P * K * bw,), dtype=X.dtype, device=X.device)
+                dist.all_gather_into_tensor(g, X.contiguous().reshape(-1), group=self.group)
+                X = g.view(P, K, bw).permute(1, 0, 2).reshape(K, P * bw)[:, base:base + n].contiguous()
+            out += [X, keys]
+        return tuple(out)
 
-        T, be, P = self.T, self.be, self.world
-        o_begin, o_count = self.slice
-        full = []
-        for X in (XA, XB):
-            g = T.empty((P * X.shape[0], X.shape[1]), dtype=X.dtype, device=X.device)
-            dist.all_gather_into_tensor(g, X.contiguous(), group=self.group)
-            full.append(g.view(P, X.shape[0], X.shape[1]).permute(1, 0, 2).reshape(X.shape[0], -1))
-        mA, mB = sum(1 << c for c in cA), sum(1 << c for c in cB)
-        low = o_count - 1
-        cols = []
-        for X, m, cl in ((full[0], mA, cA), (full[1], mB, cB)):
-            n_lo = bin(m & low).count("1")
-            base = _pext(o_begin, m)
-            keys = deposit_keys(list(cl))[base:base + (1 << n_lo)] - (o_begin & m)
-            cols.append((X[:, base:base + (1 << n_lo)].contiguous(), be.to_device(np.ascontiguousarray(keys))))
-        (A, kA), (B, kB) = cols
+    def _slice_exact(self, XA, XB, cA, cB):
+        """Exact contraction of this rank's output slice (K terms) from the transformed column blocks
+        (the slice path without data rank); collectives as :meth:`_slice_exact_operands`."""
+        A, kA, B, kB = self._slice_exact_operands(XA, XB)
         self.last_kernel = None
-        return be.gemm_keyed(A, B, keyA=kA, keyB=kB, out=self.out)
+        return self.be.gemm_keyed(A, B, keyA=kA, keyB=kB, out=self.out)
 
     def sync_stats(self):
         """Read back the ranks / acceptances of the steps since the last call (host sync):

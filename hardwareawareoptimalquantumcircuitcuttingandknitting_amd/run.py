@@ -309,13 +309,46 @@ def run_virtual_circuit_sharded(virt: VirtualCircuit, group=None, *, device: int
     return (out if rank == 0 else None), RunTimeInfo(run_time, knit_time, (0, n) if rank == 0 else (0, 0))
 
 
+def _run_reference_truncated(virt: VirtualCircuit, device: int, dense: bool):
+    """``truncation="reference"``: the reference's knit with ``ACCURACY`` applied after every
+    operation (truncated.knit_reference_truncated), then nearest_probability_distribution."""
+    from .truncated import knit_reference_truncated
+
+    if not all(isinstance(virt.get_backend(f), MI355XBackend) for f in virt.fragment_circuits if len(f)):
+        raise ValueError("truncation='reference' needs every fragment on the MI355X backend")
+    log.info("Running virtualizer with %d %s fragments and %d vgates (reference truncation)...",
+             len(virt.fragment_circuits), tuple(len(f) for f in virt.fragment_circuits), len(virt.vgate_instructions))
+    now = perf_counter()
+    out = knit_reference_truncated(virt, device, _qd.ACCURACY)
+    _sync(device)
+    info = RunTimeInfo(0.0, perf_counter() - now)
+    log.info("Knitted in %.2fs.", info.knit_time)
+    if dense:
+        return out, info
+    keys, vals = engine.nearest_probability_distribution(engine.get_context(device), out, _qd.ACCURACY)
+    return dict(zip(keys.tolist(), vals.tolist())), info
+
+
 def run_virtual_circuit(virt: VirtualCircuit, shots: int = 20000, *, device: int = 0,
                         dense: bool = False, factored: bool | None = None, sample: bool = False, seed: int = 0,
-                        group=None):
+                        group=None, truncation: str = "final"):
     """Reference-compatible entry point (``run.py:23-71``). ``group`` (a ``torch.distributed``
     process group, e.g. ``dist.group.WORLD``) runs it on every rank of the group
     (:func:`run_virtual_circuit_sharded`): ``dense=True`` returns the rank's shard, otherwise every
-    rank returns the whole reference-shaped dict (outputs of at most 24 clbits)."""
+    rank returns the whole reference-shaped dict (outputs of at most 24 clbits).
+
+    ``truncation``: ``"final"`` (default) knits exactly and applies ``ACCURACY`` once, to the result;
+    ``"reference"`` applies it after every operation as the reference's ``QuasiDistr`` dicts do
+    (``quasi_distr.py:7-10``: from_counts, every merge, every per-gate ``+ - *``), on exact instance
+    distributions, single GPU, at most 24 clbits (``dense=True``: the knit before NPD)."""
+    if truncation not in ("final", "reference"):
+        raise ValueError(f"truncation must be 'final' or 'reference', not {truncation!r}")
+    if truncation == "reference":
+        if group is not None or sample or factored is not None:
+            raise ValueError("truncation='reference': single GPU, exact instances, the direct knit")
+        if virt.circuit.num_clbits > 24:
+            raise ValueError("truncation='reference' is for outputs of at most 24 clbits")
+        return _run_reference_truncated(virt, device, dense)
     if group is not None:
         if sample:
             raise ValueError("multi-GPU runs sweep exact instances (sample=True: single GPU)")

@@ -31,6 +31,12 @@ from .quasi_distr import QuasiDistr
 RZZ_ACCURACY = 0.00001
 
 
+def _zero_like(r):
+    """The empty accumulator of a knit: ``QuasiDistr({})`` for the dict results of the reference
+    interface, ``r.zero_like()`` for device results (truncated.DenseQD)."""
+    return r.zero_like() if hasattr(r, "zero_like") else QuasiDistr({})
+
+
 def _inst(side0=(), side1=()) -> QuantumCircuit:
     """Build a 2-qubit / 1-clbit instantiation circuit from per-side op lists.
 
@@ -134,7 +140,7 @@ class VirtualMove(VirtualBinaryGate):
         ]
 
     def knit(self, results: list[QuasiDistr], clbit_idx: int) -> QuasiDistr:
-        acc = QuasiDistr({})
+        acc = _zero_like(results[0])
         for sign, r in zip(self._SIGNS, results):
             term = self._signed(r, clbit_idx)
             acc = acc + term if sign > 0 else acc - term
@@ -190,7 +196,7 @@ class VirtualCZ(VirtualBinaryGate):
         ]
 
     def knit(self, results: list[QuasiDistr], clbit_idx: int) -> QuasiDistr:
-        acc = QuasiDistr({})
+        acc = _zero_like(results[0])
         for sign, r in zip(self._SIGNS, results):
             term = self._signed(r, clbit_idx)
             acc = acc + term if sign > 0 else acc - term

@@ -411,6 +411,23 @@ int qk_npd_pairs(qk_ctx* ctx, int64_t count, const int64_t* keys, const double* 
 
 /* acc3[0] = sum sqrt(max(p,0) max(q,0)), acc3[1] = sum max(p,0), acc3[2] = sum max(q,0) (device).
  * Hellinger fidelity = (acc3[0] / sqrt(acc3[1] acc3[2]))^2 (Utilities.py:222-224). */
+/* Reference truncation semantics (qknit_trunc.hip): dense quasi-distributions whose entries with
+ * |v| <= acc are zero after every operation, as the reference's QuasiDistr drops them from its dict on
+ * every construction (quasi_distr.py:7-10). One rounding per reference operation.
+ *   qk_qd_from_rows  out[dst[r] * width + x] = trunc(rows[r * width + x])       (from_counts, :12-20)
+ *   qk_qd_merge      out = 0, then out[ka[i] ^ kb[j]] = trunc(a[i] * b[j]) for every nonzero product
+ *                    (ka / kb NULL: identity keys): the dict merge of :55-60, whose entries are the
+ *                    kept products; two nonzero products must not share a key
+ *   qk_qd_axpby      out[i] = trunc(alpha * a[i] + beta * b[i]) as fma(alpha, a, beta * b): +, - with
+ *                    (1, +-1), scalar * with (s, 0) (:62-86 and the per-gate knits,
+ *                    virtual_gates.py:105-124,179-194,262-286) */
+int qk_qd_from_rows(qk_ctx* ctx, int64_t n_rows, int64_t width, const double* rows, const int64_t* dst, double acc,
+                    double* out);
+int qk_qd_merge(qk_ctx* ctx, int64_t na, const double* a, const int64_t* ka, int64_t nb, const double* b,
+                const int64_t* kb, double acc, int64_t n_out, double* out);
+int qk_qd_axpby(qk_ctx* ctx, int64_t n, double alpha, const double* a, double beta, const double* b, double acc,
+                double* out);
+
 int qk_hellinger(qk_ctx* ctx, int64_t n, const double* p, const double* q, double* acc3);
 
 #ifdef __cplusplus

@@ -210,3 +210,78 @@ def test_generators_match_reference():
     assert ops_of(generators.sycamore(12, 2)) == gold_ops(gold["syc_12_2"])
     assert ops_of(generators.hwea(16, 1)) == gold_ops(gold["hwe_16_1"])
     assert ops_of(generators.bernstein_vazirani(5)) == gold_ops(gold["bv_5"])
+
+
+class _HostDenseQD:
+    """numpy model of truncated.DenseQD (the reference-truncation GPU path): the same operations,
+    one rounding each (a +- b, s * a), truncation |v| <= acc -> 0 after every one."""
+
+    def __init__(self, t, nbits, acc):
+        self.t, self.nbits, self.acc = t, nbits, acc
+
+    def _tr(self, v):
+        return _HostDenseQD(np.where(np.abs(v) > self.acc, v, 0.0), self.nbits, self.acc)
+
+    def zero_like(self):
+        return _HostDenseQD(None, None, self.acc)
+
+    def split(self, bit):
+        assert bit == self.nbits - 1
+        h = self.t.size // 2
+        return _HostDenseQD(self.t[:h], self.nbits - 1, self.acc), _HostDenseQD(self.t[h:], self.nbits - 1, self.acc)
+
+    def __add__(self, o):
+        return o if self.t is None else self._tr(self.t + o.t)
+
+    def __sub__(self, o):
+        return o._tr(-o.t) if self.t is None else self._tr(self.t - o.t)
+
+    def __mul__(self, s):
+        return self._tr(self.t * float(s))
+
+    __rmul__ = __mul__
+
+
+@pytest.mark.parametrize("path", KNIT_FILES, ids=[os.path.basename(p)[5:-5] for p in KNIT_FILES])
+def test_dense_truncated_knit_model_matches_reference_knit(path):
+    """The algorithm of run_virtual_circuit(truncation="reference") (truncated.knit_label_tree: dense
+    vectors over N + V key bits, leaf merges, the package's per-gate knit rules on dense operands,
+    depth-first over the label tree) on the reference's own inputs at ACCURACY 1e-5 reproduces the
+    reference VirtualCircuit.knit (golden knit_acc_1e-05) key for key within 1e-15."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.truncated import knit_label_tree
+
+    acc = 1e-5
+    gold = json.load(open(path))
+    _, cut = _case_circuits(gold["case"])
+    view = qvm.CutView(cut)
+    virt = VirtualCircuit(cut)
+    vgates = [i.operation for i in virt.vgate_instructions]
+    N, V = view.num_clbits, len(vgates)
+    frags = [list(r) for r in view.qregs if len(r)]
+    inputs = {fi: [{k: v for k, v in _items(x) if abs(v) > acc} for x in gold["inputs"][str(fi)]]
+              for fi in range(len(frags)) if str(fi) in gold["inputs"]}
+    touches = {fi: [bool(set(vg.qubits) & set(frags[fi])) for vg in virt.vgate_instructions] for fi in inputs}
+    index = {fi: {lab: r for r, lab in enumerate(view.labels(frags[fi]))} for fi in inputs}
+
+    def leaf(label):
+        merged = None
+        for fi in sorted(inputs):
+            flab = tuple(label[j] if touches[fi][j] else -1 for j in range(V))
+            d = inputs[fi][index[fi][flab]]
+            if merged is None:
+                merged = d
+            else:
+                merged = {k1 ^ k2: v1 * v2 for k1, v1 in merged.items() for k2, v2 in d.items()}
+                merged = {k: v for k, v in merged.items() if abs(v) > acc}
+        t = np.zeros(1 << (N + V))
+        for k, v in merged.items():
+            t[k] = v
+        return _HostDenseQD(t, N + V, acc)
+
+    out = knit_label_tree(vgates, N, leaf).t
+    ref = dict(_items(gold["knit_acc_1e-05"]))
+    got = {int(k): float(out[k]) for k in np.flatnonzero(out)}
+    assert set(got) == set(ref)
+    for k in ref:
+        assert got[k] == pytest.approx(ref[k], abs=1e-15, rel=1e-12)

@@ -196,8 +196,8 @@ def test_multi_rank_hip_overlapped_steps_match_oracle(case, world, veto, monkeyp
         assert incompressible == 2
 
 
-def _syc_worker(rank, world, port, q):
-    log = _watchdog(rank, "syc_32_5", after=400)
+def _syc_worker(rank, world, port, q, overlap=False):
+    log = _watchdog(rank, f"syc_32_5_{world}", after=700)
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -214,12 +214,17 @@ def _syc_worker(rank, world, port, q):
         virt = VirtualCircuit(cut)
         pipe = KnitPipeline(virt, device=0, rank=rank, world=world, factored=True)
         assert pipe.mode == "slice" and pipe.dev_rank
+        if overlap:  # pipelined steps (the multi-GPU bench default): a non-default caller stream
+            torch.cuda.set_stream(torch.cuda.Stream())
+            pipe.overlap = pipe.overlap_ok()
+            assert pipe.overlap
         log("planned")
         for it in range(2):
             sl = pipe.step()
             torch.cuda.synchronize()
             log(f"step {it}")
         pipe.sync_stats()
+        assert pipe.rank_fallbacks == 0 and pipe.last_rank is not None
         lo, cnt = pipe.slice
         total = torch.tensor([float(sl.sum())], dtype=torch.float64)
         mn = float(sl.min())
@@ -244,13 +249,16 @@ def _syc_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(500)
-def test_syc_32_5_slice_mode_two_ranks_equals_single_gpu():
-    """The bench workload's multi-GPU path (slice mode, device data rank, 2 ranks): each rank's
-    2^31-entry slice equals the same range of the single-GPU step within 1e-12, the slices sum to 1
-    and no entry is below -1e-13."""
-    total, err, mn, sl = _run(_syc_worker, 2, timeout=600)
-    assert sl == (0, 1 << 31)
+@pytest.mark.timeout(1000)
+@pytest.mark.parametrize("world,overlap", [(2, False), (8, True)])
+def test_syc_32_5_slice_mode_equals_single_gpu(world, overlap):
+    """The bench workload's multi-GPU path (slice mode, device data rank) at 2 ranks (plain steps) and
+    at 8 ranks with pipelined steps (the multi-GPU bench default, BASELINE config 5: syc 32 5 sharded
+    over 8 GPUs): each rank's 2^32 / world-entry slice equals the same range of the single-GPU step
+    within 1e-12, the slices sum to 1 and no entry is below -1e-13. The exact-slice fallback is
+    predicated on the device (no host sync in the step)."""
+    total, err, mn, sl = _run(_syc_worker, world, timeout=900, overlap=overlap)
+    assert sl == (0, (1 << 32) // world)
     assert err <= TOL
     assert abs(total - 1.0) <= 1e-10
     assert mn >= -1e-13
