@@ -367,9 +367,11 @@ def drop_in_timing(cut, ref_out, steps: int, device: int) -> dict:
     for i in range(0, out.numel(), chunk):
         diff = max(diff, float((out[i:i + chunk] - ref_out[i:i + chunk]).abs().max()))
     del out
-    times, infos = [], []
+    times, infos, builds = [], [], []
     for _ in range(max(steps, 3)):
-        virt = VirtualCircuit(cut)
+        tb = time.perf_counter()
+        virt = VirtualCircuit(cut)  # the reference builds one per call (Utilities.py:74-79)
+        builds.append(time.perf_counter() - tb)
         t0 = time.perf_counter()
         out, info = run_virtual_circuit(virt, dense=True, device=device)
         times.append(time.perf_counter() - t0)
@@ -400,7 +402,9 @@ def drop_in_timing(cut, ref_out, steps: int, device: int) -> dict:
             "steady_ms": float(sum(times) / len(times)) * 1e3, "steady_min_ms": min(times) * 1e3,
             "run_time_ms": float(sum(i.run_time for i in infos) / len(infos)) * 1e3,
             "knit_time_ms": float(sum(i.knit_time for i in infos) / len(infos)) * 1e3,
-            "calls": len(times), "max_abs_diff_vs_step": diff, "out_alloc": placement}
+            "calls": len(times), "max_abs_diff_vs_step": diff, "out_alloc": placement,
+            # host: VirtualCircuit(cut) per call (fragment circuits + the cut's content hash, the plan key)
+            "virtual_circuit_ms": float(sum(builds) / len(builds)) * 1e3}
 
 
 def npd_timing(dense, accuracy: float) -> dict:

@@ -125,8 +125,9 @@ def circuit_fingerprint(virt: VirtualCircuit) -> str:
     objects built from the same cut share it, so a repeated ``run_virtual_circuit`` reuses the
     compiled plan. Cached on the ``VirtualCircuit`` per mutation generation (``_generation``) only:
     the caller's circuit can be edited in place between calls (``cut.data[i] = ...`` keeps the list
-    and its length), so every new ``VirtualCircuit`` hashes its fragments again (syc 32 5: ~2 ms,
-    against the ~0.3 s the reference spends rebuilding it per call, ``Utilities.py:74-79``)."""
+    and its length), so every new ``VirtualCircuit`` hashes its fragments again — when it is built
+    (``VirtualCircuit.__init__``; syc 32 5: ~1.3 ms of the ~6 ms construction in the build container),
+    as the reference builds one per call (``Utilities.py:74-79``)."""
     gen = getattr(virt, "_generation", 0)
     cached = getattr(virt, "_qk_fingerprint", None)
     if cached is not None and cached[0] == gen:

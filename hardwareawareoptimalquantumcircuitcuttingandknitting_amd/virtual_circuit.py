@@ -60,6 +60,12 @@ class VirtualCircuit:
         # bumped by every mutation of fragments / backends: run_virtual_circuit's plan cache
         # (run.circuit_fingerprint) recomputes the circuit's fingerprint when it changes
         self._generation = 0
+        # the content hash of the cut as built (the plan-cache key): part of building the fragments,
+        # so a call of run_virtual_circuit on a fresh VirtualCircuit (the reference builds one per
+        # call, Utilities.py:74-79) finds its plan without hashing
+        from .run import circuit_fingerprint
+
+        circuit_fingerprint(self)
 
     def _frag(self, fragment):
         """Translate a caller's (possibly foreign) fragment register to the adopted one."""

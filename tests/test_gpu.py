@@ -681,13 +681,14 @@ def test_mapped_output_buffer_steps_match_oracle(T, case, monkeypatch):
     np.testing.assert_allclose(first.cpu().numpy(), ref, atol=1e-12, rtol=0)
     second = pipe.take_out()  # the first result is still held: a new mapping
     assert second.data_ptr() != p0
-    del first
-    third = pipe.take_out()  # ... the second one's owner is the call owner now
-    assert third.data_ptr() != p0
+    del first  # its mapping goes with it (no owner left)
+    third = pipe.take_out()  # the second result is still held: another new mapping
+    assert third.data_ptr() != second.data_ptr()
     owner = pipe._call_owner
+    assert owner.ptr == third.data_ptr()
     del second, third
     assert not owner.in_use()
-    assert pipe.take_out().data_ptr() == owner.ptr
+    assert pipe.take_out().data_ptr() == owner.ptr  # nothing holds it: handed out again
 
 
 @pytest.mark.slow
