@@ -59,6 +59,8 @@ SIGNATURES = {
     "qk_module_compile": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
                                   ctypes.POINTER(c_vp)]),
     "qk_module_destroy": (c_i32, [c_vp]),
+    "qk_module_load": (c_i32, [c_vp, c_vp, c_i64, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.POINTER(c_vp)]),
+    "qk_module_code": (c_i32, [c_vp, c_vp, ctypes.POINTER(c_i64)]),
     "qk_sweep_compiled": (c_i32, [c_vp, c_vp, ctypes.POINTER(QkProgram), c_i64, c_vp, c_vp, c_vp, c_i64,
                                   c_vp]),
     "qk_sweep_compiled_labels": (c_i32, [c_vp, c_vp, ctypes.POINTER(QkProgram), c_i64, c_vp, c_vp, c_i64, c_vp,

@@ -59,3 +59,49 @@ def build_library(force: bool = False, verbose: bool = False, out: str = OUT,
         raise RuntimeError(f"hipcc link failed:\n{' '.join(cmd)}\n{res.stderr}")
     os.replace(tmp, out)
     return out
+
+
+# BASELINE configs whose per-program kernels are compiled ahead of time (jit cache)
+AOT_CONFIGS = ("qft_16_1_p3", "syc_32_5_p2", "syc_32_1_p2", "syc_32_1_p2_forced", "hwe_16_1_p2", "hwe_16_1_p3")
+
+
+def build_jit_cache(configs=AOT_CONFIGS, verbose: bool = False) -> list:
+    """Compile the per-program sweep kernels the BASELINE configs' plans use (engine.jit_sources:
+    factored and direct plans) with ``hipcc --genco`` into engine.JIT_CACHE_DIR, so no plan of them
+    waits for hiprtc at run time (qft 16's 481 ops: ~7 s). Code objects already there are kept.
+    Returns the paths written."""
+    import tempfile
+
+    from . import VirtualCircuit, cutting, engine
+
+    todo = {}
+    for key in configs:
+        name, n, d, p, var = cutting.BASELINE_CONFIGS[key]
+        cut = cutting.config_cut_circuit(name, n, d, p, var)[1]
+        virt = VirtualCircuit(cut)
+        for basis in ({False, True} if virt.vgate_instructions else {False}):
+            for src, _ in engine.jit_sources(virt, basis=basis):
+                path = engine.jit_cache_path(src)
+                if not os.path.exists(path):
+                    todo[path] = src
+    os.makedirs(engine.JIT_CACHE_DIR, exist_ok=True)
+    procs = []
+    with tempfile.TemporaryDirectory() as tmp:
+        for i, (path, src) in enumerate(todo.items()):
+            f = os.path.join(tmp, f"prog{i}.hip")
+            with open(f, "w") as fh:
+                fh.write(src)
+            cmd = [hipcc(), "--genco", "--no-gpu-bundle-output", *engine.jit_options(src), f, "-o", path + ".tmp"]
+            procs.append((path, cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
+        errs = []
+        for path, cmd, proc in procs:
+            _, err = proc.communicate()
+            if proc.returncode != 0:
+                errs.append(f"{' '.join(cmd)}\n{err}")
+            else:
+                os.replace(path + ".tmp", path)
+                if verbose:
+                    print(f"jit cache: {path}")
+        if errs:
+            raise RuntimeError("hipcc --genco failed:\n" + "\n".join(errs))
+    return list(todo)

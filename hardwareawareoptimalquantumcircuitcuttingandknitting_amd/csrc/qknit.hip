@@ -1401,6 +1401,95 @@ __global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlocked
     }
 }
 
+// Rows form of the two-fragment knit (round 4), for masks whose B side holds the low C output bits
+// (syc 32 1: B = the 16 low bits, A the 16 high ones, K = 1): the output is cut into pieces of 2^C
+// consecutive entries; inside a piece the A index is fixed (pa = pext(piece, maskA >> C)) and the B
+// indices are one contiguous run (pb << C .. + 2^C, pb = pext(piece, maskB >> C)). A workgroup holds
+// its piece's B run in registers (lane: 2^(C - 9) adjacent pairs per k) and keeps it across the
+// pieces it writes while pb stays the same — with a grid of a multiple of the pb count, always, so B
+// is read once per workgroup — and multiplies by the piece's K scalars (scalar loads). The stores are
+// the blocked kernel's (each wave-store one 1-KiB run, a piece 2^(C+3) contiguous bytes); nothing is
+// staged in LDS and nothing re-read from L2 per output, where the B-from-global blocked form read B
+// from L2 for every output (syc 32 1: 5.55 ms, 0.77 of HBM, round 4 first measurement).
+// Outputs [o_begin, o_begin + o_count), piece-aligned, to out[o - o_begin]; kdev as the blocked kernel.
+struct OuterRowsArgs {
+    int K;
+    const double* __restrict__ A;
+    int64_t lda;
+    const double* __restrict__ B;
+    int64_t ldb;
+    uint32_t maskA_hi, maskB_hi;  // the masks shifted right by C
+    int64_t piece_begin, piece_end;
+    int64_t o_begin;
+    const int32_t* kdev;
+    double* __restrict__ out;
+};
+
+template <int KR, int C>
+__global__ __launch_bounds__(256) void qk_knit_outer_rows_kernel(OuterRowsArgs a) {
+    constexpr int NP = 1 << (C - 9);  // output pairs per lane per piece
+    int K = a.K;
+    if (a.kdev) {
+        const int kd = *a.kdev;
+        if (kd <= 0) return;
+        K = kd < K ? kd : K;
+    }
+    d2_t b[KR][NP];
+    int64_t pb_loaded = -1;
+    for (int64_t p = a.piece_begin + blockIdx.x; p < a.piece_end; p += gridDim.x) {
+        const uint32_t pl = (uint32_t)p;
+        const int64_t pb = pext32(pl, a.maskB_hi);
+        const uint32_t pa = pext32(pl, a.maskA_hi);
+        if (pb != pb_loaded) {  // uniform: the piece's B run into registers
+            const double* Bp = a.B + (pb << C) + 2 * threadIdx.x;
+#pragma unroll
+            for (int k = 0; k < KR; ++k)
+#pragma unroll
+                for (int i = 0; i < NP; ++i)
+                    b[k][i] = k < K ? *reinterpret_cast<const d2_t*>(Bp + k * a.ldb + 512 * i) : (d2_t){0.0, 0.0};
+            pb_loaded = pb;
+        }
+        double av[KR];
+#pragma unroll
+        for (int k = 0; k < KR; ++k) av[k] = k < K ? a.A[k * a.lda + pa] : 0.0;
+        double* o = a.out + ((p << C) - a.o_begin) + 2 * threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            d2_t acc = {0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < KR; ++k)
+                if (k < K) {
+                    acc.x = fma(av[k], b[k][i].x, acc.x);
+                    acc.y = fma(av[k], b[k][i].y, acc.y);
+                }
+            *reinterpret_cast<d2_t*>(o + 512 * i) = acc;
+        }
+    }
+}
+
+// log2 outputs per piece of the rows kernel for K terms (B pairs held: K * 2^(C - 9) d2 per lane, at
+// most 16: 64 VGPRs), 0 when the masks do not allow it: B must hold output bits 0 .. C-1, the range
+// must be piece-aligned, and C >= 11 (4 wave-stores per lane per piece).
+static int outer_rows_bits(int64_t K, uint64_t maskB, int align_bits) {
+    static const int off = getenv("QKNIT_OB_ROWS") ? atoi(getenv("QKNIT_OB_ROWS")) : 1;
+    if (!off || K < 1 || K > 8) return 0;
+    const int low = __builtin_ctzll(~maskB);  // contiguous B bits from bit 0
+    const int want = K <= 1 ? 13 : (K <= 2 ? 12 : 11);
+    return (want <= low && want <= align_bits) ? want : 0;
+}
+
+// resident workgroups per CU of a rows-kernel instantiation (its B registers set the occupancy)
+template <int KR, int C>
+static int outer_rows_per_cu() {
+    static int n = [] {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, qk_knit_outer_rows_kernel<KR, C>, 256, 0) != hipSuccess)
+            b = 2;
+        return b < 1 ? 1 : b;
+    }();
+    return n;
+}
+
 constexpr int64_t OB_STAGE_BYTES = 24 * 1024;  // LDS budget of the blocked kernel's operand stage
 constexpr int OB_WG_PER_CU = 64;  // bench, one box: 5.82 ms per write at 64, 5.85 at 32, 5.90 at 16, 6.00 at 8, 5.83 one per task
 
@@ -1746,6 +1835,30 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
     QK_HIP(ctx, hipSetDevice(ctx->device));
     const int cus = ctx->cus;
     const int align = __builtin_ctzll((uint64_t)(o_begin | o_count));
+    if (const int rc = outer_rows_bits(K, maskB, align)) {
+        const int64_t pieces = o_count >> rc;
+        // a grid of a multiple of the pb count (2^(|maskB| - C)) keeps every workgroup on one B run
+        const int64_t nb = int64_t(1) << (__builtin_popcountll(maskB) - rc);
+        const int per_cu = K <= 1 ? outer_rows_per_cu<1, 13>() : K <= 2 ? outer_rows_per_cu<2, 12>()
+                           : K <= 4 ? outer_rows_per_cu<4, 11>() : outer_rows_per_cu<8, 11>();
+        int64_t G = (int64_t)cus * per_cu;
+        if (G >= nb) G -= G % nb;
+        if (G > pieces) G = pieces;
+        OuterRowsArgs r{(int)K, A, lda, B, ldb, (uint32_t)(maskA >> rc), (uint32_t)(maskB >> rc), o_begin >> rc,
+                        (o_begin >> rc) + pieces, o_begin, k_dev, out};
+        const dim3 grid((unsigned)(G < 1 ? 1 : G));
+        if (K <= 1) {
+            hipLaunchKernelGGL((qk_knit_outer_rows_kernel<1, 13>), grid, dim3(256), 0, ctx->stream, r);
+        } else if (K <= 2) {
+            hipLaunchKernelGGL((qk_knit_outer_rows_kernel<2, 12>), grid, dim3(256), 0, ctx->stream, r);
+        } else if (K <= 4) {
+            hipLaunchKernelGGL((qk_knit_outer_rows_kernel<4, 11>), grid, dim3(256), 0, ctx->stream, r);
+        } else {
+            hipLaunchKernelGGL((qk_knit_outer_rows_kernel<8, 11>), grid, dim3(256), 0, ctx->stream, r);
+        }
+        QK_HIP(ctx, hipGetLastError());
+        return QK_OK;
+    }
     bool bg = false;
     const int tb = outer_blocked_tile(nbits, K, maskA, maskB, align, &bg);
     if (tb) {
@@ -1781,8 +1894,14 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
 int qk_knit_outer_stream_kind(int nbits, int64_t K, uint64_t maskA, uint64_t maskB, int64_t o_begin,
                               int64_t o_count, int* kind, int* task_bits) {
     if (!kind || !task_bits || nbits < 2 || nbits > 32 || K < 1 || K > SK_MAX || o_count <= 0) return QK_EARG;
+    const int align = __builtin_ctzll((uint64_t)(o_begin | o_count));
+    if (const int rc = outer_rows_bits(K, maskB, align)) {
+        *kind = 3;
+        *task_bits = rc;
+        return QK_OK;
+    }
     bool bg = false;
-    const int tb = outer_blocked_tile(nbits, K, maskA, maskB, __builtin_ctzll((uint64_t)(o_begin | o_count)), &bg);
+    const int tb = outer_blocked_tile(nbits, K, maskA, maskB, align, &bg);
     *kind = tb ? (bg ? 2 : 1) : 0;
     *task_bits = tb;
     return QK_OK;

@@ -11,6 +11,7 @@
 #include <hip/hiprtc.h>
 
 #include <cstdio>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -23,6 +24,7 @@
 struct qk_module {
     hipModule_t mod = nullptr;
     std::vector<hipFunction_t> fns;
+    std::vector<char> code;  // the code object it was loaded from (qk_module_code)
 };
 
 namespace {
@@ -77,21 +79,40 @@ int qk_module_compile(qk_ctx* ctx, const char* source, const char* const* names,
     std::vector<char> code(code_size);
     hiprtcGetCode(prog, code.data());
     hiprtcDestroyProgram(&prog);
+    return qk_module_load(ctx, code.data(), (int64_t)code.size(), names, n_names, out);
+}
+
+int qk_module_load(qk_ctx* ctx, const void* image, int64_t image_bytes, const char* const* names, int n_names,
+                   qk_module** out) {
+    if (!ctx || !image || image_bytes <= 0 || !names || n_names < 1 || !out) return QK_EARG;
+    *out = nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return jfail(ctx, QK_EHIP, "qk_module_load: hipSetDevice");
     qk_module* m = new qk_module();
-    if (hipModuleLoadData(&m->mod, code.data()) != hipSuccess) {
+    m->code.assign((const char*)image, (const char*)image + image_bytes);
+    if (hipModuleLoadData(&m->mod, m->code.data()) != hipSuccess) {
         delete m;
-        return jfail(ctx, QK_EHIP, "qk_module_compile: hipModuleLoadData failed");
+        return jfail(ctx, QK_EHIP, "qk_module_load: hipModuleLoadData failed");
     }
     for (int i = 0; i < n_names; ++i) {
         hipFunction_t f;
         if (hipModuleGetFunction(&f, m->mod, names[i]) != hipSuccess) {
             hipModuleUnload(m->mod);
             delete m;
-            return jfail(ctx, QK_EARG, std::string("qk_module_compile: no kernel ") + names[i]);
+            return jfail(ctx, QK_EARG, std::string("qk_module_load: no kernel ") + names[i]);
         }
         m->fns.push_back(f);
     }
     *out = m;
+    return QK_OK;
+}
+
+int qk_module_code(const qk_module* m, void* buf, int64_t* bytes) {
+    if (!m || !bytes) return QK_EARG;
+    if (buf) {
+        if (*bytes < (int64_t)m->code.size()) return QK_EARG;
+        memcpy(buf, m->code.data(), m->code.size());
+    }
+    *bytes = (int64_t)m->code.size();
     return QK_OK;
 }
 

@@ -316,6 +316,29 @@ def compiled_multi_module(device: int, encs: list):
     return _compile_module(device, *sweep_codegen.generate_multi(encs))
 
 
+# Code objects of per-program kernels compiled ahead of time (build: __graft_entry__.build() compiles
+# the BASELINE configs' programs with hipcc --genco) or at run time (written back when the directory is
+# writable): <sha1 of source + options>.hsaco. A long program's hiprtc compile costs seconds (qft 16:
+# 481 ops, ~7 s); from the cache it is a load.
+JIT_CACHE_DIR = os.environ.get("QKNIT_JIT_CACHE", os.path.join(os.path.dirname(os.path.abspath(__file__)), "jit_cache"))
+JIT_BASE_OPTIONS = ("--offload-arch=gfx950", "-O3", "-std=c++17")  # qknit_jit.hip's hiprtc options
+
+
+def jit_options(src: str) -> list:
+    """hiprtc / hipcc options of a generated source: the base ones plus its ``// qk-options:`` line."""
+    opts = list(JIT_BASE_OPTIONS)
+    tag = "// qk-options:"
+    if src.startswith(tag):
+        opts += src[len(tag):src.index("\n")].split()
+    return opts
+
+
+def jit_cache_path(src: str) -> str:
+    h = hashlib.sha1(src.encode())
+    h.update(" ".join(jit_options(src)).encode())
+    return os.path.join(JIT_CACHE_DIR, h.hexdigest() + ".hsaco")
+
+
 def _compile_module(device: int, src: str, names: list):
     key = (device, names[0], hashlib.sha1(src.encode()).hexdigest())
     with _modules_lock:
@@ -323,10 +346,35 @@ def _compile_module(device: int, src: str, names: list):
             ctx = get_context(device)
             arr = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
             h = ctypes.c_void_p()
-            ctx.check(ctx.lib.qk_module_compile(ctx.handle, src.encode(), arr, len(names), ctypes.byref(h)),
-                      "qk_module_compile")
+            path = jit_cache_path(src)
+            if os.path.exists(path):
+                img = open(path, "rb").read()
+                ctx.check(ctx.lib.qk_module_load(ctx.handle, img, len(img), arr, len(names), ctypes.byref(h)),
+                          "qk_module_load")
+            else:
+                ctx.check(ctx.lib.qk_module_compile(ctx.handle, src.encode(), arr, len(names), ctypes.byref(h)),
+                          "qk_module_compile")
+                _write_cache(ctx, h, path)
             _MODULES[key] = h
         return _MODULES[key]
+
+
+def _write_cache(ctx, module, path: str) -> None:
+    """Keep a run-time compiled code object for later processes (best effort)."""
+    if os.environ.get("QKNIT_JIT_CACHE_WRITE", "1") == "0":
+        return
+    try:
+        n = ctypes.c_int64()
+        ctx.check(ctx.lib.qk_module_code(module, None, ctypes.byref(n)), "qk_module_code")
+        buf = ctypes.create_string_buffer(n.value)
+        ctx.check(ctx.lib.qk_module_code(module, buf, ctypes.byref(n)), "qk_module_code")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            f.write(buf.raw[: n.value])
+        os.replace(tmp, path)
+    except OSError:
+        pass
 
 
 def init_prefixes(enc, jobs: JobTable):
@@ -578,7 +626,7 @@ def knit_outer_stream(ctx: Context, A, B, clbits_a: list, clbits_b: list, nbits:
 
 
 OUTER_STREAM_KERNELS = ("qk_knit_outer_stream_kernel", "qk_knit_outer_blocked_kernel",
-                        "qk_knit_outer_blocked_kernel<b_global>")
+                        "qk_knit_outer_blocked_kernel<b_global>", "qk_knit_outer_rows_kernel")
 
 
 def knit_outer_stream_kernel(K: int, clbits_a: list, clbits_b: list, nbits: int, o_begin: int = 0,
@@ -660,6 +708,8 @@ class FragmentState:
     # traced qubits beyond what a FINAL tile holds: the device program measures `log2(fold)` of them
     # too (widened outputs) and fold_traced sums them out after the sweep (_device_program)
     fold: int = 1
+    # per-program kernels: (compiled, tile bits, FINAL tile bits) as prepare_fragments chose them
+    jit: tuple = (False, None, None)
 
     @property
     def swept_labels(self) -> list:
@@ -745,18 +795,46 @@ def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = 
     split = [(fs.prog.n, fs.jobs.n_jobs) for fs, w in zip(out, want) if w and not fs.dropped and fs.prog.n > 12]
     tb = jit_tile_bits(split) if split else JIT_TILE_BITS_MAX
     jit_progs = [_device_program(fs.prog)[0] for fs, w in zip(out, want) if w and not fs.dropped and fs.prog.n > 12]
-    ftb = jit_final_tile_bits(jit_progs, tb) if (upload and jit_progs) else None
+    ftb = jit_final_tile_bits(jit_progs, tb) if jit_progs else None
     for fs, w in zip(out, want):
+        fs.jit = (bool(w and _jit_enabled()), tb, ftb)  # what upload compiles (jit_sources)
         if upload and not fs.dropped:
             fs.dprog = DeviceProgram.upload(_device_program(fs.prog)[0], device, jit=w, tile_bits=tb,
                                             final_tile_bits=ftb)
     return out
 
 
+JIT_LONG_OPS = 200  # programs this long run op-dispatch bound on the interpreter whatever their batch
+
+
 def _worth_compiling(prog: FragmentProgram, jobs: JobTable) -> bool:
-    """Per-program kernels pay their hiprtc compile (about 1 s per 100 ops) only on real work:
-    >= 2^22 amplitudes per sweep, and at most 400 ops (qft 16: 586 ops, 20 s, one instance)."""
-    return (jobs.n_jobs << prog.n) >= (1 << 22) and len(prog.ops) <= 400
+    """Per-program kernels pay their compile (hiprtc: about 1 s per 70 ops; none when the code object
+    is in JIT_CACHE_DIR) on real work: >= 2^22 amplitudes per sweep (at most 400 ops), or a long
+    program (>= JIT_LONG_OPS ops: qft 16's 586, one instance, 0.36 ms on the interpreter's 16
+    workgroups of serial op dispatch)."""
+    return ((jobs.n_jobs << prog.n) >= (1 << 22) and len(prog.ops) <= 400) or len(prog.ops) >= JIT_LONG_OPS
+
+
+def jit_sources(virt, basis: bool = False, relevance: bool = True) -> list:
+    """``[(source, kernel names)]`` of the per-program kernels a plan of ``virt`` compiles (no device:
+    the ahead-of-time cache of build()): each compiled fragment's module (upload) and, for 2-4 of
+    them on one tile width per pass round, the multi-fragment module (pipeline._plan_multi)."""
+    from . import sweep_codegen
+
+    frags = prepare_fragments(virt, upload=False, basis=basis, relevance=relevance)
+    encs = []
+    for fs in frags:
+        want, tb, ftb = fs.jit
+        dprog = _device_program(fs.prog)[0]
+        if fs.dropped or not want or dprog.n <= 12:
+            continue
+        encs.append(encode(dprog, tile_bits=tb or JIT_TILE_BITS_MAX, final_tile_bits=ftb))
+    out = [sweep_codegen.generate(e) for e in encs]
+    rounds = max((len(e.passes) for e in encs), default=0)
+    if 2 <= len(encs) <= 4 and all(len({e.pass_tile_bits(r) for e in encs if len(e.passes) > r}) == 1
+                                   for r in range(rounds)):
+        out.append(sweep_codegen.generate_multi(encs))
+    return out
 
 
 def _some_label_unmeasured(prog: FragmentProgram, labels: list) -> bool:

@@ -134,6 +134,14 @@ typedef struct qk_module qk_module;
 int qk_module_compile(qk_ctx* ctx, const char* source, const char* const* names, int n_names,
                       qk_module** out);
 int qk_module_destroy(qk_module* module);
+/* A module from a code object compiled earlier (qk_module_code of a compiled module, or the same
+ * source compiled ahead of time: hipcc --genco --offload-arch=gfx950 -O3 -std=c++17 plus the
+ * source's qk-options line), without hiprtc. */
+int qk_module_load(qk_ctx* ctx, const void* image, int64_t image_bytes, const char* const* names, int n_names,
+                   qk_module** out);
+/* The code object a module was loaded from: *bytes = its size; copied to buf when buf is non-NULL
+ * (*bytes at least that size on entry). */
+int qk_module_code(const qk_module* module, void* buf, int64_t* bytes);
 
 /* qk_sweep with pass i launched as module kernel i (kernel args: job_slots, job_sign, state,
  * pjob, n_jobs), same grid (sparse INIT pass: one tile per job). */
@@ -229,7 +237,8 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
 /* The kernel qk_knit_outer_stream_range launches for these arguments (no launch): *kind = 0 the
  * per-output gather kernel (qk_knit_outer_stream_kernel), 1 the blocked kernel with A and B staged in
  * LDS (qk_knit_outer_blocked_kernel<false>), 2 the blocked kernel reading B from global memory
- * (<true>); *task_bits = log2 outputs per blocked task (0 for kind 0). */
+ * (<true>), 3 the rows kernel holding B runs in registers (qk_knit_outer_rows_kernel: B holds the
+ * low output bits, syc 32 1); *task_bits = log2 outputs per task / piece (0 for kind 0). */
 int qk_knit_outer_stream_kind(int nbits, int64_t K, uint64_t maskA, uint64_t maskB, int64_t o_begin,
                               int64_t o_count, int* kind, int* task_bits);
 int qk_khatri_rao(qk_ctx* ctx, int64_t K, int64_t M, int64_t N, const double* A, int64_t lda,
