@@ -273,6 +273,33 @@ def test_split_mode_fragment_matches_oracle(T):
             np.testing.assert_allclose(q[li], ref, atol=TOL, rtol=0)
 
 
+def test_syc_32_5_basis_rows_match_oracle(T):
+    """Every swept row of the bench plan's syc 32 5 sweep (basis-reduced, light cone: 64 + 256
+    instances of two 16-qubit fragments, per-program kernels) against the oracle statevector
+    (golden/basis_rows_syc_32_5_p2.json, tests/golden/make_rows.py): per row 24 seeded entries
+    (1e-12), the sum, the squared norm and four seeded Rademacher projections of all 2^16 entries
+    (1e-11: each sums 2^16 terms)."""
+    from golden import make_rows
+
+    gold = json.load(open(os.path.join(GOLD, "basis_rows_syc_32_5_p2.json")))
+    _, cut = cutting.config_cut_circuit("syc", 32, 5, 2)[:2]
+    frags = engine.prepare_fragments(VirtualCircuit(cut), 0, basis=True)
+    ctx = engine.get_context(0)
+    assert len(frags) == len(gold["fragments"])
+    for fs, g in zip(frags, gold["fragments"]):
+        assert [list(lab) for lab in fs.basis_labels] == g["basis_labels"]
+        assert fs.dprog.module is not None  # the compiled per-program kernels the bench runs
+        q = engine.sweep_fragment(ctx, fs).cpu().numpy()
+        assert q.shape == (len(g["rows"]), 1 << fs.prog.m)
+        pos, proj = make_rows.probes(q.shape[1])
+        assert list(pos) == g["positions"]
+        for row, ref in zip(q, g["rows"]):
+            np.testing.assert_allclose(row[pos], ref["samples"], atol=1e-12, rtol=0)
+            assert abs(row.sum() - ref["sum"]) <= 1e-11
+            assert abs(row @ row - ref["sumsq"]) <= 1e-12
+            np.testing.assert_allclose(proj @ row, ref["proj"], atol=1e-11, rtol=0)
+
+
 def test_compiled_sweep_matches_interpreter(T):
     """Per-program kernels (sweep_codegen + hiprtc, qk_sweep_compiled) == the interpreter kernel
     (qk_sweep) on every branch job of both syc 32 5 fragments (basis-reduced: 625 jobs each)."""
