@@ -682,10 +682,11 @@ def main():
             "kernel": "per-program sweep kernels (sweep_codegen + hiprtc): shared INIT tiles (one per distinct "
                       "INIT-slot prefix), FINAL pass on narrowed single-wave tiles summing each label's branch "
                       "jobs, labels heaviest first, XCD-grouped tile order (all fragments, per step, this rank)",
-            "bound": "VALU issue: the FINAL pass (89% of the sweep) keeps the VALU busy 66% of its cycles, 51% "
+            "bound": "VALU issue: the FINAL pass (89% of the sweep) keeps the VALU busy 63% of its cycles, 53% "
                      "on f64 instructions (mostly adds: the normalised +-1/+-i gate entries fold multiplies "
-                     "away, so flop rates understate it); the INIT pass (11%) is one wave's serial op chain; "
-                     "HBM moves ~0.2 GB per step (counters, profiles/r02d_sweep_pmc.json)",
+                     "away, so flop rates understate it), LDS bank conflicts 23% of its LDS cycles, clock 1.9 "
+                     "GHz; the INIT pass (11%) is one wave's serial op chain; HBM moves ~0.2 GB per step "
+                     "(counters, profiles/r04d_sweep_pmc.json)",
             "ms_per_step": sweep_ms,
             "branch_jobs": counts["branch_jobs"],
             "hbm_bytes_model": traffic["hbm"],
