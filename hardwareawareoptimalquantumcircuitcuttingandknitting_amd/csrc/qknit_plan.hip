@@ -230,6 +230,10 @@ int lowrank_layout(qk_ctx* ctx, const qk_lowrank_plan* p, LowrankLayout& L, std:
         why = "qk_knit_lowrank: need even 2 <= terms <= 64, swept rows, transforms, probes, 2 <= nbits <= 32";
         return QK_EARG;
     }
+    if (p->rows_a > INT32_MAX || p->rows_b > INT32_MAX) {  // qk_prep_operands takes int row counts
+        why = "qk_knit_lowrank: rows_a and rows_b must be at most INT32_MAX";
+        return QK_EARG;
+    }
     const uint64_t full = (uint64_t(1) << p->nbits) - 1;
     if ((p->mask_a & p->mask_b) || (p->mask_a | p->mask_b) != full || !(p->mask_b & 1)) {
         why = "qk_knit_lowrank: masks must be disjoint, cover all nbits output bits, bit 0 in mask_b";

@@ -407,6 +407,10 @@ class KnitPipeline:
         # to the exact slice, so its collectives match). Factors that differed between ranks would mix
         # compressed columns and fail some rank's check. QKNIT_SLICE_SYNC=1: rank 0's factors broadcast.
         self.slice_sync = os.environ.get("QKNIT_SLICE_SYNC", "0") == "1"
+        # slice mode, the exact fallback of a rejected compression: "predicated" (default) all-gathers
+        # its operands every step and predicates the contraction on the device verdict (no host sync
+        # in the step); "host" reads the verdict on the host and gathers only on a rejection
+        self.slice_exact = os.environ.get("QKNIT_SLICE_EXACT", "predicated")
         self.last_kernel = None  # kernel of the last compressed contraction (None: qk_gemm_keyed)
         self.last_prep = None  # data-rank preparation of the last step: "fused" (qk_prep_operands) or "torch"
         self._probe = None
@@ -929,6 +933,17 @@ class KnitPipeline:
         # column blocks cover all of R; the ranks' factors are identical, so the local ranks are r or 0).
         # A rejection anywhere makes every rank take the exact slice, whose collectives then match.
         dist.all_reduce(k_eff, op=dist.ReduceOp.MIN, group=self.group)
+        if self.slice_exact == "host":
+            # round-3 form: the host reads the (MIN-reduced) verdict after queueing the write and
+            # gathers the exact slice's operands only on a rejection (no per-step gather)
+            on_gpu = k_eff.device.type == "cuda"
+            pinned = T.empty(1, dtype=T.int32, pin_memory=on_gpu)
+            pinned.copy_(k_eff, non_blocking=on_gpu)
+            ready = T.cuda.Event() if on_gpu else None
+            if on_gpu:
+                ready.record()
+            return {"A2": A2, "B2": B2, "k_eff": k_eff, "XA": XA, "XB": XB, "pinned": pinned, "ready": ready,
+                    "mats": mats}
         # the exact slice's operands, gathered every step (the same collectives on every rank whatever
         # the verdict; the contraction itself is predicated on the device, _launch_slice)
         ex = self._slice_exact_operands(XA, XB)
@@ -948,6 +963,12 @@ class KnitPipeline:
         if self.record_events:
             end.record()
             self.events.append((start, end))
+        if "exact" not in p:  # slice_exact == "host"
+            if p["ready"] is not None:
+                p["ready"].synchronize()  # the check only, not the knit queued behind it
+            if int(p["pinned"][0]) == 0:
+                self._slice_exact(p["XA"], p["XB"], cA, cB)
+            return self.out
         # exact contraction of this slice, predicated on the device: runs only when the (MIN-reduced)
         # accepted rank is 0 — no host round trip, the verdict is read later by sync_stats
         A, kA, B, kB = p["exact"]

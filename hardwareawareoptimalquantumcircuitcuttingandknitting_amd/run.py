@@ -106,6 +106,7 @@ def _direct_dense(virt: VirtualCircuit, shots: int, device: int, factored: bool,
 # ---------------------------------------------------------------------------- plan cache
 PLAN_CACHE_SIZE = 4  # compiled plans kept (LRU), per (circuit fingerprint, device, thread)
 PLAN_CACHE_MAX_BYTES = 16 << 30  # plans holding more device memory (a 32-qubit uncut sweep: 100 GB) are not kept
+PLAN_CACHE_TOTAL_BYTES = 32 << 30  # device bytes all cached plans may hold together (LRU eviction beyond)
 _PLANS: OrderedDict = OrderedDict()
 _PLANS_LOCK = threading.Lock()
 
@@ -182,14 +183,30 @@ def cached_plan(virt: VirtualCircuit, device: int = 0):
     with _PLANS_LOCK:
         _PLANS[key] = pipe
         _PLANS.move_to_end(key)
-        while len(_PLANS) > PLAN_CACHE_SIZE:
+        while len(_PLANS) > 1 and (len(_PLANS) > PLAN_CACHE_SIZE
+                                   or sum(_plan_held_bytes(p) for p in _PLANS.values()) > PLAN_CACHE_TOTAL_BYTES):
             _PLANS.popitem(last=False)
     return pipe
 
 
+def _plan_held_bytes(pipe) -> int:
+    """Device bytes a cached plan holds: its buffers and the output mapping it keeps for reuse."""
+    own = getattr(pipe, "_call_owner", None)
+    return pipe.plan_bytes() + (8 * own.n if own is not None else 0)
+
+
 def clear_plan_cache() -> None:
+    """Drop every cached plan (and the output mappings they keep): the device memory returns once
+    no result tensor of theirs is alive."""
     with _PLANS_LOCK:
         _PLANS.clear()
+
+
+def _is_oom(e: Exception) -> bool:
+    T = engine.torch()
+    msg = str(e)
+    return (isinstance(e, T.cuda.OutOfMemoryError) or "out of memory" in msg.lower()
+            or "hipErrorOutOfMemory" in msg)
 
 
 def _planned_dense(virt: VirtualCircuit, device: int, out):
@@ -253,7 +270,15 @@ def run_virtual_circuit_dense(virt: VirtualCircuit, shots: int = 20000, *, devic
              tuple(len(f) for f in virt.fragment_circuits), len(virt.vgate_instructions))
     native = all(isinstance(virt.get_backend(f), MI355XBackend) for f in virt.fragment_circuits if len(f))
     if factored is None and native and not sample:
-        dense, info, _ = _planned_dense(virt, device, out)
+        try:
+            dense, info, _ = _planned_dense(virt, device, out)
+        except Exception as e:  # out of device memory: drop the cached plans (and their outputs), retry once
+            if not _is_oom(e):
+                raise
+            log.warning("out of device memory (%s): clearing the plan cache and retrying", e)
+            clear_plan_cache()
+            engine.torch().cuda.empty_cache()
+            dense, info, _ = _planned_dense(virt, device, out)
     else:
         dense, info = _direct_dense(virt, shots, device, bool(factored), out, sample, seed)
     log.info("Knitted in %.2fs.", info.knit_time)

@@ -1012,10 +1012,15 @@ def test_rank_factors_device_degenerate(T):
         assert float(TA.abs().max()) == 0.0 and float(TB.abs().max()) == 0.0
 
 
-def test_concurrent_runs_from_two_threads(T):
+@pytest.mark.parametrize("default_path", [False, True])
+def test_concurrent_runs_from_two_threads(T, default_path, monkeypatch):
     """The reference calls run_virtual_circuit from several threads at once (Utilities.py:85-89,
     132-136, each with its own Pool(8)). Two threads here run different circuits concurrently (one
-    qk context per thread, same device), twice each; every result equals the oracle's knit (1e-12)."""
+    qk context per thread, same device), twice each; every result equals the oracle's knit (1e-12).
+    default_path: factored=None — each thread's cached plan (plan cache per thread) and its output
+    mapping (qk_out_alloc: OUT_MAPPED_MIN_BYTES=0 maps even these small outputs)."""
+    if default_path:
+        monkeypatch.setattr(engine, "OUT_MAPPED_MIN_BYTES", 0)
     import threading
 
     from oracle import dense
@@ -1033,7 +1038,8 @@ def test_concurrent_runs_from_two_threads(T):
     def worker(names):
         try:
             for k in names:
-                out, _ = run_virtual_circuit(VirtualCircuit(cases[k]), dense=True, factored=(k != "bv_5_1_p2"))
+                factored = None if default_path else (k != "bv_5_1_p2")
+                out, _ = run_virtual_circuit(VirtualCircuit(cases[k]), dense=True, factored=factored)
                 T.cuda.current_stream().synchronize()
                 errs.setdefault(k, []).append(float(np.abs(out.cpu().numpy() - refs[k]).max()))
         except Exception as e:  # surfaced below
