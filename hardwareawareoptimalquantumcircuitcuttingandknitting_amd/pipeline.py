@@ -945,8 +945,9 @@ class KnitPipeline:
             return {"A2": A2, "B2": B2, "k_eff": k_eff, "XA": XA, "XB": XB, "pinned": pinned, "ready": ready,
                     "mats": mats}
         # the exact slice's operands, gathered every step (the same collectives on every rank whatever
-        # the verdict; the contraction itself is predicated on the device, _launch_slice)
-        ex = self._slice_exact_operands(XA, XB)
+        # the verdict; the contraction itself is predicated on the device, _launch_slice); started
+        # asynchronously, so the write does not wait for them — only the predicated contraction does
+        ex = self._slice_exact_operands(XA, XB, async_op=True)
         return {"A2": A2, "B2": B2, "k_eff": k_eff, "exact": ex, "mats": mats}
 
     def _launch_slice(self, p: dict):
@@ -971,7 +972,7 @@ class KnitPipeline:
             return self.out
         # exact contraction of this slice, predicated on the device: runs only when the (MIN-reduced)
         # accepted rank is 0 — no host round trip, the verdict is read later by sync_stats
-        A, kA, B, kB = p["exact"]
+        A, kA, B, kB = p["exact"]()
         be.gemm_keyed(A, B, keyA=kA, keyB=kB, out=self.out, skip=p["k_eff"])
         return self.out
 
@@ -1055,7 +1056,7 @@ class KnitPipeline:
             be.bind()
             for k in ("A2", "B2", "k_eff"):
                 p[k].record_stream(W)
-            for m in list(p["mats"]) + list(p.get("exact", ())):
+            for m in p["mats"]:
                 if m is not None:
                     m.record_stream(W)
             out = self._launch_slice(p) if self.mode == "slice" else self._launch_dev_rank(p)
@@ -1090,23 +1091,62 @@ class KnitPipeline:
             self._exact_plan = plan
         return self._exact_plan
 
-    def _slice_exact_operands(self, XA, XB):
+    def _slice_exact_operands(self, XA, XB, async_op: bool = False):
         """(A, keyA, B, keyB) of this rank's exact slice from the transformed column blocks ``XA`` /
         ``XB`` [K, w / P]: a side whose columns are this rank's own block is used as it is, the other
         side is all-gathered (syc 32 at 2-8 ranks: the slice's fixed output bits are A's top bits, so
-        only B travels, K x 2^16 doubles per step)."""
+        only B travels, K x 2^16 doubles per step). ``async_op``: the gathers are started and a
+        finisher returned instead — called on the stream that needs the operands, it makes that
+        stream wait for them (their column reorder runs on a helper stream that waits for the gather,
+        so it overlaps whatever runs meanwhile, the write in pipelined steps)."""
         import torch.distributed as dist
 
         T, P = self.T, self.world
-        out = []
+        parts, pend = [], []
         for X, (base, n, local, keys) in zip((XA, XB), self._slice_exact_plan()):
-            if not local:
-                K, bw = X.shape
-                g = T.empty((P * K * bw,), dtype=X.dtype, device=X.device)
-                dist.all_gather_into_tensor(g, X.contiguous().reshape(-1), group=self.group)
-                X = g.view(P, K, bw).permute(1, 0, 2).reshape(K, P * bw)[:, base:base + n].contiguous()
-            out += [X, keys]
-        return tuple(out)
+            if local:
+                parts += [X, keys]
+                continue
+            K, bw = X.shape
+            g = T.empty((P * K * bw,), dtype=X.dtype, device=X.device)
+            work = dist.all_gather_into_tensor(g, X.contiguous().reshape(-1), group=self.group, async_op=async_op)
+            pend.append((len(parts), g, work, K, bw, base, n))
+            parts += [None, keys]
+
+        def reorder(g, K, bw, base, n):
+            return g.view(P, K, bw).permute(1, 0, 2).reshape(K, P * bw)[:, base:base + n].contiguous()
+
+        if not async_op:
+            for i, g, _, K, bw, base, n in pend:
+                parts[i] = reorder(g, K, bw, base, n)
+            return tuple(parts)
+        on_gpu = XA.device.type == "cuda"
+        if on_gpu:
+            if getattr(self, "_exact_stream", None) is None:
+                self._exact_stream = T.cuda.Stream(device=XA.device)
+            H = self._exact_stream
+            H.wait_stream(T.cuda.current_stream())
+            with T.cuda.stream(H):
+                for i, g, work, K, bw, base, n in pend:
+                    work.wait()  # H waits for the gather, the host does not
+                    parts[i] = reorder(g, K, bw, base, n)
+                    g.record_stream(H)
+            done = T.cuda.Event()
+            done.record(H)
+        else:
+            for i, g, work, K, bw, base, n in pend:
+                work.wait()
+                parts[i] = reorder(g, K, bw, base, n)
+
+        def finish():
+            if on_gpu:
+                T.cuda.current_stream().wait_event(done)
+                for t in parts:
+                    if t is not None:
+                        t.record_stream(T.cuda.current_stream())
+            return tuple(parts)
+
+        return finish
 
     def _slice_exact(self, XA, XB, cA, cB):
         """Exact contraction of this rank's output slice (K terms) from the transformed column blocks

@@ -89,11 +89,33 @@ def main():
         note("broadcast", t.numel() * t.element_size())
         return _Done() if async_op else None
 
+    side = []
+
+    class _Pending:
+        """An async stand-in collective: ran on a side stream; wait() makes the current stream wait."""
+
+        def __init__(self, ev):
+            self.ev = ev
+
+        def wait(self):
+            torch.cuda.current_stream().wait_event(self.ev)
+
     def all_gather_into_tensor(out, inp, group=None, async_op=False):
         P = world_now[0]
-        out.view(P, -1).copy_(inp.reshape(1, -1).expand(P, -1))
-        note("all_gather", out.numel() * out.element_size() * (P - 1) // P)
-        return _Done() if async_op else None
+        if not async_op:
+            out.view(P, -1).copy_(inp.reshape(1, -1).expand(P, -1))
+            note("all_gather", out.numel() * out.element_size() * (P - 1) // P)
+            return None
+        if not side:
+            side.append(torch.cuda.Stream())
+        s = side[0]
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):  # the transfer (copy + modelled xGMI time) off the issuing stream
+            out.view(P, -1).copy_(inp.reshape(1, -1).expand(P, -1))
+            note("all_gather_async", out.numel() * out.element_size() * (P - 1) // P)
+            ev = torch.cuda.Event()
+            ev.record(s)
+        return _Pending(ev)
 
     dist.all_to_all_single = all_to_all_single
     dist.all_reduce = all_reduce
