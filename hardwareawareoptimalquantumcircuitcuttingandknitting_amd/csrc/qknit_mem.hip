@@ -15,7 +15,16 @@
 //                                   last rounded up to the allocation granularity) mapped
 //                                   read-write for ctx's device at a 1-GiB-aligned address;
 //                                   below 1 GiB one chunk at an alignment of its power-of-two size
-//   qk_out_free(ctx, ptr)           synchronizes the device, unmaps, releases
+//   qk_out_free(ctx, ptr)           synchronizes the device, unmaps, releases the physical chunks;
+//                                   the virtual range stays reserved (retired, never mapped again)
+//
+// Retired ranges: a freed range whose addresses were reserved again for the next mapping read back
+// wrong — 32-KiB runs of a live small mapping came back as zeros after other mappings had been freed
+// and re-reserved (tools/diag/mapped_loop.py: 44 of 60 drop-in calls on cx_8x8 with 512-KiB outputs;
+// none while no mapping was ever freed, tools/diag/mapped_read.py), i.e. translations of the old
+// mapping outlived it. So a freed range's addresses are never handed out again: the physical memory
+// goes back at once, the address range (not memory) only when a reservation fails (the 47-bit
+// device address space holds thousands of 34-GB outputs).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -36,6 +45,7 @@ struct OutMapping {
 
 std::mutex g_mu;
 std::map<uintptr_t, OutMapping> g_maps;
+std::vector<std::pair<void*, size_t>> g_retired;  // unmapped ranges kept reserved (see above)
 
 constexpr size_t OUT_CHUNK = size_t(1) << 30;
 
@@ -52,6 +62,25 @@ void unmap_release(void* va, OutMapping& m) {
     (void)hipMemUnmap(va, m.bytes);
     for (auto h : m.chunks) (void)hipMemRelease(h);
     (void)hipMemAddressFree(va, m.bytes);
+}
+
+// unmap and release the physical chunks; the range stays reserved, retired
+void unmap_retire(void* va, OutMapping& m) {
+    (void)hipMemUnmap(va, m.bytes);
+    for (auto h : m.chunks) (void)hipMemRelease(h);
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_retired.emplace_back(va, m.bytes);
+}
+
+// give the retired ranges back (only when a reservation fails: the address space is exhausted)
+size_t free_retired() {
+    std::vector<std::pair<void*, size_t>> r;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        r.swap(g_retired);
+    }
+    for (auto& x : r) (void)hipMemAddressFree(x.first, x.second);
+    return r.size();
 }
 
 }  // namespace
@@ -81,6 +110,7 @@ int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr) {
     OutMapping m{n_chunks * chunk, ctx->device, {}};
     void* va = nullptr;
     e = hipMemAddressReserve(&va, m.bytes, align, nullptr, 0);
+    if (e != hipSuccess && free_retired() > 0) e = hipMemAddressReserve(&va, m.bytes, align, nullptr, 0);
     if (e != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_alloc: hipMemAddressReserve", e);
     size_t mapped = 0;
     for (size_t i = 0; i < n_chunks; ++i) {
@@ -128,7 +158,7 @@ int qk_out_free(qk_ctx* ctx, void* ptr) {
     (void)hipSetDevice(m.device);
     // kernels on any stream may still write the buffer: the mapping goes only when they are done
     hipError_t e = hipDeviceSynchronize();
-    unmap_release(ptr, m);
+    unmap_retire(ptr, m);
     if (e != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_free: hipDeviceSynchronize", e);
     return QK_OK;
 }

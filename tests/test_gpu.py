@@ -705,7 +705,11 @@ def test_mapped_output_buffer_steps_match_oracle(T, case, monkeypatch):
     first = pipe.take_out()
     p0 = first.data_ptr()
     pipe.run_into(first)
-    np.testing.assert_allclose(first.cpu().numpy(), ref, atol=1e-12, rtol=0)
+    got = first.cpu().numpy()
+    bad = np.flatnonzero(np.abs(got - ref) > 1e-12)
+    pipe.sync_stats()
+    assert bad.size == 0, (f"{bad.size} wrong entries [{bad[0]}, {bad[-1]}], kernel {pipe.last_kernel}, "
+                           f"rank {pipe.last_rank}, out {first.data_ptr():#x}")
     second = pipe.take_out()  # the first result is still held: a new mapping
     assert second.data_ptr() != p0
     del first  # its mapping goes with it (no owner left)
@@ -716,6 +720,32 @@ def test_mapped_output_buffer_steps_match_oracle(T, case, monkeypatch):
     del second, third
     assert not owner.in_use()
     assert pipe.take_out().data_ptr() == owner.ptr  # nothing holds it: handed out again
+
+
+def test_mapped_outputs_freed_and_remapped_read_back_exactly(T, monkeypatch):
+    """Drop-in calls that keep some results and drop others: mappings are freed and new ones made
+    between calls. Each result equals the oracle (1e-12) read back by the D2H copy. Freed ranges'
+    addresses used to be reserved again for later mappings, and 32-KiB runs of those read back as
+    zeros in 44 of 60 calls (qknit_mem.hip: retired ranges; tools/diag/mapped_loop.py)."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    monkeypatch.setattr(engine, "OUT_MAPPED_MIN_BYTES", 0)
+    cut = circuits.two_fragment("cx", 8, 8, n_cuts=4)[1]
+    pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
+    ref = dense.run_dense(cut)
+    held, wrong = [], []
+    for it in range(30):
+        out = pipe.take_out()
+        pipe.run_into(out)
+        bad = int(np.count_nonzero(np.abs(out.cpu().numpy() - ref) > 1e-12))
+        if bad:
+            wrong.append((it, bad))
+        if it % 3 == 0:
+            held.append(out)  # kept: the next call maps a new buffer
+        if len(held) > 2:
+            held.pop(0)  # dropped: its mapping is freed
+        del out
+    assert not wrong, f"calls with wrong entries (call, count): {wrong}"
 
 
 @pytest.mark.slow

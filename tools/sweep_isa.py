@@ -25,7 +25,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="syc_32_5_p2")
     ap.add_argument("--keep", default=None)
-    ap.add_argument("--tile-bits", type=int, default=13)
+    ap.add_argument("--tile-bits", type=int, default=None, help="default: what prepare_fragments picks")
+    ap.add_argument("--final-tile-bits", type=int, default=None, help="default: what prepare_fragments picks")
     ap.add_argument("--flags", nargs="*", default=[], help="extra compiler flags (e.g. -fno-signed-zeros)")
     args = ap.parse_args()
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting, engine
@@ -34,7 +35,11 @@ def main():
     name, n, d, p, var = cutting.BASELINE_CONFIGS[args.workload]
     _, cut, _ = cutting.config_cut_circuit(name, n, d, p, var)
     frags = engine.prepare_fragments(VirtualCircuit(cut), 0, upload=False, basis=True)
-    encs = [sweep_plan.encode(fs.prog, tile_bits=args.tile_bits) for fs in frags if not fs.dropped]
+    live = [fs for fs in frags if not fs.dropped]
+    tb = args.tile_bits or live[0].jit[1]
+    ftb = args.final_tile_bits if args.final_tile_bits is not None else live[0].jit[2]
+    encs = [sweep_plan.encode(engine._device_program(fs.prog)[0], tile_bits=tb, final_tile_bits=ftb or None)
+            for fs in live]
     src, names = sweep_codegen.generate_multi(encs)
     d = args.keep or tempfile.mkdtemp()
     os.makedirs(d, exist_ok=True)
