@@ -53,6 +53,7 @@ struct PrepSide {
 struct PrepArgs {
     PrepSide s[2];
     int K;
+    int split;     // 1: even workgroups take side 0's tiles, odd ones side 1's (prep_grid)
     double* part;  // [2][gridDim.x][PPART]
 };
 
@@ -128,7 +129,12 @@ __global__ __launch_bounds__(PTH, 2 * QK_PREP_WG_PER_CU) void qk_prep_operands_k
         const int nst = (R + PRS - 1) / PRS;
         const int64_t tiles = S.N / PCT;
         d4_t g0 = {0, 0, 0, 0}, g1 = {0, 0, 0, 0}, u = {0, 0, 0, 0};
-        for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        // split grids: a workgroup does one side's tile, so the two sides' serial stage chains (R / PRS
+        // dependent stage loads each) run side by side instead of one after the other
+        const bool mine = !a.split || (int)(blockIdx.x & 1) == sd;
+        const int64_t t_first = a.split ? (int64_t)(blockIdx.x >> 1) : (int64_t)blockIdx.x;
+        const int64_t t_step = a.split ? (int64_t)(gridDim.x >> 1) : (int64_t)gridDim.x;
+        for (int64_t t = mine ? t_first : tiles; t < tiles; t += t_step) {
             const int64_t c0 = t * PCT;
             // stage loads: this wave moves q rows PRPW w + h (one 1-KiB wave-instruction each) and the
             // same Wt rows (lanes < K/2: 16 B each); rows >= R are not loaded (masked at use)
@@ -651,8 +657,21 @@ int fail(qk_ctx* ctx, int code, const char* msg) {
     return code;
 }
 
+// Workgroups of qk_prep_operands_kernel. A workgroup takes a tile of each side in turn; when both
+// sides' tiles fit the resident workgroups at once (slice mode: 64 tiles per side at 8 ranks on the
+// 96 preparation CUs) the grid is split, one side per workgroup (prep_split): 114 -> ? us at 8 ranks.
+#ifndef QK_PREP_SPLIT
+#define QK_PREP_SPLIT 1
+#endif
+bool prep_split(qk_ctx* ctx, int64_t NA, int64_t NB) {
+    const int64_t tiles = (NA > NB ? NA : NB) / PCT;
+    const int64_t g = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * QK_PREP_WG_PER_CU;
+    return QK_PREP_SPLIT && tiles > 0 && 2 * tiles <= g;
+}
+
 int prep_grid(qk_ctx* ctx, int64_t NA, int64_t NB) {
     const int64_t tiles = (NA > NB ? NA : NB) / PCT;
+    if (prep_split(ctx, NA, NB)) return (int)(2 * tiles);
     const int64_t g = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * QK_PREP_WG_PER_CU;
     return (int)(tiles < g ? (tiles > 0 ? tiles : 1) : g);
 }
@@ -688,6 +707,7 @@ int qk_prep_operands(qk_ctx* ctx, int K, int RA, const double* WtA, const double
     args.s[0] = PrepSide{WtA, qA, ldqA, NA, RA, XA, nullptr};
     args.s[1] = PrepSide{WtB, qB, ldqB, NB, RB, XB, probes};
     args.K = K;
+    args.split = prep_split(ctx, NA, NB) ? 1 : 0;
     args.part = work;
     hipLaunchKernelGGL(qk_prep_operands_kernel, dim3(G), dim3(PTH), 0, ctx->stream, args);
     const int outs = 2 * K * K + PNP * K;

@@ -67,6 +67,29 @@ def _shard(n: int, rank: int, world: int) -> tuple[int, int]:
     return lo, min(n, lo + per)
 
 
+# branch jobs per swept row at most (QKNIT_ROW_JOBS; 0: one row per label). The FINAL pass gives each
+# (row, tile) one workgroup that walks the row's branch jobs serially; syc 32 5's labels carry 1-16
+# jobs, and at 8 ranks the rank holding the 16-job label waited for it (FINAL 127 us for an eighth of
+# the labels, profiles/r04r_rank_sim_8_timeline.txt). A longer label is swept as several rows of
+# consecutive jobs whose sum is its row: the transforms repeat its row (Wt[src]), so the knit
+# operands X = Wt^T q are the same sums.
+ROW_JOBS = int(os.environ.get("QKNIT_ROW_JOBS", "4"))
+
+
+def _split_rows(offsets: np.ndarray, max_jobs: int):
+    """(source label of every swept row, row job offsets): labels of more than ``max_jobs`` branch
+    jobs become ceil(jobs / max_jobs) rows of consecutive jobs (as even as possible)."""
+    src, offs = [], [0]
+    for lab in range(len(offsets) - 1):
+        j0, j1 = int(offsets[lab]), int(offsets[lab + 1])
+        n = j1 - j0
+        pieces = max(1, -(-n // max_jobs)) if max_jobs > 0 else 1
+        for p in range(pieces):
+            src.append(lab)
+            offs.append(j0 + (n * (p + 1)) // pieces)
+    return np.asarray(src, dtype=np.int64), np.asarray(offs, dtype=np.int64)
+
+
 def _deal_rows(jobs_per_row: np.ndarray, world: int) -> list:
     """Swept rows per rank, balanced by branch jobs: rows in descending job count dealt
     round-robin, reversing direction every round (at most ceil(n / world) rows per rank).
@@ -427,6 +450,7 @@ class KnitPipeline:
         self.sweep_events = []  # (start, end) events around each step's sweep (all fragments)
         self.prep_events = []  # (sweep end, knit start): operand transforms + data-rank compression
         self.record_events = False
+        self.row_jobs = ROW_JOBS
         self.out_alloc = None  # how the last output buffer was allocated (new_out)
         self._plan()
 
@@ -453,15 +477,30 @@ class KnitPipeline:
     def _plan(self):
         T, be = self.T, self.be
         self.sweeps = []  # per fragment: device job tables and buffers, or None (dropped)
+        # per fragment: source label of each swept row when labels are split (ROW_JOBS), else None;
+        # and the number of swept rows
+        self.row_src, self.n_rows = [], []
         L = self.ops.num_terms
         self.term_range = _shard(L, self.rank, self.world) if self.mode == "reduce" else (0, L)
         self.place = {}  # gather mode: fragment -> position of each swept row in the gathered rows
         for i, fs in enumerate(self.frags):
             if fs.dropped:
                 self.sweeps.append(None)
+                self.row_src.append(None)
+                self.n_rows.append(fs.n_rows)
                 continue
             nl = fs.n_rows
             jobs = fs.jobs
+            src = None
+            if self.ops.transforms[i] is not None and self.row_jobs > 0 and jobs.n_jobs:
+                src, offs = _split_rows(jobs.label_offsets, self.row_jobs)
+                if len(src) > nl:
+                    jobs = JobTable(jobs.slot_mats, jobs.sign, offs, jobs.branch_bits)
+                    nl = len(src)
+                else:
+                    src = None
+            self.row_src.append(src)
+            self.n_rows.append(nl)
             lo = 0
             if self.mode in ("gather", "slice"):
                 per = -(-nl // self.world)
@@ -544,7 +583,7 @@ class KnitPipeline:
         self.split_a = (len(self.order) == 2 and len(live) == 2 and width_a % P == 0)
         self.xbuf = {}
         for i in live:
-            per = -(-self.frags[i].n_rows // P)
+            per = -(-self.n_rows[i] // P)
             width = 1 << self.frags[i].prog.m
             if self.mode == "slice" or (self.split_a and i == a_side):
                 bw = width // P
@@ -559,9 +598,11 @@ class KnitPipeline:
         for i, fs in enumerate(self.frags):
             place = self.place.get(i)
             if ops.transforms[i] is not None:
-                Wt = ops.transforms[i].T  # [swept rows, terms]
+                Wt = ops.transforms[i].T  # [labels, terms]
+                if self.row_src[i] is not None:  # split labels: every piece row takes its label's row
+                    Wt = Wt[self.row_src[i]]
                 if place is not None:  # rows as the collectives deliver them (rank-major, padded)
-                    Wg = np.zeros((self.world * -(-fs.n_rows // self.world), Wt.shape[1]))
+                    Wg = np.zeros((self.world * -(-self.n_rows[i] // self.world), Wt.shape[1]))
                     Wg[place] = Wt
                     Wt = Wg
                 self.transforms.append(be.to_device(Wt))

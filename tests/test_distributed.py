@@ -106,7 +106,7 @@ def test_multi_rank_pipeline_matches_oracle(case, mode, factored, world):
     np.testing.assert_allclose(res, ref, atol=1e-12, rtol=0)
 
 
-def _slice_worker(rank, world, port, case, data_rank, q, veto_rank=None):
+def _slice_worker(rank, world, port, case, data_rank, q, veto_rank=None, row_jobs=None):
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -117,9 +117,11 @@ def _slice_worker(rank, world, port, case, data_rank, q, veto_rank=None):
     try:
         from cpu_backend import CpuBackend
 
-        from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit
+        from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, pipeline
         from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
 
+        if row_jobs is not None:
+            pipeline.ROW_JOBS = row_jobs
         _, cut = _slice_case(case)
         pipe = KnitPipeline(VirtualCircuit(cut), rank=rank, world=world, factored=True, backend=CpuBackend(),
                             data_rank=data_rank)
@@ -151,9 +153,10 @@ def _slice_case(name):
     }[name]()
 
 
-@pytest.mark.parametrize("case,world,data_rank", [("hwe_p2", 2, True), ("hwe_p2", 4, True), ("cx_8x8", 2, True),
-                                                  ("cx_6x5", 2, True), ("hwe_p2", 2, False)])
-def test_slice_mode_matches_oracle(case, world, data_rank):
+@pytest.mark.parametrize("case,world,data_rank,row_jobs", [("hwe_p2", 2, True, None), ("hwe_p2", 4, True, None),
+                                                           ("cx_8x8", 2, True, None), ("cx_6x5", 2, True, None),
+                                                           ("hwe_p2", 2, False, None), ("cx_6x5", 2, True, 1)])
+def test_slice_mode_matches_oracle(case, world, data_rank, row_jobs):
     """slice mode: each rank writes the contiguous range [rank, rank + 1) * 2^N / world of the
     reference-ordered distribution; the slices concatenate (no permutation) to the oracle's dense
     knit within 1e-12, twice in a row. cx_8x8's knit has rank > 8 (the exact contraction of the
@@ -163,7 +166,8 @@ def test_slice_mode_matches_oracle(case, world, data_rank):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_slice_worker, args=(r, world, port, case, data_rank, q)) for r in range(world)]
+    procs = [ctx.Process(target=_slice_worker, args=(r, world, port, case, data_rank, q, None, row_jobs))
+             for r in range(world)]
     for p in procs:
         p.start()
     outs, sl, last_rank, fallbacks, incompressible, dev, prep = q.get(timeout=300)

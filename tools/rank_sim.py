@@ -152,8 +152,11 @@ def main():
         model.clear()
         pipe.record_events = True
         t0 = time.perf_counter()
+        host = 0.0
         for _ in range(args.steps):
+            h0 = time.perf_counter()
             pipe.step()
+            host += time.perf_counter() - h0
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / args.steps * 1e3
         pipe.sync_stats()
@@ -162,7 +165,7 @@ def main():
         prep = sum(s.elapsed_time(e) for s, e in pipe.prep_events) / max(len(pipe.prep_events), 1)
         M, N, K = pipe.gemm_shape()
         print(json.dumps({"workload": args.workload, "mode": pipe.mode, "world": world, "rank": args.rank,
-                          "slice": list(pipe.slice), "ms_per_step_no_xgmi": round(ms, 3),
+                          "slice": list(pipe.slice), "ms_per_step_no_xgmi": round(ms, 3), "host_ms_per_step": round(host / args.steps * 1e3, 3),
                           "sweep_ms": round(sweep, 3), "prep_ms": round(prep, 3), "knit_ms": round(knit, 3),
                           "knit_GBs": round(8 * M * N / (knit * 1e-3) / 1e9, 1), "accepted_rank": pipe.last_rank,
                           "received_bytes_per_step": {k: v // args.steps for k, v in recv.items()},

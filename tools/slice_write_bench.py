@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""The slice-mode write alone: qk_knit_outer_stream over [r 2^N / P, (r + 1) 2^N / P) of syc 32 5's
+compressed operands (taken from a one-GPU step) into a 2^N / P buffer, for P = 1, 2, 4, 8, on all
+CUs and on a 160-CU masked stream (the pipelined multi-GPU write), HIP events per launch.
+
+    python tools/slice_write_bench.py [--steps 10]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10)
+    args = ap.parse_args()
+    import torch
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting, engine
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    name, n, d, p, var = cutting.BASELINE_CONFIGS["syc_32_5_p2"]
+    cut = cutting.config_cut_circuit(name, n, d, p, var)[1]
+    pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
+    qs = pipe.sweep()
+    p_ = pipe._prep_dev_rank(qs)
+    torch.cuda.synchronize()
+    A2, B2, k = p_["A2"], p_["B2"], p_["k_eff"]
+    ia, ib = pipe.order[0], pipe.order[-1]
+    cA, cB = pipe.ops.clbits[ia], pipe.ops.clbits[ib]
+    N = pipe.N
+    del pipe
+    torch.cuda.empty_cache()
+    ctx = engine.get_context(0)
+    total = torch.cuda.get_device_properties(0).multi_processor_count
+    for streams in ("all", "masked160"):
+        if streams == "all":
+            s = torch.cuda.Stream()
+        else:
+            s = engine.cu_masked_stream(0, tuple(range(total - 96)))  # the write CUs of a 96-CU prep split
+        with torch.cuda.stream(s):
+            ctx.bind_stream()
+            for P in (1, 2, 4, 8):
+                n_out = (1 << N) // P
+                out, owner = engine.out_buffer(ctx, n_out)
+                ts = []
+                for it in range(args.steps + 2):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    engine.knit_outer_stream(ctx, A2, B2, cA, cB, N, out, o_begin=(P - 1) * n_out, o_count=n_out,
+                                             k_dev=k)
+                    b.record()
+                    ts.append((a, b))
+                torch.cuda.synchronize()
+                ms = [a.elapsed_time(b) for a, b in ts[2:]]
+                avg = sum(ms) / len(ms)
+                print(json.dumps({"streams": streams, "world": P, "write_ms": round(avg, 4),
+                                  "GBs": round(8 * n_out / avg / 1e6, 1), "min_ms": round(min(ms), 4)}), flush=True)
+                del out, owner
+        ctx.bind_stream()
+
+
+if __name__ == "__main__":
+    main()
