@@ -1500,8 +1500,9 @@ constexpr int OB_WG_PER_CU = 64;  // bench, one box: 5.82 ms per write at 64, 5.
 int outer_blocked_tile(int nbits, int64_t K, uint64_t maskA, uint64_t maskB, int align_bits, bool* b_global) {
     int top = nbits < 16 ? nbits : 16;
     top = align_bits < top ? align_bits : top;
-    // QKNIT_OB_TB (A/B experiments): cap the task width
-    static const int cap_tb = getenv("QKNIT_OB_TB") ? atoi(getenv("QKNIT_OB_TB")) : 16;
+    // QKNIT_OB_TB (A/B experiments, read at every call): cap the task width
+    const char* cap_env = getenv("QKNIT_OB_TB");
+    const int cap_tb = cap_env ? atoi(cap_env) : 16;
     top = cap_tb < top ? cap_tb : top;
     int both = 0, aonly = 0;
     for (int tb = top; tb >= 9; --tb) {
@@ -1868,7 +1869,8 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
         const int64_t tasks = o_count >> tb;
         // workgroups per CU of the grid-stride launch; QKNIT_OB_WG_PER_CU=0: one workgroup per task
         // (workgroups retire as they finish, so work on other streams can take their slots)
-        static const int wgpc = getenv("QKNIT_OB_WG_PER_CU") ? atoi(getenv("QKNIT_OB_WG_PER_CU")) : OB_WG_PER_CU;
+        const char* wgpc_env = getenv("QKNIT_OB_WG_PER_CU");  // read at every launch (A/B experiments)
+        const int wgpc = wgpc_env ? atoi(wgpc_env) : OB_WG_PER_CU;
         const int64_t G0 = wgpc > 0 ? (int64_t)cus * wgpc : tasks;
         OuterBlockedArgs b{(int)K, tb, A, lda, B, ldb, (uint32_t)maskA, (uint32_t)maskB, o_begin >> tb,
                            (o_begin >> tb) + tasks, o_begin, k_dev, out};

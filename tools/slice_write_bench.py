@@ -16,6 +16,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--streams", nargs="+", default=["all", "masked160"])
+    ap.add_argument("--where", nargs="+", default=["last"],
+                    help="last: the last slice into its own mapping; first: the first slice; "
+                         "inbig: the first slice into the first part of a full-size mapping")
     args = ap.parse_args()
     import torch
 
@@ -36,28 +41,35 @@ def main():
     torch.cuda.empty_cache()
     ctx = engine.get_context(0)
     total = torch.cuda.get_device_properties(0).multi_processor_count
-    for streams in ("all", "masked160"):
+    for streams in args.streams:
         if streams == "all":
             s = torch.cuda.Stream()
         else:
             s = engine.cu_masked_stream(0, tuple(range(total - 96)))  # the write CUs of a 96-CU prep split
         with torch.cuda.stream(s):
             ctx.bind_stream()
-            for P in (1, 2, 4, 8):
+            big = None
+            for P, where in [(P, w) for P in args.worlds for w in args.where]:
                 n_out = (1 << N) // P
-                out, owner = engine.out_buffer(ctx, n_out)
+                if where == "inbig":
+                    if big is None:
+                        big = engine.out_buffer(ctx, 1 << N)
+                    out, owner = big[0][:n_out], None
+                else:
+                    out, owner = engine.out_buffer(ctx, n_out)
+                o_begin = (P - 1) * n_out if where == "last" else 0
                 ts = []
                 for it in range(args.steps + 2):
                     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     a.record()
-                    engine.knit_outer_stream(ctx, A2, B2, cA, cB, N, out, o_begin=(P - 1) * n_out, o_count=n_out,
+                    engine.knit_outer_stream(ctx, A2, B2, cA, cB, N, out, o_begin=o_begin, o_count=n_out,
                                              k_dev=k)
                     b.record()
                     ts.append((a, b))
                 torch.cuda.synchronize()
                 ms = [a.elapsed_time(b) for a, b in ts[2:]]
                 avg = sum(ms) / len(ms)
-                print(json.dumps({"streams": streams, "world": P, "write_ms": round(avg, 4),
+                print(json.dumps({"streams": streams, "world": P, "where": where, "wg_per_cu": os.environ.get("QKNIT_OB_WG_PER_CU", "64"), "write_ms": round(avg, 4),
                                   "GBs": round(8 * n_out / avg / 1e6, 1), "min_ms": round(min(ms), 4)}), flush=True)
                 del out, owner
         ctx.bind_stream()
