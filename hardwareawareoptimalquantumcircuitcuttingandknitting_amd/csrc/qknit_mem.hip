@@ -15,6 +15,8 @@
 //                                   last rounded up to the allocation granularity) mapped
 //                                   read-write for ctx's device at a 1-GiB-aligned address;
 //                                   below 1 GiB one chunk at an alignment of its power-of-two size
+//   qk_out_write_rate(ctx, p, n, &gbs)  GB/s of the knit's static store order over [p, p + n) (one
+//                                   timed launch after a warm one; the contents are overwritten)
 //   qk_out_free(ctx, ptr)           synchronizes the device, unmaps, releases the physical chunks;
 //                                   the virtual range stays reserved (retired, never mapped again)
 //
@@ -160,6 +162,44 @@ int qk_out_free(qk_ctx* ctx, void* ptr) {
     hipError_t e = hipDeviceSynchronize();
     unmap_retire(ptr, m);
     if (e != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_free: hipDeviceSynchronize", e);
+    return QK_OK;
+}
+
+// The static store order of the knit's write (512-KiB blocks, a grid-stride over them): the rate
+// qk_out_write_rate reports for a mapping.
+__global__ __launch_bounds__(256) void qk_out_probe_kernel(double* __restrict__ out, int64_t nblocks) {
+    typedef double d2_t __attribute__((ext_vector_type(2)));
+    for (int64_t t = blockIdx.x; t < nblocks; t += gridDim.x) {
+        d2_t* o = reinterpret_cast<d2_t*>(out) + (t << 15);
+#pragma unroll 4
+        for (int it = 0; it < 128; ++it) o[256 * it + threadIdx.x] = (d2_t){0.0, 0.0};
+    }
+}
+
+int qk_out_write_rate(qk_ctx* ctx, void* ptr, int64_t bytes, double* gbs) {
+    if (!ctx || !ptr || !gbs || bytes < (int64_t(1) << 19))
+        return mem_fail(ctx, QK_EARG, "qk_out_write_rate: need a context, a buffer of >= 512 KiB, an out pointer", hipSuccess);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_write_rate: hipSetDevice", e);
+    const int64_t nblocks = bytes >> 19;
+    hipEvent_t t0, t1;
+    if ((e = hipEventCreate(&t0)) != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_write_rate: event", e);
+    if ((e = hipEventCreate(&t1)) != hipSuccess) {
+        (void)hipEventDestroy(t0);
+        return mem_fail(ctx, QK_EHIP, "qk_out_write_rate: event", e);
+    }
+    const dim3 grid((unsigned)(ctx->cus > 0 ? ctx->cus : 256) * 64);
+    hipLaunchKernelGGL(qk_out_probe_kernel, grid, dim3(256), 0, ctx->stream, (double*)ptr, nblocks);  // warm
+    (void)hipEventRecord(t0, ctx->stream);
+    hipLaunchKernelGGL(qk_out_probe_kernel, grid, dim3(256), 0, ctx->stream, (double*)ptr, nblocks);
+    (void)hipEventRecord(t1, ctx->stream);
+    e = hipEventSynchronize(t1);
+    float ms = 0.0f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, t0, t1);
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    if (e != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_write_rate", e);
+    *gbs = ms > 0 ? (double)(nblocks << 19) / (ms * 1e6) : 0.0;
     return QK_OK;
 }
 

@@ -192,15 +192,48 @@ class MappedOut:
 
 
 OUT_MAPPED_MIN_BYTES = int(os.environ.get("QKNIT_OUT_MAPPED_MIN_BYTES", str(1 << 30)))  # below: torch allocation
+# Large outputs are kept only if they write fast. The knit writes its 2^32 fp64 outputs at 4.8-5.0 ms
+# into most mappings and at 5.2-5.9 ms into others — fixed per mapping (stable over seconds), the same
+# for every store order tried (task widths 2^12-2^16, compact or spread windows, other grids), for
+# 1-GiB-aligned and unaligned addresses, chunks created per buffer or all first (tools/write_probe11-13,
+# out_mapping_tb.py). qk_out_write_rate times the knit's store order into a new mapping
+# (one 5-ms launch for 34 GB); below OUT_FAST_GBS another mapping is made while the slow one is held
+# (so its memory cannot come straight back), up to OUT_TRIES, the fastest kept and the others freed.
+# Extra tries only with free memory for them (2 GiB spare): a 2^32 output holds at most OUT_TRIES x
+# 34 GB for the few milliseconds of the selection.
+OUT_SELECT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_SELECT_MIN_BYTES", str(16 << 30)))
+OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "6850"))
+OUT_TRIES = int(os.environ.get("QKNIT_OUT_TRIES", "3"))
+out_selections: list = []  # per selected output: the candidates' write rates (GB/s), the kept one first
+
+
+def _out_rate(ctx: Context, owner) -> float:
+    g = ctypes.c_double()
+    ctx.check(ctx.lib.qk_out_write_rate(ctx.handle, ctypes.c_void_p(owner.ptr), 8 * owner.n, ctypes.byref(g)),
+              "qk_out_write_rate")
+    return g.value
 
 
 def out_buffer(ctx: Context, n: int):
     """(tensor [n] float64, owner or None): a ``qk_out_alloc`` mapping for outputs of at least
-    OUT_MAPPED_MIN_BYTES, torch's allocator below that. Contents are undefined."""
+    OUT_MAPPED_MIN_BYTES (from OUT_SELECT_MIN_BYTES on, one that writes fast: see above), torch's
+    allocator below that. Contents are undefined."""
     T = torch()
     if 8 * n < OUT_MAPPED_MIN_BYTES:
         return T.empty(n, dtype=T.float64, device=T.device("cuda", ctx.device)), None
     owner = MappedOut(ctx, n)
+    if 8 * n >= OUT_SELECT_MIN_BYTES and OUT_TRIES > 1:
+        tried = [(_out_rate(ctx, owner), owner)]
+        while tried[-1][0] < OUT_FAST_GBS and len(tried) < OUT_TRIES:
+            free, _ = T.cuda.mem_get_info(ctx.device)
+            if free < 8 * n + (2 << 30):
+                break
+            cand = MappedOut(ctx, n)
+            tried.append((_out_rate(ctx, cand), cand))
+        best = max(range(len(tried)), key=lambda i: tried[i][0])
+        owner = tried[best][1]
+        out_selections.append([round(tried[best][0], 1)] + [round(r, 1) for i, (r, _) in enumerate(tried) if i != best])
+        del tried  # the others are unmapped here
     return owner.tensor(), owner
 
 

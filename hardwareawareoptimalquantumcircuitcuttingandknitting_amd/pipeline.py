@@ -1293,13 +1293,11 @@ class KnitPipeline:
         out[ia], out[ib] = A, B
         return self._contract(out)
 
-    # The output buffer (round 4): the write kernel's rate depended on the 2^N buffer's placement — 4.8
-    # or 5.9 ms for the same kernel into different 34 GB hipMalloc blocks — and round 3 timed up to six
-    # candidate allocations to keep a fast one. The slow mode follows the virtual-to-physical mapping, not
-    # the memory: the same writes into buffers mapped from 1-GiB physical allocations at 1-GiB-aligned
-    # addresses run at 4.83-4.86 ms whichever of the device's memory backs them (tools/write_probe10,
-    # DESIGN.md §4). Large outputs are therefore allocated that way (qk_out_alloc, engine.out_buffer);
-    # small ones (< 1 GiB) from torch.
+    # The output buffer (round 4): the write kernel's rate depends on the 2^N buffer — 4.8-5.0 ms for
+    # most 34 GB buffers, 5.2-5.9 ms for others, fixed per buffer, for hipMalloc blocks and 1-GiB-chunk
+    # mappings alike and for every store order tried. Large outputs are mapped from 1-GiB
+    # chunks (qk_out_alloc) and kept only if the knit's store order writes fast into them
+    # (engine.out_buffer: at most OUT_TRIES candidates, the fastest kept); small ones come from torch.
 
     def _alloc_out(self, mats):
         """This rank's output buffer: 2^N entries (single / reduce), its slice (slice mode), or its block
@@ -1320,8 +1318,11 @@ class KnitPipeline:
         if alloc is None:
             self.out_alloc = "backend"
             return self.be.zeros((n,), self.T.float64) if zero else self.be.empty((n,), self.T.float64)
+        n_sel = len(engine.out_selections)
         out, owner = alloc(n)
         self.out_alloc = "qk_out_alloc (1-GiB mapped chunks)" if owner is not None else "torch"
+        if len(engine.out_selections) > n_sel:  # candidates' write rates, the kept one first
+            self.out_alloc += f", write-rate selected: {engine.out_selections[-1]} GB/s"
         self._last_owner = owner
         if zero:
             out.zero_()

@@ -105,15 +105,18 @@ int qk_stream_cu_count(int device, void* stream, int* cus);
 const char* qk_version(void);
 
 /* Output buffers for the write-bound knit kernels (qknit_mem.hip): at least `bytes` of device memory
- * built from 1-GiB physical allocations (hipMemCreate) mapped read-write at a 1-GiB-aligned virtual
- * address (below 1 GiB: one allocation at its power-of-two alignment). The 2^32-entry knit writes at
- * 4.83-4.86 ms into every such buffer and at 4.8 or 5.9 ms into plain hipMalloc blocks, depending
- * on the block. Replaces the output dict the reference allocates per merge
- * (quasi_distr.py:55-60): the caller owns the buffer; qk_out_free synchronizes the device and
- * unmaps it. qk_out_mapped_bytes: the mapped size of a qk_out_alloc pointer (QK_EARG otherwise). */
+ * built from 1-GiB physical allocations (hipMemCreate) mapped read-write (below 1 GiB: one
+ * allocation). Replaces the output dict the reference allocates per merge (quasi_distr.py:55-60): the
+ * caller owns the buffer; qk_out_free synchronizes the device, unmaps it and releases its memory (its
+ * address range is never handed out again). qk_out_mapped_bytes: the mapped size of a qk_out_alloc
+ * pointer (QK_EARG otherwise). qk_out_write_rate: GB/s of the knit's store order into [ptr, ptr +
+ * bytes) (one timed launch; overwrites the contents) — the 2^32-entry knit writes at 4.8-5.0 ms into
+ * most buffers and at 5.2-5.9 ms into others, fixed per buffer, whatever the store order (DESIGN.md
+ * §4), so the engine keeps a large output only if it writes fast (engine.out_buffer). */
 int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr);
 int qk_out_free(qk_ctx* ctx, void* ptr);
 int qk_out_mapped_bytes(const void* ptr, int64_t* bytes);
+int qk_out_write_rate(qk_ctx* ctx, void* ptr, int64_t bytes, double* gbs);
 
 /* Workspace (bytes) qk_sweep needs for n_jobs jobs of prog (0 in PACKED mode). */
 int qk_sweep_workspace_bytes(const qk_program* prog, int64_t n_jobs, int64_t* bytes);

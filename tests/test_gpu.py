@@ -722,6 +722,40 @@ def test_mapped_output_buffer_steps_match_oracle(T, case, monkeypatch):
     assert pipe.take_out().data_ptr() == owner.ptr  # nothing holds it: handed out again
 
 
+def test_output_selection_keeps_fastest_and_frees_the_others(T, monkeypatch):
+    """engine.out_buffer's write-rate selection (forced here on a 512-KiB output: every candidate
+    tried): OUT_TRIES mappings are made and timed, the fastest is kept (its rate first in
+    out_selections), the others are unmapped, and the knit into the kept one equals the oracle."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import _lib
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    monkeypatch.setattr(engine, "OUT_MAPPED_MIN_BYTES", 0)
+    monkeypatch.setattr(engine, "OUT_SELECT_MIN_BYTES", 0)
+    monkeypatch.setattr(engine, "OUT_FAST_GBS", float("inf"))
+    monkeypatch.setattr(engine, "OUT_TRIES", 3)
+    made = []
+    real = engine.MappedOut
+
+    class Spy(real):
+        def __init__(self, ctx, n):
+            super().__init__(ctx, n)
+            made.append(self.ptr)
+
+    monkeypatch.setattr(engine, "MappedOut", Spy)
+    cut = circuits.two_fragment("cx", 8, 8, n_cuts=4)[1]
+    pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
+    got = pipe.step().cpu().numpy()
+    np.testing.assert_allclose(got, dense.run_dense(cut), atol=1e-12, rtol=0)
+    sel = engine.out_selections[-1]
+    assert len(sel) == 3 and sel[0] == max(sel) and all(r > 0 for r in sel)
+    assert "write-rate selected" in pipe.out_alloc and len(made) == 3
+    kept = pipe.out.data_ptr()
+    size = ctypes.c_int64()
+    for ptr in made:
+        rc = _lib.lib().qk_out_mapped_bytes(ctypes.c_void_p(ptr), ctypes.byref(size))
+        assert (rc == 0) == (ptr == kept)
+
+
 def test_mapped_outputs_freed_and_remapped_read_back_exactly(T, monkeypatch):
     """Drop-in calls that keep some results and drop others: mappings are freed and new ones made
     between calls. Each result equals the oracle (1e-12) read back by the D2H copy. Freed ranges'
