@@ -267,8 +267,8 @@ def cpu_baseline_same(pipe, cut, qs_host, n_inst_sample: int = 8, out_block_bits
     t_sweep = t_batch * -(-swept // done)
     ia, ib = pipe.order[0], pipe.order[-1]
     t1 = time.perf_counter()
-    A = pipe.ops.transforms[ia] @ qs_host[ia]
-    B = pipe.ops.transforms[ib] @ qs_host[ib]
+    A = pipe.row_transform(ia) @ qs_host[ia]
+    B = pipe.row_transform(ib) @ qs_host[ib]
     f = data_rank.rank_factors(A @ A.T, B @ B.T)
     TA, TB = f
     A2, B2 = TA @ A, TB @ B
@@ -656,6 +656,7 @@ def main():
             "instances_ref": counts["instances_ref"],
             "instances_unique": counts["instances_unique"],
             "instances_swept": counts["instances_swept"],
+            "rows_swept": counts["rows_swept"],
             "branch_jobs": counts["branch_jobs"],
             "labels": counts["labels_ref"],
             "knit": ("direct" if args.direct else

@@ -74,6 +74,16 @@ def _shard(n: int, rank: int, world: int) -> tuple[int, int]:
 # consecutive jobs whose sum is its row: the transforms repeat its row (Wt[src]), so the knit
 # operands X = Wt^T q are the same sums.
 ROW_JOBS = int(os.environ.get("QKNIT_ROW_JOBS", "4"))
+# Swept rows the knit does not depend on are not swept (QKNIT_ROW_PRUNE: relative threshold, 0: off).
+# A two-fragment knit is R = q_0^T C q_1 with the core C = W_0^T W_1 (engine._compress_core); a swept
+# row whose column of the compressed transform is zero to rounding — max |W[:, j]| below ROW_PRUNE x
+# max |W| — multiplies nothing: on syc 32 5, 192 of the column side's 256 light-cone basis rows (their
+# core columns are exactly 0 for 42 of them and at most 1e-14 of the core's largest entry for the
+# others, cancellations left at rounding level; the compressed transform's columns for them are
+# 1e-20..2e-15 against entries of 1e-4..1.2 for the 64 others). Their 500 of the fragment's 625 branch
+# jobs are dropped, and the operand transforms lose those rows; every operand X = Wt^T q changes by
+# at most sum_j |W[:, j]| |q_j| <= 192 x 2e-15 (q: probabilities), below the rounding of X itself.
+ROW_PRUNE = float(os.environ.get("QKNIT_ROW_PRUNE", "1e-12"))
 
 
 def _split_rows(offsets: np.ndarray, max_jobs: int):
@@ -451,6 +461,7 @@ class KnitPipeline:
         self.prep_events = []  # (sweep end, knit start): operand transforms + data-rank compression
         self.record_events = False
         self.row_jobs = ROW_JOBS
+        self.row_prune = ROW_PRUNE
         self.out_alloc = None  # how the last output buffer was allocated (new_out)
         self._plan()
 
@@ -477,8 +488,8 @@ class KnitPipeline:
     def _plan(self):
         T, be = self.T, self.be
         self.sweeps = []  # per fragment: device job tables and buffers, or None (dropped)
-        # per fragment: source label of each swept row when labels are split (ROW_JOBS), else None;
-        # and the number of swept rows
+        # per fragment: source label of each swept row when rows are pruned (ROW_PRUNE) or labels split
+        # (ROW_JOBS), else None; and the number of swept rows
         self.row_src, self.n_rows = [], []
         L = self.ops.num_terms
         self.term_range = _shard(L, self.rank, self.world) if self.mode == "reduce" else (0, L)
@@ -492,13 +503,18 @@ class KnitPipeline:
             nl = fs.n_rows
             jobs = fs.jobs
             src = None
-            if self.ops.transforms[i] is not None and self.row_jobs > 0 and jobs.n_jobs:
-                src, offs = _split_rows(jobs.label_offsets, self.row_jobs)
-                if len(src) > nl:
+            W = self.ops.transforms[i]
+            if W is not None and self.row_prune > 0 and jobs.n_jobs:
+                cm = np.abs(np.asarray(W)).max(axis=0)  # per swept row: its largest transform entry
+                live = np.flatnonzero(cm > self.row_prune * cm.max())
+                if 0 < live.size < nl:
+                    src, jobs, nl = live, jobs.take(live), live.size
+            if W is not None and self.row_jobs > 0 and jobs.n_jobs:
+                piece_src, offs = _split_rows(jobs.label_offsets, self.row_jobs)
+                if len(piece_src) > nl:
                     jobs = JobTable(jobs.slot_mats, jobs.sign, offs, jobs.branch_bits)
-                    nl = len(src)
-                else:
-                    src = None
+                    nl = len(piece_src)
+                    src = piece_src if src is None else src[piece_src]
             self.row_src.append(src)
             self.n_rows.append(nl)
             lo = 0
@@ -599,7 +615,7 @@ class KnitPipeline:
             place = self.place.get(i)
             if ops.transforms[i] is not None:
                 Wt = ops.transforms[i].T  # [labels, terms]
-                if self.row_src[i] is not None:  # split labels: every piece row takes its label's row
+                if self.row_src[i] is not None:  # pruned / split rows: every row takes its label's row
                     Wt = Wt[self.row_src[i]]
                 if place is not None:  # rows as the collectives deliver them (rank-major, padded)
                     Wg = np.zeros((self.world * -(-self.n_rows[i] // self.world), Wt.shape[1]))
@@ -1473,12 +1489,23 @@ class KnitPipeline:
         return out
 
     # ------------------------------------------------------------------ accounting
+    def row_transform(self, i: int):
+        """Host transform ``[terms, swept rows]`` of fragment i's operand ``X = W q`` over the rows the
+        sweep writes (``ops.transforms[i]`` restricted / repeated by ``row_src``), or None."""
+        W = self.ops.transforms[i]
+        if W is None or self.row_src[i] is None:
+            return W
+        return np.ascontiguousarray(np.asarray(W)[:, self.row_src[i]])
+
     def instance_counts(self) -> dict:
         """Reference instance count (``run.py:37-39``: sum of per-fragment label lists) and jobs."""
         return {
             "instances_ref": int(sum(len(fs.labels) for fs in self.frags)),
             "instances_unique": int(sum(len(fs.unique_labels) for fs in self.frags)),
-            "instances_swept": int(sum(fs.n_rows for fs in self.frags)),
+            # instance labels the sweep simulates (pruned rows left out), and the rows it writes (split)
+            "instances_swept": int(sum((fs.n_rows if src is None else np.unique(src).size)
+                                       for fs, src in zip(self.frags, self.row_src))),
+            "rows_swept": int(sum(self.n_rows)),
             "branch_jobs": int(sum(fs.jobs.n_jobs for fs in self.frags if not fs.dropped)),
             "labels": int(self.ops.num_terms),
             "labels_ref": int(np.prod([v.operation.num_instantiations for v in self.virt.vgate_instructions])),
