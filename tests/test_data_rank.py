@@ -112,6 +112,47 @@ def test_split_swept_rows_match_oracle(case, row_jobs, monkeypatch):
     np.testing.assert_allclose(pipe.step().numpy(), dense.run_dense(cut), atol=1e-12, rtol=0)
 
 
+def test_pruned_rows_of_syc_32_5_carry_no_weight(monkeypatch):
+    """ROW_PRUNE on the headline plan (no sweep: the plan only): 64 of the column side's 256 light-cone
+    basis rows are swept (125 of 625 branch jobs), every row of the row side; the rows left out have
+    core columns (C = W_0^T W_1 of the uncompressed factored transforms) of at most 1e-14 of the core's
+    largest entry, and the kept rows' transforms give the same core to rounding. With ROW_PRUNE = 0
+    every row is swept."""
+    from cpu_backend import CpuBackend
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting, engine, pipeline
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    name, n, d, p, var = cutting.BASELINE_CONFIGS["syc_32_5_p2"]
+    _, cut, _ = cutting.config_cut_circuit(name, n, d, p, var)
+    virt = VirtualCircuit(cut)
+    monkeypatch.setattr(pipeline, "ROW_JOBS", 0)
+    pipe = KnitPipeline(virt, factored=True, backend=CpuBackend(), data_rank=True)
+    ia, ib = pipe.order[0], pipe.order[-1]
+    labels = [fs.n_rows for fs in pipe.frags]
+    kept = [np.arange(labels[i]) if pipe.row_src[i] is None else pipe.row_src[i] for i in range(2)]
+    assert sorted(len(k) for k in kept) == [64, 64] and sorted(labels) == [64, 256]
+    assert sum(sw["n_jobs"] for sw in pipe.sweeps) == 250
+    raw = engine.knit_operands(virt, pipe.frags, True, compress=False)
+    W0, W1 = (np.asarray(w) for w in raw.transforms)
+    C = W0.T @ W1  # [rows of fragment 0, rows of fragment 1]
+    big = np.abs(C).max()
+    dead0 = np.setdiff1d(np.arange(labels[0]), kept[0])
+    dead1 = np.setdiff1d(np.arange(labels[1]), kept[1])
+    assert dead0.size + dead1.size == 192
+    if dead0.size:
+        assert np.abs(C[dead0]).max() <= 1e-14 * big
+    if dead1.size:
+        assert np.abs(C[:, dead1]).max() <= 1e-14 * big
+    # the compressed transforms restricted to the kept rows reproduce the core on them
+    T0, T1 = pipe.row_transform(0), pipe.row_transform(1)
+    Ck = T0.T @ T1
+    assert np.abs(Ck - C[np.ix_(kept[0], kept[1])]).max() <= 1e-10 * big
+    monkeypatch.setattr(pipeline, "ROW_PRUNE", 0.0)
+    full = KnitPipeline(virt, factored=True, backend=CpuBackend(), data_rank=True)
+    assert full.n_rows == labels and all(s is None for s in full.row_src)
+
+
 def test_split_rows_offsets():
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import _split_rows
 

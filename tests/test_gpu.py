@@ -680,6 +680,32 @@ def test_syc_32_5_data_rank_step_matches_exact_step(T):
     T.cuda.empty_cache()
 
 
+@pytest.mark.slow
+def test_syc_32_5_pruned_rows_step_matches_unpruned_step(T, monkeypatch):
+    """Row pruning (pipeline.ROW_PRUNE: the 192 column-side basis rows whose compressed transform
+    columns are zero to rounding are not swept, 250 of 750 branch jobs run) against the step that
+    sweeps every row (ROW_PRUNE = 0), both through the data-rank write: every one of the 2^32 outputs
+    within 1e-13."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import pipeline
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    cut = cutting.config_cut_circuit("syc", 32, 5, 2, "ref")[1]
+    pruned = KnitPipeline(VirtualCircuit(cut), factored=True)
+    assert sum(sw["n_jobs"] for sw in pruned.sweeps) == 250
+    got = pruned.step()
+    monkeypatch.setattr(pipeline, "ROW_PRUNE", 0.0)
+    full = KnitPipeline(VirtualCircuit(cut), factored=True)
+    assert sum(sw["n_jobs"] for sw in full.sweeps) == 750
+    ref = full.step()
+    pruned.sync_stats()
+    full.sync_stats()
+    assert pruned.rank_fallbacks == 0 and full.rank_fallbacks == 0
+    T.cuda.synchronize()
+    assert _chunked_max_abs_diff(got, ref) <= 1e-13
+    del pruned, full, got, ref
+    T.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("case", ["hwe_p2", "cx_8x8"])
 def test_mapped_output_buffer_steps_match_oracle(T, case, monkeypatch):
     """Outputs in a qk_out_alloc mapping (OUT_MAPPED_MIN_BYTES=0: small outputs mapped too, one
