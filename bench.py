@@ -683,11 +683,12 @@ def main():
             "kernel": "per-program sweep kernels (sweep_codegen + hiprtc): shared INIT tiles (one per distinct "
                       "INIT-slot prefix), FINAL pass on narrowed single-wave tiles summing each label's branch "
                       "jobs, labels heaviest first, XCD-grouped tile order (all fragments, per step, this rank)",
-            "bound": "VALU issue: the FINAL pass (89% of the sweep) keeps the VALU busy 63% of its cycles, 53% "
-                     "on f64 instructions (mostly adds: the normalised +-1/+-i gate entries fold multiplies "
-                     "away, so flop rates understate it), LDS bank conflicts 23% of its LDS cycles, clock 1.9 "
-                     "GHz; the INIT pass (11%) is one wave's serial op chain; HBM moves ~0.2 GB per step "
-                     "(counters, profiles/r04d_sweep_pmc.json)",
+            "bound": "latency: 250 branch jobs after row pruning (the column side's 192 rows the knit does not "
+                     "depend on are not swept; 750 before): the FINAL pass is 8320 single-wave workgroups at 2 "
+                     "waves per SIMD (170 VGPRs), VALU busy 0.46 of its cycles, f64 issue 0.37 (mostly adds: the "
+                     "normalised +-1/+-i gate entries fold multiplies away), waves waiting 0.33 of their cycles; "
+                     "the INIT pass is one wave's serial op chain per prefix; HBM ~0.09 GB per step (counters, "
+                     "profiles/r04s2_sweep_pmc.json; before pruning r04d_sweep_pmc.json: VALU busy 0.63)",
             "ms_per_step": sweep_ms,
             "branch_jobs": counts["branch_jobs"],
             "hbm_bytes_model": traffic["hbm"],

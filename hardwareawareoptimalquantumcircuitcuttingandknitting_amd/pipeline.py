@@ -490,7 +490,7 @@ class KnitPipeline:
         self.sweeps = []  # per fragment: device job tables and buffers, or None (dropped)
         # per fragment: source label of each swept row when rows are pruned (ROW_PRUNE) or labels split
         # (ROW_JOBS), else None; and the number of swept rows
-        self.row_src, self.n_rows = [], []
+        self.row_src, self.n_rows, self.plan_jobs = [], [], []  # plan_jobs: branch jobs swept (all ranks)
         L = self.ops.num_terms
         self.term_range = _shard(L, self.rank, self.world) if self.mode == "reduce" else (0, L)
         self.place = {}  # gather mode: fragment -> position of each swept row in the gathered rows
@@ -499,6 +499,7 @@ class KnitPipeline:
                 self.sweeps.append(None)
                 self.row_src.append(None)
                 self.n_rows.append(fs.n_rows)
+                self.plan_jobs.append(0)
                 continue
             nl = fs.n_rows
             jobs = fs.jobs
@@ -517,6 +518,7 @@ class KnitPipeline:
                     src = piece_src if src is None else src[piece_src]
             self.row_src.append(src)
             self.n_rows.append(nl)
+            self.plan_jobs.append(jobs.n_jobs)
             lo = 0
             if self.mode in ("gather", "slice"):
                 per = -(-nl // self.world)
@@ -1506,7 +1508,8 @@ class KnitPipeline:
             "instances_swept": int(sum((fs.n_rows if src is None else np.unique(src).size)
                                        for fs, src in zip(self.frags, self.row_src))),
             "rows_swept": int(sum(self.n_rows)),
-            "branch_jobs": int(sum(fs.jobs.n_jobs for fs in self.frags if not fs.dropped)),
+            "branch_jobs": int(sum(self.plan_jobs)),  # swept (pruned rows left out), all ranks
+            "branch_jobs_all_rows": int(sum(fs.jobs.n_jobs for fs in self.frags if not fs.dropped)),
             "labels": int(self.ops.num_terms),
             "labels_ref": int(np.prod([v.operation.num_instantiations for v in self.virt.vgate_instructions])),
             "terms_factored": int(self.ops.factored_terms or self.ops.num_terms),
