@@ -1334,6 +1334,7 @@ struct OuterBlockedArgs {
     int64_t o_begin;
     const int32_t* kdev;
     double* __restrict__ out;
+    int64_t spread;  // task order: the i-th task taken is (i % spread) * (n / spread) + i / spread
 };
 
 // BG: the B operand is read from global memory (L2: the task's B indices are one contiguous range
@@ -1362,7 +1363,9 @@ __global__ __launch_bounds__(256) void qk_knit_outer_blocked_kernel(OuterBlocked
     __syncthreads();
     const uint32_t r0 = tab[0][0][(2 * threadIdx.x) & 255], c0 = tab[1][0][(2 * threadIdx.x) & 255];
     const int iters = (1 << a.TB) / 512;
-    for (int64_t t = a.task_begin + blockIdx.x; t < a.task_end; t += gridDim.x) {
+    const int64_t n_tasks = a.task_end - a.task_begin, per_part = n_tasks / a.spread;
+    for (int64_t i = blockIdx.x; i < n_tasks; i += gridDim.x) {
+        const int64_t t = a.task_begin + (i % a.spread) * per_part + i / a.spread;
         const uint32_t base = (uint32_t)(t << a.TB);
         const uint32_t ah = pext32(base, a.maskA), bh = pext32(base, a.maskB);
         __syncthreads();  // the previous task's readers are done with the stage
@@ -1872,8 +1875,16 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
         const char* wgpc_env = getenv("QKNIT_OB_WG_PER_CU");  // read at every launch (A/B experiments)
         const int wgpc = wgpc_env ? atoi(wgpc_env) : OB_WG_PER_CU;
         const int64_t G0 = wgpc > 0 ? (int64_t)cus * wgpc : tasks;
+        // Task order: with >= 4 tasks per workgroup the i-th task taken is (i % 8) x (tasks / 8) + i / 8, so
+        // consecutive workgroups write 8 far-apart parts of the range at once: 1% faster on syc 32 5's
+        // 2^32 outputs (4.82-4.90 vs 4.85-4.96 ms on each of 4 buffers, tools/out_mapping_tb.py), slower
+        // for one-task-per-workgroup slices (0.80 vs 0.75 ms at 2^29, tools/slice_write_bench.py).
+        // QKNIT_OB_SPREAD (A/B experiments, read per launch) sets the part count.
+        const char* spread_env = getenv("QKNIT_OB_SPREAD");
+        int64_t spread = spread_env ? atoll(spread_env) : (tasks >= 4 * G0 ? 8 : 1);
+        if (spread < 1 || tasks % spread) spread = 1;
         OuterBlockedArgs b{(int)K, tb, A, lda, B, ldb, (uint32_t)maskA, (uint32_t)maskB, o_begin >> tb,
-                           (o_begin >> tb) + tasks, o_begin, k_dev, out};
+                           (o_begin >> tb) + tasks, o_begin, k_dev, out, spread};
         const dim3 grid((unsigned)(tasks < G0 ? tasks : G0));
         if (bg)
             hipLaunchKernelGGL(qk_knit_outer_blocked_kernel<true>, grid, dim3(256), stage, ctx->stream, b);

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <map>
 #include <mutex>
@@ -102,8 +103,11 @@ int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr) {
     e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum);
     if (e != hipSuccess || gran == 0) return mem_fail(ctx, QK_EHIP, "qk_out_alloc: allocation granularity", e);
     size_t want = ((size_t)bytes + gran - 1) / gran * gran;
-    size_t chunk = OUT_CHUNK, align = OUT_CHUNK;
-    if (want < OUT_CHUNK) {  // one chunk, aligned to its power-of-two size
+    // QKNIT_OUT_CHUNK_MB (A/B experiments, read per call): physical chunk size, a multiple of the granularity
+    const char* chunk_env = getenv("QKNIT_OUT_CHUNK_MB");
+    const size_t big = chunk_env ? ((size_t)atoll(chunk_env) << 20) / gran * gran : OUT_CHUNK;
+    size_t chunk = big > 0 ? big : OUT_CHUNK, align = chunk;
+    if (want < chunk) {  // one chunk, aligned to its power-of-two size
         chunk = want;
         align = gran;
         while (align < want) align <<= 1;

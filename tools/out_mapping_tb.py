@@ -17,7 +17,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--buffers", type=int, default=5)
     ap.add_argument("--tbs", nargs="+", default=["16", "14", "12"],
-                    help="task widths, or WGPC:TB pairs (QKNIT_OB_WG_PER_CU as well)")
+                    help="task widths, or WGPC:TB pairs (QKNIT_OB_WG_PER_CU as well), optionally /SPREAD "
+                         "(QKNIT_OB_SPREAD), e.g. 16/8")
     ap.add_argument("--steps", type=int, default=3)
     args = ap.parse_args()
     import torch
@@ -43,7 +44,9 @@ def main():
         held.append((out, owner))
         rec = {"buffer": b}
         for spec in args.tbs:
-            wgpc, _, tb = spec.rpartition(":")
+            head, _, spread = spec.partition("/")
+            os.environ["QKNIT_OB_SPREAD"] = spread or "1"
+            wgpc, _, tb = head.rpartition(":")
             os.environ["QKNIT_OB_TB"] = tb
             if wgpc:
                 os.environ["QKNIT_OB_WG_PER_CU"] = wgpc
@@ -60,6 +63,7 @@ def main():
             ms = [a.elapsed_time(b_) for a, b_ in ts[1:]]
             rec[spec] = round(sum(ms) / len(ms), 3)
         os.environ.pop("QKNIT_OB_TB", None)
+        os.environ.pop("QKNIT_OB_SPREAD", None)
         print(json.dumps(rec), flush=True)
 
 

@@ -69,8 +69,11 @@ def main():
                 torch.cuda.synchronize()
                 ms = [a.elapsed_time(b) for a, b in ts[2:]]
                 avg = sum(ms) / len(ms)
+                q = len(ms) // 4 or 1
+                trend = [round(sum(ms[i:i + q]) / len(ms[i:i + q]), 4) for i in range(0, len(ms), q)][:4]
                 print(json.dumps({"streams": streams, "world": P, "where": where, "wg_per_cu": os.environ.get("QKNIT_OB_WG_PER_CU", "64"), "write_ms": round(avg, 4),
-                                  "GBs": round(8 * n_out / avg / 1e6, 1), "min_ms": round(min(ms), 4)}), flush=True)
+                                  "GBs": round(8 * n_out / avg / 1e6, 1), "min_ms": round(min(ms), 4),
+                                  "quarters_ms": trend}), flush=True)
                 del out, owner
         ctx.bind_stream()
 
