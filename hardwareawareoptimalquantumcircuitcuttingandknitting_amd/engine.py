@@ -201,7 +201,9 @@ OUT_MAPPED_MIN_BYTES = int(os.environ.get("QKNIT_OUT_MAPPED_MIN_BYTES", str(1 <<
 # (so its memory cannot come straight back), up to OUT_TRIES, the fastest kept and the others freed.
 # Extra tries only with free memory for them (2 GiB spare): a 2^32 output holds at most OUT_TRIES x
 # 34 GB for the few milliseconds of the selection.
-OUT_SELECT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_SELECT_MIN_BYTES", str(16 << 30)))
+# (only full 2^32 outputs: a rank's slice of it writes at 5.7-6.9 TB/s into every buffer, by its size,
+# tools/slice_write_bench.py, so the threshold would reject good buffers there)
+OUT_SELECT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_SELECT_MIN_BYTES", str(24 << 30)))
 OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "6850"))
 OUT_TRIES = int(os.environ.get("QKNIT_OUT_TRIES", "3"))
 out_selections: list = []  # per selected output: the candidates' write rates (GB/s), the kept one first
