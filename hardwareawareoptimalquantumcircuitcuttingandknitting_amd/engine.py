@@ -230,7 +230,10 @@ def out_buffer(ctx: Context, n: int):
             free, _ = T.cuda.mem_get_info(ctx.device)
             if free < 8 * n + (2 << 30):
                 break
-            cand = MappedOut(ctx, n)
+            try:  # memory taken meanwhile (another thread / process): keep the best so far
+                cand = MappedOut(ctx, n)
+            except _lib.QknitError:
+                break
             tried.append((_out_rate(ctx, cand), cand))
         best = max(range(len(tried)), key=lambda i: tried[i][0])
         owner = tried[best][1]
