@@ -95,6 +95,7 @@ SIGNATURES = {
                                 c_i64, c_vp, c_i64, c_vp, c_vp, ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp,
                                 c_i64]),
     "qk_probe_accept": (c_i32, [c_vp, c_vp, ctypes.c_int, c_vp, ctypes.c_double, ctypes.c_double, c_vp, c_vp]),
+    "qk_rank_tally": (c_i32, [c_vp, c_vp, c_vp, c_vp]),
     "qk_knit_workspace_bytes": (c_i32, [ctypes.POINTER(QkKnitPlan), ctypes.POINTER(c_i64)]),
     "qk_knit": (c_i32, [c_vp, ctypes.POINTER(QkKnitPlan), c_vp, c_vp, c_i64, c_vp]),
     "qk_khatri_rao": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),

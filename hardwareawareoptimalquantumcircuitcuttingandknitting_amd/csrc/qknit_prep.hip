@@ -778,6 +778,31 @@ int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx,
     return QK_OK;
 }
 
+// Per-step statistics of the device data rank kept on the device (qk_rank_tally): acc[0] += (r == 0)
+// (no factorisation of rank <= rmax), acc[1] += (r > 0 && k == 0) (probe check rejected), acc[2] = k
+// (the last accepted rank), acc[3] += 1 (steps). The host reads acc only when asked
+// (KnitPipeline.sync_stats), so a loop of steps never waits for the device.
+__global__ __launch_bounds__(64) void qk_rank_tally_kernel(const int32_t* __restrict__ r, const int32_t* __restrict__ k,
+                                                          int64_t* __restrict__ acc) {
+    if (threadIdx.x == 0) {
+        const int rv = *r, kv = *k;
+        acc[0] += rv == 0 ? 1 : 0;
+        acc[1] += (rv > 0 && kv == 0) ? 1 : 0;
+        acc[2] = kv;
+        acc[3] += 1;
+    }
+}
+
+int qk_rank_tally(qk_ctx* ctx, const int32_t* r_dev, const int32_t* k_dev, int64_t* acc) {
+    if (!ctx) return QK_EARG;
+    if (!r_dev || !k_dev || !acc) return fail(ctx, QK_EARG, "qk_rank_tally: null buffer");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_rank_tally: hipSetDevice");
+    hipLaunchKernelGGL(qk_rank_tally_kernel, dim3(1), dim3(64), 0, ctx->stream, r_dev, k_dev, acc);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_rank_tally: ") + hipGetErrorString(e)).c_str());
+    return QK_OK;
+}
+
 int qk_probe_accept(qk_ctx* ctx, const double* e2, int n, const int32_t* r_dev, double tol, double rel_tol,
                     int32_t* k_out, double* err_out) {
     if (!ctx) return QK_EARG;

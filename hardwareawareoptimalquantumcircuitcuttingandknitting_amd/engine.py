@@ -17,6 +17,7 @@ Pipeline of one virtual-circuit run (``run.py:23-71`` in the reference):
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import dataclasses
 import hashlib
@@ -49,6 +50,19 @@ def _ptr(t) -> int | None:
 
 
 # ----------------------------------------------------------------------------- context
+# set at interpreter exit (atexit): finalizers that would call into the HIP runtime (unmapping outputs,
+# destroying contexts) then leave it to the process exit — a mapping or context still alive in a
+# reference cycle the final collection breaks crashed the process there (rank_sim --host-profile)
+_OUT_EXITING = [False]
+
+
+def _out_exiting():
+    _OUT_EXITING[0] = True
+
+
+atexit.register(_out_exiting)
+
+
 class Context:
     """One ``qk_ctx`` per (thread, device); ops run on torch's current stream."""
 
@@ -77,6 +91,8 @@ class Context:
             self.handle = None
 
     def __del__(self):
+        if _OUT_EXITING[0]:  # interpreter exit: the HIP runtime may be gone; the process frees it
+            return
         try:
             self.close()
         except Exception:
@@ -183,12 +199,15 @@ class MappedOut:
         return any(w() is not None for w in self._leases)
 
     def __del__(self):
-        if getattr(self, "ptr", None):
+        # at interpreter exit (after atexit: _OUT_EXITING) the HIP runtime may already be torn down — a
+        # mapping still alive then (e.g. held by a reference cycle the final collection breaks) is left to
+        # the process exit; unmapping it there crashed the process (rank_sim --host-profile)
+        if getattr(self, "ptr", None) and not _OUT_EXITING[0]:
             try:
                 self.lib.qk_out_free(None, ctypes.c_void_p(self.ptr))
             except Exception:
                 pass
-            self.ptr = None
+        self.ptr = None
 
 
 OUT_MAPPED_MIN_BYTES = int(os.environ.get("QKNIT_OUT_MAPPED_MIN_BYTES", str(1 << 30)))  # below: torch allocation

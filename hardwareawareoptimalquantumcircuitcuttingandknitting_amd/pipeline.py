@@ -341,6 +341,11 @@ class HipBackend:
     def probe_accept(self, e2, r, tol, rel_tol=0.0):
         return engine.probe_accept(self.ctx, e2, r, tol, rel_tol)
 
+    def rank_tally(self, r, k, acc):
+        """acc[0] += (r == 0), acc[1] += (r > 0 and k == 0), acc[2] = k, acc[3] += 1 on the device."""
+        self.ctx.check(self.ctx.lib.qk_rank_tally(self.ctx.handle, r.data_ptr(), k.data_ptr(), acc.data_ptr()),
+                       "qk_rank_tally")
+
     def compress(self, TA, XA, TB, XB):
         return engine.compress_operands(self.ctx, TA, XA, TB, XB)
 
@@ -432,7 +437,9 @@ class KnitPipeline:
         # no host round trip before the write (single mode: none at all)
         self.dev_rank = bool(self.data_rank and cA is not None and self.ops.num_terms <= 64
                              and hasattr(self.be, "rank_factors"))
-        self._pending = []  # device (rank, accepted) of steps not yet read back
+        self._pending = 0  # device-rank steps whose statistics are not yet read back (sync_stats)
+        self._tally = None  # device int64[4]: incompressible, rejected, last accepted rank, steps (_note_rank)
+        self._tally_read = np.zeros(4, dtype=np.int64)
         # slice mode, fused preparation: every rank factors the same all-reduced Grams with the same
         # deterministic kernel, so no broadcast of the factors; each rank checks the rows of R in its
         # A column block against every probe, and a MIN all-reduce of the accepted ranks gives one
@@ -857,7 +864,7 @@ class KnitPipeline:
         self.last_prep = "fused"
         return mats, G, U
 
-    def _accept(self, A, B, A2, B2, x, r, ref_rows=None, cmp_rows=None, reduce_err=None):
+    def _accept(self, A, B, A2, B2, x, r, ref_rows=None, cmp_rows=None, reduce_err=None, note=True):
         """Device-side probe check of a compressed knit: ``(k_eff, err)``, ``k_eff`` = the rank when
         every probe's ``||(A^T B - A2^T B2) x||_2 <= rank_tol`` (see ``__init__``), else 0."""
         T = self.T
@@ -871,7 +878,8 @@ class KnitPipeline:
         err = e2[:n].max().sqrt()
         bound = T.clamp(self.rank_tol_rel * e2[n:].max().sqrt(), min=self.rank_tol)
         k_eff = T.where((err <= bound) & (r > 0), r, T.zeros_like(r))
-        self._pending.append((r, k_eff))
+        if note:
+            self._note_rank(r, k_eff)
         return k_eff, err
 
     def _prep_dev_rank(self, qs) -> dict:
@@ -888,7 +896,7 @@ class KnitPipeline:
             A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib])
             _, k_eff, _ = self.be.probe_errors(mats[ia], A2, U, B2, x, r=r, tol=self.rank_tol,
                                                rel_tol=self.rank_tol_rel)
-            self._pending.append((r, k_eff))
+            self._note_rank(r, k_eff)
             return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
         mats = self.operands(qs)
         self.last_prep = "torch"
@@ -982,16 +990,16 @@ class KnitPipeline:
             # this rank's A columns (its rows of R) against all probes (B2 / probes: every column)
             e2, _, _ = be.probe_errors(XA, A2, U, B2, x_full.contiguous(), a2_cols=(self.rank * bwA, bwA))
             k_eff, _ = be.probe_accept(e2, r, self.rank_tol, self.rank_tol_rel)
-            self._pending.append((r, k_eff))
         else:
             # rows of R in this rank's A column block, against all probes
             ref_rows = XA.T @ Bx
             cmp_rows = A2[:, self.rank * bwA:(self.rank + 1) * bwA].T @ _mm_nt(B2, x_full)
-            k_eff, _ = self._accept(None, None, None, None, None, r, ref_rows, cmp_rows)
+            k_eff, _ = self._accept(None, None, None, None, None, r, ref_rows, cmp_rows, note=False)
         # one decision for every rank: the accepted rank only if every rank's rows of R passed (the A
         # column blocks cover all of R; the ranks' factors are identical, so the local ranks are r or 0).
         # A rejection anywhere makes every rank take the exact slice, whose collectives then match.
         dist.all_reduce(k_eff, op=dist.ReduceOp.MIN, group=self.group)
+        self._note_rank(r, k_eff)  # the decision every rank takes
         if self.slice_exact == "host":
             # round-3 form: the host reads the (MIN-reduced) verdict after queueing the write and
             # gathers the exact slice's operands only on a rejection (no per-step gather)
@@ -1214,17 +1222,35 @@ class KnitPipeline:
         self.last_kernel = None
         return self.be.gemm_keyed(A, B, keyA=kA, keyB=kB, out=self.out)
 
+    def _note_rank(self, r, k_eff):
+        """A device-rank step's verdict into the device-side tally (no host read: the loop of steps never
+        waits for the device; round 4 read every 32 steps back, which drained the pipelined multi-GPU
+        queue each time). In slice mode k_eff is MIN-all-reduced in place afterwards, so the tally is
+        queued there after that reduction (_prep_slice)."""
+        T = self.T
+        if self._tally is None or self._tally.device != k_eff.device:
+            self._tally = T.zeros(4, dtype=T.int64, device=k_eff.device)
+        tally = getattr(self.be, "rank_tally", None)
+        if tally is not None:
+            tally(r, k_eff, self._tally)
+        else:  # host backends (CPU tests): the same counts with torch
+            rv, kv = int(r.reshape(-1)[0]), int(k_eff.reshape(-1)[0])
+            self._tally += T.tensor([int(rv == 0), int(rv > 0 and kv == 0), 0, 1], dtype=T.int64)
+            self._tally[2] = kv
+        self._pending += 1
+
     def sync_stats(self):
-        """Read back the ranks / acceptances of the steps since the last call (host sync):
-        ``last_rank`` (accepted rank, or None when the last step fell back) and ``rank_fallbacks``."""
-        for r, k in self._pending:
-            rv, kv = int(r.reshape(-1)[0]), int(k.reshape(-1)[0])
-            self.last_rank = kv if kv > 0 else None
-            if rv == 0:  # no factorisation of rank <= 8: exact contraction, not a rejected check
-                self.rank_incompressible += 1
-            elif kv == 0:
-                self.rank_fallbacks += 1
-        self._pending = []
+        """Read back the device tally of the steps since the last call (host sync): ``last_rank``
+        (accepted rank, or None when the last step fell back), ``rank_fallbacks`` (probe check rejected),
+        ``rank_incompressible`` (no factorisation of rank <= 8: the exact contraction)."""
+        if self._pending and self._tally is not None:
+            acc = self._tally.cpu().numpy()
+            d = acc - self._tally_read
+            self.rank_incompressible += int(d[0])
+            self.rank_fallbacks += int(d[1])
+            self.last_rank = int(acc[2]) if acc[2] > 0 else None
+            self._tally_read = acc
+        self._pending = 0
         return self.last_rank, self.rank_fallbacks
 
     def _rank_compress(self, mats):
@@ -1467,14 +1493,11 @@ class KnitPipeline:
         finally:
             self.out = keep
 
-    PENDING_MAX = 32  # device-rank steps whose (rank, accepted) tensors are kept before a read-back
 
     def step(self):
         bind = getattr(self.be, "bind", None)
         if bind is not None:  # the caller may have switched torch's current stream since the last step
             bind()
-        if len(self._pending) >= self.PENDING_MAX:
-            self.sync_stats()  # bounded: one host read every PENDING_MAX steps of a long loop
         if self.overlap and self.overlap_ok():
             return self._step_overlapped()
         if not self.record_events:

@@ -360,6 +360,10 @@ int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx,
                     double* err_out, double* work, int64_t work_bytes);
 int qk_probe_accept(qk_ctx* ctx, const double* e2, int n, const int32_t* r_dev, double tol, double rel_tol,
                     int32_t* k_out, double* err_out);
+/* Device-side statistics of a step's data rank (r: factorisation rank, k: accepted rank, both DEVICE
+ * int32): acc[0] += (r == 0), acc[1] += (r > 0 && k == 0), acc[2] = k, acc[3] += 1 (acc: DEVICE int64[4]),
+ * so steps in a loop never read their verdicts back; the host reads acc when it needs the counts. */
+int qk_rank_tally(qk_ctx* ctx, const int32_t* r_dev, const int32_t* k_dev, int64_t* acc);
 
 /* ---- post-processing (reference-shaped results; quasi_distr.py:3-43, run.py:71) ---------- */
 

@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--xgmi-gbs", type=float, default=0.0, help="modelled per-link xGMI GB/s (0: no delay)")
     ap.add_argument("--coll-lat-us", type=float, default=20.0, help="modelled latency per collective")
     ap.add_argument("--overlap", action="store_true", help="pipelined steps (CU-masked prep stream)")
+    ap.add_argument("--cprofile", action="store_true", help="cProfile the timed steps (top host functions to stderr)")
+    ap.add_argument("--host-profile", action="store_true",
+                    help="host time per pipeline phase (sweep / preparation / launch), to find blocking calls")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -145,19 +148,50 @@ def main():
         if args.overlap:
             torch.cuda.set_stream(torch.cuda.Stream())
             pipe.overlap = pipe.overlap_ok()
+        host_phase = {}
+        if args.host_profile:
+            import functools
+
+            for name in ("sweep", "_prep_slice", "_launch_slice", "_slice_exact_operands", "_prep_fused",
+                         "_exchange", "_fold"):
+                fn = getattr(pipe, name)
+
+                @functools.wraps(fn)
+                def timed(*a, _fn=fn, _name=name, **kw):
+                    h = time.perf_counter()
+                    try:
+                        return _fn(*a, **kw)
+                    finally:
+                        host_phase[_name] = host_phase.get(_name, 0.0) + time.perf_counter() - h
+
+                setattr(pipe, name, timed)
         for _ in range(args.warmup):
             pipe.step()
         torch.cuda.synchronize()
         recv.clear()
         model.clear()
+        host_phase.clear()
         pipe.record_events = True
         t0 = time.perf_counter()
         host = 0.0
+        prof = None
+        if args.cprofile:
+            import cProfile
+
+            prof = cProfile.Profile()
+            prof.enable()
         for _ in range(args.steps):
             h0 = time.perf_counter()
             pipe.step()
             host += time.perf_counter() - h0
+        if prof is not None:
+            import pstats
+
+            prof.disable()
+            pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(60)
+        t_loop = time.perf_counter()
         torch.cuda.synchronize()
+        drain = time.perf_counter() - t_loop  # how far the host got ahead of the device
         ms = (time.perf_counter() - t0) / args.steps * 1e3
         pipe.sync_stats()
         knit = sum(s.elapsed_time(e) for s, e in pipe.events) / len(pipe.events)
@@ -165,14 +199,16 @@ def main():
         prep = sum(s.elapsed_time(e) for s, e in pipe.prep_events) / max(len(pipe.prep_events), 1)
         M, N, K = pipe.gemm_shape()
         print(json.dumps({"workload": args.workload, "mode": pipe.mode, "world": world, "rank": args.rank,
-                          "slice": list(pipe.slice), "ms_per_step_no_xgmi": round(ms, 3), "host_ms_per_step": round(host / args.steps * 1e3, 3),
+                          "slice": list(pipe.slice), "ms_per_step_no_xgmi": round(ms, 3), "host_ms_per_step": round(host / args.steps * 1e3, 3), "drain_ms": round(drain * 1e3, 3),
                           "sweep_ms": round(sweep, 3), "prep_ms": round(prep, 3), "knit_ms": round(knit, 3),
                           "knit_GBs": round(8 * M * N / (knit * 1e-3) / 1e9, 1), "accepted_rank": pipe.last_rank,
                           "received_bytes_per_step": {k: v // args.steps for k, v in recv.items()},
                           "xgmi_model": ({"per_link_GBs": args.xgmi_gbs, "latency_us": args.coll_lat_us,
                                           "us_per_step": {k: round(v / args.steps, 1) for k, v in model.items()}}
                                          if args.xgmi_gbs > 0 else None),
-                          "overlap": bool(pipe.overlap), "cus": pipe.overlap_cus}), flush=True)
+                          "overlap": bool(pipe.overlap), "cus": pipe.overlap_cus,
+                          "host_phase_ms": {k: round(v / args.steps * 1e3, 3) for k, v in host_phase.items()}}),
+              flush=True)
         del pipe
         torch.cuda.empty_cache()
 

@@ -3,8 +3,8 @@
 
   python tools/step_timeline.py run_kernel_trace.csv [--steps N]
 
-Takes the last N (default 5) occurrences of the write kernel (qk_knit_outer_*) as step markers and
-prints, for the last complete step interval, every kernel that started in it: its stream, start
+Takes the write kernel launches (qk_knit_outer_*) as step markers and prints, for the step
+interval in the middle of the run, every kernel that started in it: its stream, start
 offset from the interval start, duration, and the gaps on each stream (time no kernel of that
 stream ran). Used for the 8-rank rank_sim step."""
 import csv
@@ -20,7 +20,8 @@ def main():
     writes = [k for k in ks if "qk_knit_outer" in k[2]]
     if len(writes) < 3:
         sys.exit("fewer than 3 write kernels in the trace")
-    t0, t1 = writes[-3][0], writes[-2][0]
+    mid = len(writes) // 2  # a step in the middle of the run (the last ones have no next preparation)
+    t0, t1 = writes[mid][0], writes[mid + 1][0]
     print(f"step interval {(t1 - t0) / 1e3:.1f} us (write start to write start)")
     busy = defaultdict(float)
     for s, e, name, st, q in ks:
