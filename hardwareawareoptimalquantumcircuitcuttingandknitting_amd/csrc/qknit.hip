@@ -1426,6 +1426,7 @@ struct OuterRowsArgs {
     int64_t o_begin;
     const int32_t* kdev;
     double* __restrict__ out;
+    int64_t spread;  // piece order: the i-th piece taken is (i % spread) * (n / spread) + i / spread
 };
 
 template <int KR, int C>
@@ -1439,7 +1440,9 @@ __global__ __launch_bounds__(256) void qk_knit_outer_rows_kernel(OuterRowsArgs a
     }
     d2_t b[KR][NP];
     int64_t pb_loaded = -1;
-    for (int64_t p = a.piece_begin + blockIdx.x; p < a.piece_end; p += gridDim.x) {
+    const int64_t n_pieces = a.piece_end - a.piece_begin, per_part = n_pieces / a.spread;
+    for (int64_t i = blockIdx.x; i < n_pieces; i += gridDim.x) {
+        const int64_t p = a.piece_begin + (i % a.spread) * per_part + i / a.spread;
         const uint32_t pl = (uint32_t)p;
         const int64_t pb = pext32(pl, a.maskB_hi);
         const uint32_t pa = pext32(pl, a.maskA_hi);
@@ -1848,8 +1851,14 @@ int qk_knit_outer_stream_range(qk_ctx* ctx, int nbits, int64_t K, const double* 
         int64_t G = (int64_t)cus * per_cu;
         if (G >= nb) G -= G % nb;
         if (G > pieces) G = pieces;
+        // piece order as the blocked kernel's task order (8 far-apart parts at once); a workgroup keeps
+        // its B run when the grid is a multiple of 8 x the run count (then i % 8 and the run of i / 8 are
+        // the same for all of its pieces). QKNIT_OR_SPREAD (A/B, read per launch) sets the part count.
+        const char* rs_env = getenv("QKNIT_OR_SPREAD");
+        int64_t spread = rs_env ? atoll(rs_env) : 8;
+        if (spread < 1 || pieces % spread || G % (spread * nb) || pieces < 4 * G) spread = 1;
         OuterRowsArgs r{(int)K, A, lda, B, ldb, (uint32_t)(maskA >> rc), (uint32_t)(maskB >> rc), o_begin >> rc,
-                        (o_begin >> rc) + pieces, o_begin, k_dev, out};
+                        (o_begin >> rc) + pieces, o_begin, k_dev, out, spread};
         const dim3 grid((unsigned)(G < 1 ? 1 : G));
         if (K <= 1) {
             hipLaunchKernelGGL((qk_knit_outer_rows_kernel<1, 13>), grid, dim3(256), 0, ctx->stream, r);

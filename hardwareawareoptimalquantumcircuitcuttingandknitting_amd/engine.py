@@ -91,7 +91,7 @@ class Context:
             self.handle = None
 
     def __del__(self):
-        if _OUT_EXITING[0]:  # interpreter exit: the HIP runtime may be gone; the process frees it
+        if _OUT_EXITING is None or _OUT_EXITING[0]:  # interpreter exit (module globals cleared too)
             return
         try:
             self.close()
@@ -202,7 +202,7 @@ class MappedOut:
         # at interpreter exit (after atexit: _OUT_EXITING) the HIP runtime may already be torn down — a
         # mapping still alive then (e.g. held by a reference cycle the final collection breaks) is left to
         # the process exit; unmapping it there crashed the process (rank_sim --host-profile)
-        if getattr(self, "ptr", None) and not _OUT_EXITING[0]:
+        if getattr(self, "ptr", None) and _OUT_EXITING is not None and not _OUT_EXITING[0]:
             try:
                 self.lib.qk_out_free(None, ctypes.c_void_p(self.ptr))
             except Exception:
