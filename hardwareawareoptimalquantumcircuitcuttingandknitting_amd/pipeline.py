@@ -988,8 +988,9 @@ class KnitPipeline:
         B2 = gat[:, R8 * bwA:].view(P, R8, bwB).permute(1, 0, 2).reshape(R8, P * bwB).contiguous()
         if self._fused_prep(qs):
             # this rank's A columns (its rows of R) against all probes (B2 / probes: every column)
-            e2, _, _ = be.probe_errors(XA, A2, U, B2, x_full.contiguous(), a2_cols=(self.rank * bwA, bwA))
-            k_eff, _ = be.probe_accept(e2, r, self.rank_tol, self.rank_tol_rel)
+            # (the accepted rank from the same launch chain: no separate accept kernel)
+            _, k_eff, _ = be.probe_errors(XA, A2, U, B2, x_full.contiguous(), r=r, tol=self.rank_tol,
+                                          a2_cols=(self.rank * bwA, bwA), rel_tol=self.rank_tol_rel)
         else:
             # rows of R in this rank's A column block, against all probes
             ref_rows = XA.T @ Bx
