@@ -226,6 +226,7 @@ OUT_SELECT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_SELECT_MIN_BYTES", str(24 <
 OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "6850"))
 OUT_TRIES = int(os.environ.get("QKNIT_OUT_TRIES", "3"))
 out_selections: list = []  # per selected output: the candidates' write rates (GB/s), the kept one first
+_out_select_lock = threading.Lock()  # one selection at a time per process: two threads' candidates never stack
 
 
 def _out_rate(ctx: Context, owner) -> float:
@@ -242,8 +243,11 @@ def out_buffer(ctx: Context, n: int):
     T = torch()
     if 8 * n < OUT_MAPPED_MIN_BYTES:
         return T.empty(n, dtype=T.float64, device=T.device("cuda", ctx.device)), None
-    owner = MappedOut(ctx, n)
-    if 8 * n >= OUT_SELECT_MIN_BYTES and OUT_TRIES > 1:
+    if 8 * n < OUT_SELECT_MIN_BYTES or OUT_TRIES <= 1:
+        owner = MappedOut(ctx, n)
+        return owner.tensor(), owner
+    with _out_select_lock:
+        owner = MappedOut(ctx, n)
         tried = [(_out_rate(ctx, owner), owner)]
         while tried[-1][0] < OUT_FAST_GBS and len(tried) < OUT_TRIES:
             free, _ = T.cuda.mem_get_info(ctx.device)
@@ -257,7 +261,8 @@ def out_buffer(ctx: Context, n: int):
         best = max(range(len(tried)), key=lambda i: tried[i][0])
         owner = tried[best][1]
         out_selections.append([round(tried[best][0], 1)] + [round(r, 1) for i, (r, _) in enumerate(tried) if i != best])
-        del tried  # the others are unmapped here
+        del tried  # the others are unmapped here (cand: the last candidate's name)
+        cand = None
     return owner.tensor(), owner
 
 
