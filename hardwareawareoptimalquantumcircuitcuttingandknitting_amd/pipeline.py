@@ -1077,8 +1077,14 @@ class KnitPipeline:
                 self._write_stream = engine.cu_masked_stream(dev, write)
                 self.overlap_cus = (len(prep), len(write))
             else:
-                self._prep_stream = T.cuda.Stream(device=self.be.dev)
-                self._write_stream = None
+                # QKNIT_OVERLAP_PRIO: HSA queue priorities instead of a CU split. "write": the write
+                # stream high, the preparation normal (the dispatcher serves the preparation's
+                # workgroups only where the write's queue has none left: its tail); "prep": the
+                # preparation high (its few workgroups go first, the write keeps every CU)
+                prio = os.environ.get("QKNIT_OVERLAP_PRIO", "")
+                hi = min(T.cuda.Stream.priority_range()) if prio else 0
+                self._prep_stream = T.cuda.Stream(device=self.be.dev, priority=hi if prio == "prep" else 0)
+                self._write_stream = T.cuda.Stream(device=self.be.dev, priority=hi) if prio == "write" else None
                 self.overlap_cus = (0, total)
             self._prep_stream.wait_stream(T.cuda.current_stream())  # plan uploads before the first step
         return self._prep_stream, self._write_stream

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--prep-cus", type=int, nargs="*", default=[32, 48, 64, 0])
     ap.add_argument("--layouts", nargs="*", default=["block"])
+    ap.add_argument("--prio", nargs="*", default=[""], help="QKNIT_OVERLAP_PRIO values for --prep-cus 0 ('', write, prep)")
     ap.add_argument("--no-final-plain", action="store_true", help="end with the pipelined runs (timelines)")
     args = ap.parse_args()
     import torch
@@ -75,7 +76,10 @@ def main():
     ref = pipe.out.clone()
     run(5, timed=True)
     print(json.dumps({"setting": "plain", "ms_per_step": plain, **stats()}), flush=True)
-    for c, lay in [(c, lay) for c in args.prep_cus for lay in (args.layouts if c else ["-"])]:
+    settings = [(c, lay, pr) for c in args.prep_cus for lay in (args.layouts if c else ["-"])
+                for pr in (args.prio if c == 0 else [""])]
+    for c, lay, pr in settings:
+        os.environ["QKNIT_OVERLAP_PRIO"] = pr
         os.environ["QKNIT_PREP_CUS"] = str(c)
         os.environ["QKNIT_PREP_CU_LAYOUT"] = lay
         pipe._prep_stream = pipe._write_stream = None
@@ -87,7 +91,7 @@ def main():
         diff = float((pipe.out - ref).abs().max())
         run(5, timed=True)
         pipe.sync_stats()
-        print(json.dumps({"setting": "pipelined", "prep_cus": c, "layout": lay, "cus": pipe.overlap_cus, "ms_per_step": ms,
+        print(json.dumps({"setting": "pipelined", "prep_cus": c, "layout": lay, "prio": pr, "cus": pipe.overlap_cus, "ms_per_step": ms,
                           "max_abs_diff_vs_plain": diff, "rank_fallbacks": pipe.rank_fallbacks, "host_ms": host_ms, **stats()}),
               flush=True)
     if not args.no_final_plain:
