@@ -463,6 +463,10 @@ class KnitPipeline:
         # so the side stream's sweep waits for it), 6.55 with a one-workgroup-per-task write grid,
         # 6.06 with 4 write workgroups per CU. QKNIT_OVERLAP=1 turns it on.
         self.overlap = os.environ.get("QKNIT_OVERLAP", "0") == "1"
+        # speculative write (single-GPU device data rank): the probe check runs beside the write instead
+        # of before it (QKNIT_SPEC_WRITE=1)
+        self.spec_write = os.environ.get("QKNIT_SPEC_WRITE", "0") == "1"
+        self._spec_stream = None
         self.events = []  # (start, end) events around the main contraction GEMM
         self.sweep_events = []  # (start, end) events around each step's sweep (all fragments)
         self.prep_events = []  # (sweep end, knit start): operand transforms + data-rank compression
@@ -894,6 +898,25 @@ class KnitPipeline:
             mats, G, U = self._prep_fused(qs, x)
             TA, TB, r = self.be.rank_factors(G[0], G[1])
             A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib])
+            if self.spec_write and getattr(self.be, "dev", None) is not None and self.be.dev.type == "cuda":
+                # speculative write: the write runs at the factored rank r while the probe check runs
+                # beside it on a side stream; the exact contraction after both is predicated on the
+                # check (k = 0) and overwrites every output, as when the write was skipped
+                T = self.T
+                main = T.cuda.current_stream()
+                if self._spec_stream is None:
+                    self._spec_stream = T.cuda.Stream(device=self.be.dev)
+                S2 = self._spec_stream
+                S2.wait_stream(main)
+                with T.cuda.stream(S2):
+                    self.be.bind()
+                    _, k_eff, _ = self.be.probe_errors(mats[ia], A2, U, B2, x, r=r, tol=self.rank_tol,
+                                                       rel_tol=self.rank_tol_rel)
+                    self._note_rank(r, k_eff)
+                self.be.bind()
+                for t in (mats[ia], A2, U, B2, x, r, k_eff):
+                    t.record_stream(S2)
+                return {"A2": A2, "B2": B2, "k_eff": k_eff, "k_write": r, "check": S2, "mats": mats}
             _, k_eff, _ = self.be.probe_errors(mats[ia], A2, U, B2, x, r=r, tol=self.rank_tol,
                                                rel_tol=self.rank_tol_rel)
             self._note_rank(r, k_eff)
@@ -919,10 +942,12 @@ class KnitPipeline:
             start, end = self.be.event(), self.be.event()
             start.record()
         self.last_kernel = self._kernel_name(p["A2"].shape[0], cA, cB)
-        self.be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, self.out, k_dev=p["k_eff"])
+        self.be.knit_outer_stream(p["A2"], p["B2"], cA, cB, self.N, self.out, k_dev=p.get("k_write", p["k_eff"]))
         if self.record_events:
             end.record()
             self.events.append((start, end))
+        if "check" in p:  # speculative write: the exact path waits for the probe check
+            self.T.cuda.current_stream().wait_stream(p["check"])
         return self._contract(p["mats"], skip=p["k_eff"])  # exact path: runs only if the check rejected
 
     def _prep_slice(self, qs) -> dict:
