@@ -655,7 +655,7 @@ def test_gemm_outer_paired_matches_torch(T, K, odd_rows):
     assert float((got - ref).abs().max()) <= 1e-12 * K
 
 
-@pytest.mark.parametrize("case", ["cx_3cuts", "move_gate", "syc_16"])
+@pytest.mark.parametrize("case", ["cx_6x6_3cuts", "cx_8x8_2cuts", "syc_16"])
 @pytest.mark.parametrize("reject", [False, True])
 def test_speculative_write_matches_oracle(T, case, reject):
     """Speculative write (QKNIT_SPEC_WRITE): the write runs at the factored rank while the probe check
@@ -663,8 +663,8 @@ def test_speculative_write_matches_oracle(T, case, reject):
     above 8) still ends in the exact contraction over every output. Equal to the oracle (1e-12)."""
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
 
-    cut = {"cx_3cuts": lambda: circuits.two_fragment("cx", 3, 3, n_cuts=3)[1],
-           "move_gate": lambda: circuits.wire_cut(3, 2, extra_gate_cut=True)[1],
+    cut = {"cx_6x6_3cuts": lambda: circuits.two_fragment("cx", 6, 6, n_cuts=3)[1],
+           "cx_8x8_2cuts": lambda: circuits.two_fragment("cx", 8, 8, n_cuts=2)[1],
            "syc_16": lambda: circuits.two_fragment("cx", 8, 8, n_cuts=4)[1]}[case]()
     pipe = KnitPipeline(VirtualCircuit(cut), factored=True, data_rank=True)
     pipe.spec_write = True
