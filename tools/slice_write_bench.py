@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--where", nargs="+", default=["last"],
                     help="last: the last slice into its own mapping; first: the first slice; "
                          "inbig: the first slice into the first part of a full-size mapping")
+    ap.add_argument("--env-sets", nargs="+", default=[""],
+                    help="A/B settings timed into the same buffer in turn, each 'VAR=v;VAR=v' (read per launch)")
+    ap.add_argument("--rounds", type=int, default=1, help="passes over --env-sets per buffer")
     args = ap.parse_args()
     import torch
 
@@ -58,22 +61,35 @@ def main():
                 else:
                     out, owner = engine.out_buffer(ctx, n_out)
                 o_begin = (P - 1) * n_out if where == "last" else 0
-                ts = []
-                for it in range(args.steps + 2):
-                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    a.record()
-                    engine.knit_outer_stream(ctx, A2, B2, cA, cB, N, out, o_begin=o_begin, o_count=n_out,
-                                             k_dev=k)
-                    b.record()
-                    ts.append((a, b))
-                torch.cuda.synchronize()
-                ms = [a.elapsed_time(b) for a, b in ts[2:]]
-                avg = sum(ms) / len(ms)
-                q = len(ms) // 4 or 1
-                trend = [round(sum(ms[i:i + q]) / len(ms[i:i + q]), 4) for i in range(0, len(ms), q)][:4]
-                print(json.dumps({"streams": streams, "world": P, "where": where, "wg_per_cu": os.environ.get("QKNIT_OB_WG_PER_CU", "64"), "write_ms": round(avg, 4),
-                                  "GBs": round(8 * n_out / avg / 1e6, 1), "min_ms": round(min(ms), 4),
-                                  "quarters_ms": trend}), flush=True)
+                for rnd in range(args.rounds):
+                    for es in args.env_sets:
+                        saved = {}
+                        for kv in filter(None, es.split(";")):
+                            kk, vv = kv.split("=", 1)
+                            saved[kk] = os.environ.get(kk)
+                            os.environ[kk] = vv
+                        ts = []
+                        for it in range(args.steps + 2):
+                            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                            a.record()
+                            engine.knit_outer_stream(ctx, A2, B2, cA, cB, N, out, o_begin=o_begin, o_count=n_out,
+                                                     k_dev=k)
+                            b.record()
+                            ts.append((a, b))
+                        torch.cuda.synchronize()
+                        for kk, vv in saved.items():
+                            if vv is None:
+                                os.environ.pop(kk, None)
+                            else:
+                                os.environ[kk] = vv
+                        ms = [a.elapsed_time(b) for a, b in ts[2:]]
+                        avg = sum(ms) / len(ms)
+                        q = len(ms) // 4 or 1
+                        trend = [round(sum(ms[i:i + q]) / len(ms[i:i + q]), 4) for i in range(0, len(ms), q)][:4]
+                        print(json.dumps({"streams": streams, "world": P, "where": where, "env": es, "round": rnd,
+                                          "wg_per_cu": os.environ.get("QKNIT_OB_WG_PER_CU", "64"), "write_ms": round(avg, 4),
+                                          "GBs": round(8 * n_out / avg / 1e6, 1), "min_ms": round(min(ms), 4),
+                                          "quarters_ms": trend}), flush=True)
                 del out, owner
         ctx.bind_stream()
 

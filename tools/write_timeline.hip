@@ -34,7 +34,15 @@ __global__ __launch_bounds__(256) void write_kernel(const double* __restrict__ A
                                                     double* __restrict__ out, int64_t n_tasks, int64_t spread,
                                                     unsigned long long* __restrict__ stamps, int per_wg) {
     __shared__ double sA[K * NA], sB[K * NB];
+    __shared__ uint32_t tab[2][2][256];  // pext of bytes 0 / 1 of a task offset, per side (as the knit)
     const uint32_t mA = 0xAAAAAAAAu, mB = 0x55555555u, low = (1u << TB) - 1;
+    for (int i = threadIdx.x; i < 512; i += 256) {
+        const int byte = i >> 8, v = i & 255;
+        tab[0][byte][v] = pext32((uint32_t)v << (8 * byte), mA & low);
+        tab[1][byte][v] = pext32((uint32_t)v << (8 * byte), mB & low);
+    }
+    __syncthreads();
+    const uint32_t r0 = tab[0][0][(2 * threadIdx.x) & 255], c0 = tab[1][0][(2 * threadIdx.x) & 255];
     const int64_t per_part = n_tasks / spread;
     int slot = 0;
     for (int64_t i = blockIdx.x; i < n_tasks; i += gridDim.x, ++slot) {
@@ -47,10 +55,10 @@ __global__ __launch_bounds__(256) void write_kernel(const double* __restrict__ A
         for (int j = threadIdx.x; j < K * NB; j += 256) sB[j] = B[(j / NB) * 65536 + bh + j % NB];
         __syncthreads();
         double* o = out + (int64_t)t * (1 << TB);
-        const uint32_t r0 = pext32(2u * threadIdx.x, mA & low), c0 = pext32(2u * threadIdx.x, mB & low);
+#pragma unroll 4
         for (int it = 0; it < (1 << TB) / 512; ++it) {
-            const uint32_t off = 512u * it + 2u * threadIdx.x;
-            const uint32_t row = r0 + pext32(512u * it, mA & low), col = c0 + pext32(512u * it, mB & low);
+            const uint32_t hi = (uint32_t)(2 * it + (threadIdx.x >> 7));
+            const uint32_t row = r0 + tab[0][1][hi], col = c0 + tab[1][1][hi];
             double2 acc = {0.0, 0.0};
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -59,10 +67,9 @@ __global__ __launch_bounds__(256) void write_kernel(const double* __restrict__ A
                 acc.x = fma(av, bv.x, acc.x);
                 acc.y = fma(av, bv.y, acc.y);
             }
-            *reinterpret_cast<double2*>(o + off) = acc;
+            *reinterpret_cast<double2*>(o + 512 * it + 2 * threadIdx.x) = acc;
         }
         if (threadIdx.x == 0 && slot < per_wg) {
-            __threadfence();
             stamps[2 * ((int64_t)blockIdx.x * per_wg + slot)] = t0;
             stamps[2 * ((int64_t)blockIdx.x * per_wg + slot) + 1] = wall_clock64();
         }
