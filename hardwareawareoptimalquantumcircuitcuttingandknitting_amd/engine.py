@@ -121,10 +121,11 @@ def device_cu_count(device: int = 0) -> int:
     return n.value
 
 
-def cu_masked_stream(device: int, cus: tuple):
+def cu_masked_stream(device: int, cus: tuple, tag: int = 0):
     """A torch stream over a HIP stream restricted to the logical CUs ``cus``
-    (``qk_stream_create_cu_masked``), created once per (device, CU set) and kept for the process."""
-    key = (device, tuple(sorted(cus)))
+    (``qk_stream_create_cu_masked``), created once per (device, CU set, tag) and kept for the process
+    (``tag``: another stream over the same CUs)."""
+    key = (device, tuple(sorted(cus)), tag)
     with _modules_lock:
         if key not in _MASKED_STREAMS:
             lib = _lib.lib()

@@ -467,6 +467,13 @@ class KnitPipeline:
         # of before it (QKNIT_SPEC_WRITE=1)
         self.spec_write = os.environ.get("QKNIT_SPEC_WRITE", "0") == "1"
         self._spec_stream = None
+        # pipelined steps: output buffers (QKNIT_OUT_BUFFERS; 2: steps alternate between two buffers and
+        # two write streams, so step i+1's write may start while step i's drains)
+        self.out_buffers = int(os.environ.get("QKNIT_OUT_BUFFERS", "1"))
+        self._outs = None
+        self._wstreams = None
+        self._flip = 0
+        self._write_cus = None
         self.events = []  # (start, end) events around the main contraction GEMM
         self.sweep_events = []  # (start, end) events around each step's sweep (all fragments)
         self.prep_events = []  # (sweep end, knit start): operand transforms + data-rank compression
@@ -1100,6 +1107,7 @@ class KnitPipeline:
                 write = tuple(i for i in range(total) if i not in set(prep))
                 self._prep_stream = engine.cu_masked_stream(dev, prep)
                 self._write_stream = engine.cu_masked_stream(dev, write)
+                self._write_cus = write
                 self.overlap_cus = (len(prep), len(write))
             else:
                 # QKNIT_OVERLAP_PRIO: HSA queue priorities instead of a CU split. "write": the write
@@ -1134,6 +1142,17 @@ class KnitPipeline:
             return self.knit(self.sweep())
         S, W = self._overlap_streams()
         W = W if W is not None else main
+        if self.out_buffers > 1:
+            if self._outs is None:
+                self._outs = [self.out, self._alloc_out(None)]
+                dev = self.be.dev.index or 0
+                self._wstreams = ([W, engine.cu_masked_stream(dev, self._write_cus, tag=1)] if self._write_cus
+                                  else [T.cuda.Stream(device=self.be.dev), T.cuda.Stream(device=self.be.dev)])
+                for w in self._wstreams:
+                    w.wait_stream(main)
+            k = self._flip
+            self._flip ^= 1
+            self.out, W = self._outs[k], self._wstreams[k]
         with T.cuda.stream(S):
             be.bind()
             if self.record_events:

@@ -688,6 +688,36 @@ def test_speculative_write_matches_oracle(T, case, reject):
             assert pipe.rank_fallbacks == 0 and pipe.last_rank is not None
 
 
+@pytest.mark.parametrize("prep_cus", ["96", "0"])
+def test_pipelined_double_buffered_steps_match_oracle(T, prep_cus):
+    """Pipelined steps with two output buffers and two write streams (QKNIT_OUT_BUFFERS=2): the steps
+    alternate buffers, step i+1's write may run beside step i's; every step's returned buffer equals
+    the oracle (1e-12), the two buffers are distinct, and a buffer is reused two steps later."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    cut = circuits.two_fragment("cx", 8, 8, n_cuts=2)[1]
+    ref = dense.run_dense(cut)
+    saved = os.environ.get("QKNIT_PREP_CUS")
+    os.environ["QKNIT_PREP_CUS"] = prep_cus
+    try:
+        with T.cuda.stream(T.cuda.Stream()):
+            pipe = KnitPipeline(VirtualCircuit(cut), factored=True, data_rank=True)
+            assert pipe.overlap_ok()
+            pipe.overlap, pipe.out_buffers = True, 2
+            outs = []
+            for _ in range(5):
+                out = pipe.step()
+                outs.append(out)
+                T.cuda.current_stream().synchronize()
+                np.testing.assert_allclose(out.cpu().numpy(), ref, atol=1e-12, rtol=0)
+            assert outs[1].data_ptr() != outs[2].data_ptr() and outs[1].data_ptr() == outs[3].data_ptr()
+    finally:
+        if saved is None:
+            os.environ.pop("QKNIT_PREP_CUS", None)
+        else:
+            os.environ["QKNIT_PREP_CUS"] = saved
+
+
 @pytest.mark.slow
 def test_syc_32_5_data_rank_step_matches_exact_step(T):
     """The bench step (factored knit, light-cone basis, data-rank compression: the rank-64
