@@ -468,8 +468,12 @@ class KnitPipeline:
         self.spec_write = os.environ.get("QKNIT_SPEC_WRITE", "0") == "1"
         self._spec_stream = None
         # pipelined steps: output buffers (QKNIT_OUT_BUFFERS; 2: steps alternate between two buffers and
-        # two write streams, so step i+1's write may start while step i's drains)
-        self.out_buffers = int(os.environ.get("QKNIT_OUT_BUFFERS", "1"))
+        # two write streams, so step i+1's write may start while step i's drains). Default 2 at 4 ranks
+        # only: rank_sim (modelled xGMI, 20 steps, 4 runs each) 1.56-1.64 vs 1.70-1.80 ms per step at 4
+        # ranks, 2.71 vs 2.67-2.74 at 2, 0.94-1.21 vs 0.90-1.13 at 8; 5.00-5.03 vs 4.97-5.06 pipelined
+        # on one GPU (profiles/r04bq_*)
+        ob = os.environ.get("QKNIT_OUT_BUFFERS", "")
+        self.out_buffers = int(ob) if ob else (2 if world == 4 else 1)
         self._outs = None
         self._wstreams = None
         self._flip = 0

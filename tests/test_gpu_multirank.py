@@ -219,7 +219,7 @@ def _syc_worker(rank, world, port, q, overlap=False):
             pipe.overlap = pipe.overlap_ok()
             assert pipe.overlap
         log("planned")
-        for it in range(2):
+        for it in range(3):  # plain first step, then pipelined (at 4 ranks: both output buffers)
             sl = pipe.step()
             torch.cuda.synchronize()
             log(f"step {it}")
@@ -250,11 +250,11 @@ def _syc_worker(rank, world, port, q, overlap=False):
 
 
 @pytest.mark.timeout(1000)
-@pytest.mark.parametrize("world,overlap", [(2, False), (8, True)])
+@pytest.mark.parametrize("world,overlap", [(2, False), (4, True), (8, True)])
 def test_syc_32_5_slice_mode_equals_single_gpu(world, overlap):
     """The bench workload's multi-GPU path (slice mode, device data rank) at 2 ranks (plain steps) and
-    at 8 ranks with pipelined steps (the multi-GPU bench default, BASELINE config 5: syc 32 5 sharded
-    over 8 GPUs): each rank's 2^32 / world-entry slice equals the same range of the single-GPU step
+    at 4 and 8 ranks with pipelined steps (the multi-GPU bench default, BASELINE config 5: syc 32 5
+    sharded over 8 GPUs; at 4 ranks two output buffers alternate, QKNIT_OUT_BUFFERS): each rank's 2^32 / world-entry slice equals the same range of the single-GPU step
     within 1e-12, the slices sum to 1 and no entry is below -1e-13. The exact-slice fallback is
     predicated on the device (no host sync in the step)."""
     total, err, mn, sl = _run(_syc_worker, world, timeout=900, overlap=overlap)
