@@ -669,6 +669,8 @@ def main():
             "gemm_mnk": [M, Nn, K],
             "output_entries": 1 << pipe.N,
             "parallelism": f"labels x{world} ({pipe.mode})",
+            "slice_prep": pipe.slice_prep,  # slice mode: "replicated" (no collective) or "sharded"
+            "slice_cost_model_ms": pipe.slice_costs,
         },
         "roofline": {
             "kernel": kernel,

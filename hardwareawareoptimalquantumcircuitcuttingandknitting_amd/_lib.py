@@ -120,6 +120,7 @@ SIGNATURES = {
     "qk_knit_select_workspace_bytes": (c_i32, [ctypes.c_int, c_u64, c_u64, ctypes.POINTER(c_i64)]),
     "qk_knit_select": (c_i32, [c_vp, ctypes.c_int, c_i64, c_vp, c_i64, c_vp, c_i64, c_u64, c_u64, ctypes.c_double,
                                c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "qk_select_above": (c_i32, [c_vp, c_i64, c_vp, ctypes.c_double, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "qk_npd_pairs_workspace_bytes": (c_i32, [c_i64, ctypes.POINTER(c_i64)]),
     "qk_npd_pairs": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "qk_sample_cdf": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),

@@ -10,8 +10,9 @@ SRCS = [os.path.join(HERE, "csrc", f) for f in ("qknit.hip", "qknit_post.hip", "
                                                               "qknit_sample.hip", "qknit_rank.hip",
                                                               "qknit_plan.hip", "qknit_prep.hip",
                                                               "qknit_select.hip", "qknit_comm.hip",
-                                                              "qknit_mem.hip", "qknit_trunc.hip")]
-DEPS = SRCS + [os.path.join(HERE, "csrc", h) for h in ("internal.h", "sweep_ops.h")]
+                                                              "qknit_mem.hip", "qknit_trunc.hip",
+                                                              "qknit_prim.hip")]
+DEPS = SRCS + [os.path.join(HERE, "csrc", h) for h in ("internal.h", "sweep_ops.h", "prim.h")]
 HEADER = os.path.join(os.path.dirname(HERE), "include", "qknit.h")
 OUT = os.path.join(HERE, "libqknit.so")
 ARCH = os.environ.get("QKNIT_ARCH", "gfx950")

@@ -16,4 +16,10 @@ struct qk_ctx {
     std::string err;     // last error message (qk_last_error)
 };
 
+// qknit_select.hip: nearest_probability_distribution (quasi_distr.py:28-43) of count (key, value) pairs
+// with keys below 2^key_bits — sort by key, stably by value, prefix sums, the closed-form projection
+size_t npd_pairs_bytes(int64_t count);
+int npd_pairs_bits(qk_ctx* ctx, int64_t count, const int64_t* keys, const double* vals, int key_bits, void* ws,
+                   int64_t ws_bytes, int64_t* out_keys, double* out_vals, int64_t* n_out_dev);
+
 #endif  // QKNIT_INTERNAL_H

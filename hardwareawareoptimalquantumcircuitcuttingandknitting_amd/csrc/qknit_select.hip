@@ -18,12 +18,12 @@
 // qk_npd_pairs then sorts them by key and, stably, by value, so the result does not depend on the
 // append order.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <cstdint>
 #include <cstdio>
 
 #include "internal.h"
+#include "prim.h"
 
 namespace {
 
@@ -229,66 +229,67 @@ int qk_knit_select(qk_ctx* ctx, int nbits, int64_t K, const double* A, int64_t l
     return QK_OK;
 }
 
-int qk_npd_pairs_workspace_bytes(int64_t count, int64_t* bytes) {
-    if (!bytes || count < 0 || count > 0x7fffffff) return QK_EARG;
-    const int c = (int)(count > 0 ? count : 1);
-    size_t s1 = 0, s2 = 0, s3 = 0;
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, s1, (int64_t*)nullptr, (int64_t*)nullptr, (double*)nullptr,
-                                           (double*)nullptr, c) != hipSuccess ||
-        hipcub::DeviceRadixSort::SortPairs(nullptr, s2, (double*)nullptr, (double*)nullptr, (int64_t*)nullptr,
-                                           (int64_t*)nullptr, c) != hipSuccess ||
-        hipcub::DeviceScan::ExclusiveSum(nullptr, s3, (double*)nullptr, (double*)nullptr, c) != hipSuccess)
-        return QK_EHIP;
-    size_t cub = s1 > s2 ? s1 : s2;
-    cub = cub > s3 ? cub : s3;
-    // + keys / vals twice (ping-pong), prefix sums, first-kept index
-    *bytes = (int64_t)(al256(cub) + 4 * al256((size_t)c * 8) + al256((size_t)c * 8) + 256);
-    return QK_OK;
+}  // extern "C"
+
+// nearest_probability_distribution of (key, value) pairs whose keys fit `key_bits` bits (internal.h:
+// qk_npd_pairs and the dense qk_npd share it)
+size_t npd_pairs_bytes(int64_t count) {
+    const size_t c = (size_t)(count > 0 ? count : 1);
+    const size_t prim = qkp::radix_sort_bytes((int64_t)c) > qkp::scan_bytes((int64_t)c) ? qkp::radix_sort_bytes((int64_t)c)
+                                                                                      : qkp::scan_bytes((int64_t)c);
+    // keys / vals sorted by key, then by value; prefix sums; first-kept index; the primitives' scratch
+    return 5 * al256(8 * c) + 256 + al256(prim);
 }
 
-int qk_npd_pairs(qk_ctx* ctx, int64_t count, const int64_t* keys, const double* vals, void* ws, int64_t ws_bytes,
-                 int64_t* out_keys, double* out_vals, int64_t* n_out_dev) {
+int npd_pairs_bits(qk_ctx* ctx, int64_t count, const int64_t* keys, const double* vals, int key_bits, void* ws,
+                   int64_t ws_bytes, int64_t* out_keys, double* out_vals, int64_t* n_out_dev) {
     if (!ctx) return QK_EARG;
-    if (count < 0 || count > 0x7fffffff || !n_out_dev || (count > 0 && (!keys || !vals || !out_keys || !out_vals)))
+    if (count < 0 || count > 0x7fffffff || !n_out_dev || (count > 0 && (!keys || !vals || !out_keys || !out_vals)) ||
+        key_bits < 0 || key_bits > 64)
         return sel_fail(ctx, "qk_npd_pairs: bad argument");
-    int64_t need = 0;
-    if (qk_npd_pairs_workspace_bytes(count, &need) != QK_OK) return sel_fail(ctx, "qk_npd_pairs: workspace query");
-    if (!ws || ws_bytes < need) return sel_fail(ctx, "qk_npd_pairs: workspace too small");
+    if (!ws || ws_bytes < (int64_t)npd_pairs_bytes(count)) return sel_fail(ctx, "qk_npd_pairs: workspace too small");
     QKS_HIP(ctx, hipSetDevice(ctx->device));
     if (count == 0) {
         QKS_HIP(ctx, hipMemsetAsync(n_out_dev, 0, sizeof(int64_t), ctx->stream));
         return QK_OK;
     }
-    const int c = (int)count;
-    size_t s1 = 0, s2 = 0, s3 = 0;
-    QKS_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, s1, (int64_t*)nullptr, (int64_t*)nullptr,
-                                                    (double*)nullptr, (double*)nullptr, c));
-    QKS_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, s2, (double*)nullptr, (double*)nullptr,
-                                                    (int64_t*)nullptr, (int64_t*)nullptr, c));
-    QKS_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, s3, (double*)nullptr, (double*)nullptr, c));
-    size_t cub = s1 > s2 ? s1 : s2;
-    cub = cub > s3 ? cub : s3;
+    const size_t c = (size_t)count;
     char* base = (char*)ws;
-    size_t off = al256(cub);
-    int64_t* k1 = (int64_t*)(base + off); off += al256((size_t)c * 8);
-    double* v1 = (double*)(base + off); off += al256((size_t)c * 8);
-    int64_t* k2 = (int64_t*)(base + off); off += al256((size_t)c * 8);
-    double* v2 = (double*)(base + off); off += al256((size_t)c * 8);
-    double* S = (double*)(base + off); off += al256((size_t)c * 8);
-    unsigned long long* first = (unsigned long long*)(base + off);
-    size_t t = cub;
+    size_t off = 0;
+    int64_t* k1 = (int64_t*)(base + off); off += al256(8 * c);
+    double* v1 = (double*)(base + off); off += al256(8 * c);
+    int64_t* k2 = (int64_t*)(base + off); off += al256(8 * c);
+    double* v2 = (double*)(base + off); off += al256(8 * c);
+    double* S = (double*)(base + off); off += al256(8 * c);
+    unsigned long long* first = (unsigned long long*)(base + off); off += 256;
+    void* tmp = base + off;
+    const size_t tmp_bytes = (size_t)ws_bytes - off;
     // by key, then stably by value: ties in value come out in key order whatever the append order was
-    QKS_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(ws, t, keys, k1, vals, v1, c, 0, 64, ctx->stream));
-    t = cub;
-    QKS_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(ws, t, v1, v2, k1, k2, c, 0, 64, ctx->stream));
-    t = cub;
-    QKS_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(ws, t, v2, S, c, ctx->stream));
+    QKS_HIP(ctx, qkp::radix_sort_pairs(ctx->stream, count, (const uint64_t*)keys, (const uint64_t*)vals, (uint64_t*)k1,
+                                       (uint64_t*)v1, 0, key_bits, qkp::KEY_U64, tmp, tmp_bytes));
+    QKS_HIP(ctx, qkp::radix_sort_pairs(ctx->stream, count, (const uint64_t*)v1, (const uint64_t*)k1, (uint64_t*)v2,
+                                       (uint64_t*)k2, 0, 64, qkp::KEY_F64, tmp, tmp_bytes));
+    QKS_HIP(ctx, qkp::exclusive_sum(ctx->stream, count, v2, S, tmp, tmp_bytes));
     hipLaunchKernelGGL(sel_init_first_kernel, dim3(1), dim3(1), 0, ctx->stream, count, first);
     hipLaunchKernelGGL(sel_first_kept_kernel, dim3(sel_grid(count)), dim3(256), 0, ctx->stream, count, v2, S, first);
     hipLaunchKernelGGL(sel_emit_kernel, dim3(sel_grid(count)), dim3(256), 0, ctx->stream, count, v2, k2, S, first,
                        out_keys, out_vals, n_out_dev);
     QKS_HIP(ctx, hipGetLastError());
     return QK_OK;
+}
+
+extern "C" {
+
+int qk_npd_pairs_workspace_bytes(int64_t count, int64_t* bytes) {
+    if (!bytes || count < 0 || count > 0x7fffffff) return QK_EARG;
+    *bytes = (int64_t)npd_pairs_bytes(count);
+    return QK_OK;
+}
+
+int qk_npd_pairs(qk_ctx* ctx, int64_t count, const int64_t* keys, const double* vals, void* ws, int64_t ws_bytes,
+                 int64_t* out_keys, double* out_vals, int64_t* n_out_dev) {
+    // keys are any non-negative int64 (qk_knit_select: pdep of up to 62 output bits): all 64 bits sorted
+    return npd_pairs_bits(ctx, count, keys, vals, 64, ws, ws_bytes, out_keys, out_vals, n_out_dev);
 }
 
 }  // extern "C"

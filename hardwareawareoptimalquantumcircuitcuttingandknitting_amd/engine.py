@@ -639,12 +639,14 @@ def gemm_keyed(ctx: Context, A, B, keyA=None, keyB=None, out=None, strideA: int 
     """
     K, M = A.shape
     K2, N = B.shape
-    assert K == K2 and A.dtype == B.dtype and A.is_contiguous() and B.is_contiguous()
+    # row-major operands; a column range of a wider matrix (X[:, lo:hi]) passes its row stride as lda
+    assert K == K2 and A.dtype == B.dtype and (A.stride(1) == 1 or M == 1) and (B.stride(1) == 1 or N == 1)
+    lda, ldb = (A.stride(0) if K > 1 else M), (B.stride(0) if K > 1 else N)
     if keyA is not None:
         assert keyA.shape[0] == M and keyA.dtype == torch().int64
     if keyB is not None:
         assert keyB.shape[0] == N and keyB.dtype == torch().int64
-    ctx.check(ctx.lib.qk_gemm_keyed_pred(ctx.handle, M, N, K, A.data_ptr(), M, B.data_ptr(), N,
+    ctx.check(ctx.lib.qk_gemm_keyed_pred(ctx.handle, M, N, K, A.data_ptr(), lda, B.data_ptr(), ldb,
                                          _ptr(keyA), strideA, _ptr(keyB), strideB, out.data_ptr(), beta, _ptr(skip)),
               "qk_gemm_keyed_pred")
     return out
@@ -1460,7 +1462,10 @@ def knit_select(ctx: Context, A, B, clbits_a: list, clbits_b: list, nbits: int, 
     reruns with exactly enough room when the first capacity was short."""
     T = torch()
     K = A.shape[0]
-    assert B.shape[0] == K and 1 <= K <= 8 and A.is_contiguous() and B.is_contiguous()
+    # row-major operands; a column range of wider ones (a rank's slice) passes its row stride
+    assert B.shape[0] == K and 1 <= K <= 8 and (A.stride(1) == 1 or A.shape[1] == 1) and (
+        B.stride(1) == 1 or B.shape[1] == 1)
+    lda, ldb = (A.stride(0) if K > 1 else A.shape[1]), (B.stride(0) if K > 1 else B.shape[1])
     mA, mB = sum(1 << c for c in clbits_a), sum(1 << c for c in clbits_b)
     dev = A.device
     need = ctypes.c_int64()
@@ -1472,13 +1477,33 @@ def knit_select(ctx: Context, A, B, clbits_a: list, clbits_b: list, nbits: int, 
     while True:
         keys = T.empty(max(cap, 1), dtype=T.int64, device=dev)
         vals = T.empty(max(cap, 1), dtype=T.float64, device=dev)
-        ctx.check(ctx.lib.qk_knit_select(ctx.handle, nbits, K, A.data_ptr(), A.shape[1], B.data_ptr(), B.shape[1],
+        ctx.check(ctx.lib.qk_knit_select(ctx.handle, nbits, K, A.data_ptr(), lda, B.data_ptr(), ldb,
                                          mA, mB, float(accuracy), _ptr(k_dev), work.data_ptr(), work.numel() * 8,
                                          cap, keys.data_ptr(), vals.data_ptr(), cnt.data_ptr()), "qk_knit_select")
         n = int(cnt.item())
         if n <= cap:
             return keys[:n], vals[:n]
         cap = n
+
+
+def select_above(ctx: Context, dense, accuracy: float, key_base: int = 0):
+    """``qk_select_above``: device ``(keys, vals)`` of the entries ``|v| > accuracy`` of a dense vector
+    (keys = index + ``key_base``), unordered. One host read of the count; reruns with exactly enough
+    room when the first capacity was short."""
+    T = torch()
+    dense = dense.contiguous().view(-1)
+    n, dev = dense.numel(), dense.device
+    cnt = T.empty(1, dtype=T.int64, device=dev)
+    cap = min(n, 1 << 20)
+    while True:
+        keys = T.empty(max(cap, 1), dtype=T.int64, device=dev)
+        vals = T.empty(max(cap, 1), dtype=T.float64, device=dev)
+        ctx.check(ctx.lib.qk_select_above(ctx.handle, n, dense.data_ptr(), float(accuracy), int(key_base), cap,
+                                          keys.data_ptr(), vals.data_ptr(), cnt.data_ptr()), "qk_select_above")
+        k = int(cnt.item())
+        if k <= cap:
+            return keys[:k], vals[:k]
+        cap = k
 
 
 def npd_pairs(ctx: Context, keys, vals):

@@ -81,9 +81,16 @@ ROW_JOBS = int(os.environ.get("QKNIT_ROW_JOBS", "4"))
 # core columns are exactly 0 for 42 of them and at most 1e-14 of the core's largest entry for the
 # others, cancellations left at rounding level; the compressed transform's columns for them are
 # 1e-20..2e-15 against entries of 1e-4..1.2 for the 64 others). Their 500 of the fragment's 625 branch
-# jobs are dropped, and the operand transforms lose those rows; every operand X = Wt^T q changes by
-# at most sum_j |W[:, j]| |q_j| <= 192 x 2e-15 (q: probabilities), below the rounding of X itself.
+# jobs are dropped, and the operand transforms lose those rows. Whether that is sound is not assumed:
+# the plan sweeps every row once (the plan's inputs are fixed, the sweep exact and deterministic, so
+# every step sees the same q) and bounds the change of every output of R = X_A^T X_B, X_f = W_f q_f:
+# with X_f = X'_f + D_f (kept rows / pruned rows),
+#   |R - R'|[a, b] <= sum_k  m_A[k] d_B[k] + d_A[k] m_B[k] + d_A[k] d_B[k],
+#   m_f[k] = max_x |X'_f[k, x]|,  d_f[k] = sum_{j pruned} |W_f[k, j]| max_x |q_f[j, x]|
+# (_prune_bound). Rows are pruned only when that bound is at most PRUNE_TOL; otherwise the threshold
+# is lowered tenfold (down to 1e-16) and, failing that, nothing is pruned. syc 32 5: see DESIGN §3.
 ROW_PRUNE = float(os.environ.get("QKNIT_ROW_PRUNE", "1e-12"))
+PRUNE_TOL = float(os.environ.get("QKNIT_PRUNE_TOL", "1e-13"))  # largest output change pruning may cause
 
 
 def _split_rows(offsets: np.ndarray, max_jobs: int):
@@ -250,6 +257,11 @@ class HipBackend:
     def sweep(self, fs, slot, sign, n_jobs, pjob, ws):
         engine.sweep_jobs(self.ctx, fs.dprog, slot, sign, n_jobs, pjob=pjob, workspace=ws)
 
+    def sweep_rows(self, fs):
+        """Every swept row of fragment ``fs`` [rows, 2^m] (the plan's one-off sweep for the row-pruning
+        bound, KnitPipeline._prune_rows)."""
+        return engine.sweep_fragment(self.ctx, fs)
+
     def fold_traced(self, q, fold):
         return engine.fold_traced(self.ctx, q, fold)
 
@@ -354,6 +366,9 @@ class HipBackend:
 
     def npd_pairs(self, keys, vals):
         return engine.npd_pairs(self.ctx, keys, vals)
+
+    def select_above(self, dense, accuracy, key_base=0):
+        return engine.select_above(self.ctx, dense, accuracy, key_base=key_base)
 
     def npd_dense(self, dense, accuracy):
         return engine.nearest_probability_distribution(self.ctx, dense, accuracy)
@@ -485,6 +500,13 @@ class KnitPipeline:
         self.row_jobs = ROW_JOBS
         self.row_prune = ROW_PRUNE
         self.out_alloc = None  # how the last output buffer was allocated (new_out)
+        # slice mode: how a rank gets the operands of its slice (_choose_slice_prep, QKNIT_SLICE_PREP):
+        # "replicated" — every rank sweeps every swept row and runs the whole preparation chain itself
+        # (deterministic kernels on identical inputs: identical operands and verdicts on every rank), then
+        # writes its slice; no collective in the step. "sharded" — rows dealt over the ranks, one
+        # all_to_all / all_reduce / all_gather / MIN all_reduce per step (round 2-4's slice mode).
+        self.slice_prep = None
+        self.slice_costs = None  # the cost model's per-step estimates (ms) of both, when it chose
         self._plan()
 
     def _stream_bits(self):
@@ -502,7 +524,8 @@ class KnitPipeline:
         two-fragment knit written by the streaming kernel; world a power of two; >= 2^9 outputs and
         whole column blocks of both fragments per rank)."""
         cA, cB = self._stream_bits()
-        if cA is None or world < 2 or world & (world - 1) or not self.factored:
+        # world 1: only when asked for (mode="slice": the collectives on a one-rank group, tests)
+        if cA is None or world < 1 or world & (world - 1) or not self.factored:
             return False
         return (1 << self.N) // world >= 512 and min(len(cA), len(cB)) >= world.bit_length() - 1
 
@@ -516,6 +539,11 @@ class KnitPipeline:
         L = self.ops.num_terms
         self.term_range = _shard(L, self.rank, self.world) if self.mode == "reduce" else (0, L)
         self.place = {}  # gather mode: fragment -> position of each swept row in the gathered rows
+        pruned = self._prune_rows()
+        swept = [self._swept_rows(i, fs, pruned.get(i)) for i, fs in enumerate(self.frags)]
+        if self.mode == "slice":
+            self.slice_prep, self.slice_costs = self._choose_slice_prep(swept)
+        self.sharded = self.mode == "gather" or (self.mode == "slice" and self.slice_prep == "sharded")
         for i, fs in enumerate(self.frags):
             if fs.dropped:
                 self.sweeps.append(None)
@@ -523,26 +551,12 @@ class KnitPipeline:
                 self.n_rows.append(fs.n_rows)
                 self.plan_jobs.append(0)
                 continue
-            nl = fs.n_rows
-            jobs = fs.jobs
-            src = None
-            W = self.ops.transforms[i]
-            if W is not None and self.row_prune > 0 and jobs.n_jobs:
-                cm = np.abs(np.asarray(W)).max(axis=0)  # per swept row: its largest transform entry
-                live = np.flatnonzero(cm > self.row_prune * cm.max())
-                if 0 < live.size < nl:
-                    src, jobs, nl = live, jobs.take(live), live.size
-            if W is not None and self.row_jobs > 0 and jobs.n_jobs:
-                piece_src, offs = _split_rows(jobs.label_offsets, self.row_jobs)
-                if len(piece_src) > nl:
-                    jobs = JobTable(jobs.slot_mats, jobs.sign, offs, jobs.branch_bits)
-                    nl = len(piece_src)
-                    src = piece_src if src is None else src[piece_src]
+            src, jobs, nl = swept[i]
             self.row_src.append(src)
             self.n_rows.append(nl)
             self.plan_jobs.append(jobs.n_jobs)
             lo = 0
-            if self.mode in ("gather", "slice"):
+            if self.sharded:
                 per = -(-nl // self.world)
                 dealt = _deal_rows(jobs.label_jobs(), self.world)
                 place = np.zeros(nl, dtype=np.int64)
@@ -563,9 +577,9 @@ class KnitPipeline:
             n_jobs = sub.n_jobs
             width = self.be.device_width(fs) if hasattr(self.be, "device_width") else 1 << fs.prog.m
             need = be.workspace_bytes(fs, n_jobs) if n_jobs else 0
-            # gather mode: a rank's rows live in a zero-padded [per, width] buffer (the unit of
-            # the collectives); padding rows stay zero
-            sharded = self.mode in ("gather", "slice")
+            # gather / sharded slice mode: a rank's rows live in a zero-padded [per, width] buffer (the
+            # unit of the collectives); padding rows stay zero
+            sharded = self.sharded
             rows = -(-nl // self.world) if sharded else max(n_local, 1)
             alloc = be.zeros if sharded else be.empty
             branching = n_jobs != n_local
@@ -585,9 +599,114 @@ class KnitPipeline:
                                     q=alloc((max(rows, 1), width), T.float64) if branching else None,
                                     ws=be.empty((max(need, 1),), T.uint8)))
         self._plan_knit()
-        if self.mode in ("gather", "slice"):
+        if self.sharded:
             self._plan_exchange()
         self._plan_multi()
+
+    def _prune_rows(self) -> dict:
+        """{fragment: kept swept rows} of the row pruning (ROW_PRUNE, PRUNE_TOL): two live fragments
+        with factored transforms only; the bound of every output's change (``_prune_bound``) on the
+        plan's own rows, swept once here, must be at most PRUNE_TOL. ``self.prune_bound`` keeps it."""
+        self.prune_bound = None
+        W = self.ops.transforms
+        live = [i for i, fs in enumerate(self.frags) if not fs.dropped]
+        if (self.row_prune <= 0 or len(live) != 2 or any(W[i] is None or not self.frags[i].jobs.n_jobs for i in live)
+                or not hasattr(self.be, "sweep_rows")):
+            return {}
+        cms = {i: np.abs(np.asarray(W[i])).max(axis=0) for i in live}  # per swept row: largest entry
+        qs, thr = None, self.row_prune
+        while thr >= 1e-16:
+            keep = {i: np.flatnonzero(cms[i] > thr * cms[i].max()) for i in live}
+            pruned = {i: k for i, k in keep.items() if k.size < cms[i].size}
+            if not pruned:  # nothing below this threshold, so nothing below any smaller one
+                return {}
+            if qs is None:
+                qs = {i: self.be.sweep_rows(self.frags[i]) for i in live}
+            bound = self._prune_bound(qs, keep)
+            if bound <= PRUNE_TOL:
+                self.prune_bound = bound
+                return pruned
+            thr /= 10
+        return {}
+
+    def _prune_bound(self, qs: dict, keep: dict) -> float:
+        """Bound on max |R - R'| over every output when only the ``keep`` rows of each side are swept
+        (the ROW_PRUNE comment): ``qs`` every swept row of both sides [rows, 2^m], exact."""
+        T = self.T
+        m, d = [], []
+        for i in sorted(keep):
+            q = qs[i]
+            Wi = T.as_tensor(np.ascontiguousarray(self.ops.transforms[i]), dtype=T.float64, device=q.device)
+            k = T.as_tensor(keep[i], device=q.device)
+            m.append((Wi[:, k] @ q[k]).abs().amax(dim=1))
+            gone = np.setdiff1d(np.arange(Wi.shape[1]), keep[i])
+            if gone.size:
+                g = T.as_tensor(gone, device=q.device)
+                d.append((Wi[:, g].abs() * q[g].abs().amax(dim=1)[None, :]).sum(dim=1))
+            else:
+                d.append(T.zeros(Wi.shape[0], dtype=T.float64, device=q.device))
+        return float((m[0] * d[1] + d[0] * m[1] + d[0] * d[1]).sum())
+
+    def _swept_rows(self, i: int, fs, keep):
+        """(source label of every swept row or None, job table, rows) of fragment i: the ``keep`` rows
+        of the row pruning, labels of more than ROW_JOBS branch jobs split into several rows."""
+        if fs.dropped:
+            return None, None, fs.n_rows
+        nl, jobs, src = fs.n_rows, fs.jobs, None
+        if keep is not None:
+            src, jobs, nl = keep, jobs.take(keep), keep.size
+        if self.ops.transforms[i] is not None and self.row_jobs > 0 and jobs.n_jobs:
+            piece_src, offs = _split_rows(jobs.label_offsets, self.row_jobs)
+            if len(piece_src) > nl:
+                jobs = JobTable(jobs.slot_mats, jobs.sign, offs, jobs.branch_bits)
+                nl = len(piece_src)
+                src = piece_src if src is None else src[piece_src]
+        return src, jobs, nl
+
+    # slice-mode cost model (_choose_slice_prep), per step on one rank. Rates measured on syc 32 5:
+    # the sweep's modelled fp64 flops (_sweep_flops_per_job) ran at ~49 TF/s (2.79 GFLOP in 0.057 ms,
+    # BENCH_r04), the preparation chain 0.14 ms for 2 x 65 rows x 2^16 columns x K = 64 (2.2 GFLOP of
+    # transforms + Grams at ~27 TF/s, plus ~60 us of dependent small launches whatever the size);
+    # collectives as rank_sim's xGMI model: 20 us per collective + received bytes / (min(world - 1, 7)
+    # links x 50 GB/s), and the packing glue around them at a third of HBM speed (read + reorder +
+    # write; ~200 us at 8 ranks on syc 32 5, profiles/r04s_rank_sim_8_timeline_split.txt)
+    SWEEP_MODEL_TFS = 49.0
+    PREP_FIXED_MS, PREP_GFS = 0.06, 27000.0  # MFMA GFLOP/s the transforms + Grams reach in the chain
+    XGMI_GBS, COLL_LAT_MS = 50.0, 0.020
+
+    def _choose_slice_prep(self, rows: list):
+        """("replicated" | "sharded", {estimates}) for slice mode. ``QKNIT_SLICE_PREP`` forces one.
+        Replicated: every rank runs the whole sweep and preparation (t_sweep + t_prep), no collective.
+        Sharded: 1/world of each plus four collectives (all_to_all of the rows' column blocks, the
+        Gram all_reduce, the compressed-operand all_gather, the MIN all_reduce) and, with the
+        predicated exact fallback, the all_gather of the exact operands. The cheaper estimate wins."""
+        P = self.world
+        force = os.environ.get("QKNIT_SLICE_PREP", "auto")
+        from . import sweep_plan
+
+        flops, prep_flops, a2a, gat = 0, 0.0, 0, 0
+        K = self.ops.num_terms
+        for i, fs in enumerate(self.frags):
+            src, jobs, nl = rows[i]
+            if fs.dropped or jobs is None:
+                continue
+            enc = fs.dprog.enc if getattr(fs, "dprog", None) is not None else sweep_plan.encode(fs.prog)
+            flops += jobs.n_jobs * _sweep_flops_per_job(enc)
+            w = 1 << fs.prog.m
+            prep_flops += 2.0 * K * nl * w + 2.0 * K * K * w
+            a2a += 8 * nl * w * (P - 1) // (P * P)  # received: its column block of every peer's rows
+            gat += 8 * K * w * (P - 1) // P  # the exact operands' column blocks (one side travels)
+        t_sweep = flops / (self.SWEEP_MODEL_TFS * 1e9)
+        t_prep = self.PREP_FIXED_MS + prep_flops / (self.PREP_GFS * 1e6)
+        links = max(1, min(P - 1, 7))
+        coll = lambda nbytes: self.COLL_LAT_MS + nbytes / (links * self.XGMI_GBS * 1e6)  # noqa: E731
+        glue = 3 * (a2a + gat) / (8000 * 1e6) * 3
+        t_rep = t_sweep + t_prep
+        t_sh = (t_sweep + t_prep) / P + coll(a2a) + 3 * self.COLL_LAT_MS + coll(gat // 2) + glue
+        costs = {"replicated_ms": round(t_rep, 4), "sharded_ms": round(t_sh, 4)}
+        if force in ("replicated", "sharded"):
+            return force, costs
+        return ("replicated" if t_rep <= t_sh else "sharded"), costs
 
     def _plan_multi(self):
         """Single and gather mode: when every swept fragment runs compiled kernels of one tile
@@ -686,7 +805,7 @@ class KnitPipeline:
                     qs[i] = be.zeros((fs.n_rows, 1), T.float64) + 1.0
                     continue
                 q = self._fold(fs, sw["q"] if sw["fused"] else sw["pjob"])
-                if self.mode in ("gather", "slice"):
+                if self.sharded:
                     work, qs[i] = self._exchange(i, q)
                     pending.append(work)
                 else:
@@ -714,7 +833,7 @@ class KnitPipeline:
                     q = self._fold(fs, self._sweep_fragment(fs, sw))
             else:
                 q = self._fold(fs, self._sweep_fragment(fs, sw))
-            if self.mode in ("gather", "slice"):
+            if self.sharded:
                 work, qs[i] = self._exchange(i, q)
                 pending.append(work)
             else:
@@ -806,17 +925,20 @@ class KnitPipeline:
             self._probe = T.randn((self.N_PROBES, n), generator=g, dtype=T.float64).to(device)
         return self._probe
 
+    def _prep_step(self, qs) -> dict:
+        """The device data-rank preparation of one step: the sharded slice collectives, or the local
+        chain (single mode, replicated slice mode)."""
+        return self._prep_slice(qs) if self.mode == "slice" and self.sharded else self._prep_dev_rank(qs)
+
+    def _launch_step(self, p: dict):
+        return self._launch_slice(p) if self.mode == "slice" else self._launch_dev_rank(p)
+
     def knit(self, qs: list):
         if self.dev_rank and self.mode in ("single", "slice"):
-            if self.mode == "slice":
-                p = self._prep_slice(qs)
-                if self.out is None:
-                    self.out = self._alloc_out(None)
-                return self._launch_slice(p)
-            p = self._prep_dev_rank(qs)
+            p = self._prep_step(qs)
             if self.out is None:
                 self.out = self._alloc_out(None)
-            return self._launch_dev_rank(p)
+            return self._launch_step(p)
         mats = self.operands(qs)
         if self.out is None:
             self.out = self._alloc_out(mats)
@@ -1068,6 +1190,13 @@ class KnitPipeline:
         if self.record_events:
             end.record()
             self.events.append((start, end))
+        if not self.sharded:
+            # replicated preparation: every rank holds the whole transformed operands, so the exact
+            # slice (predicated on the same device verdict, identical on every rank) reads its columns
+            # in place — no collective
+            A, kA, B, kB = self._slice_exact_operands(*self._exact_mats(p))
+            be.gemm_keyed(A, B, keyA=kA, keyB=kB, out=self.out, skip=p["k_eff"])
+            return self.out
         if "exact" not in p:  # slice_exact == "host"
             if p["ready"] is not None:
                 p["ready"].synchronize()  # the check only, not the knit queued behind it
@@ -1100,8 +1229,20 @@ class KnitPipeline:
         if self._prep_stream is None:
             T = self.T
             dev = self.be.dev.index or 0
-            c = int(os.environ.get("QKNIT_PREP_CUS", str(self.PREP_CUS)))
+            env = os.environ.get("QKNIT_PREP_CUS", str(self.PREP_CUS))
             total = engine.device_cu_count(dev)
+            if env == "all":
+                # no CU split: both streams may use every CU (their own hardware queues); the write's
+                # grid (QKNIT_OB_WG_PER_CU) decides how many slots per CU it holds, the preparation
+                # takes the others
+                every = tuple(range(total))
+                self._prep_stream = engine.cu_masked_stream(dev, every)
+                self._write_stream = engine.cu_masked_stream(dev, every, tag=2)
+                self._write_cus = every
+                self.overlap_cus = (total, total)
+                self._prep_stream.wait_stream(T.cuda.current_stream())
+                return self._prep_stream, self._write_stream
+            c = int(env)
             if 0 < c < total:
                 # the top c logical CUs. The CU-mask bits of a stream are dealt over the XCDs (bit i ->
                 # XCD i % 8, CU i // 8 of it; tools/cu_mask_probe.py): a contiguous block of bits is
@@ -1146,6 +1287,14 @@ class KnitPipeline:
             return self.knit(self.sweep())
         S, W = self._overlap_streams()
         W = W if W is not None else main
+        # the caller's reads of an output buffer are queued on its stream after the step that wrote it
+        # returned; the write that reuses the buffer (next step with one buffer, the one after with two)
+        # waits for an event the caller's stream records at the start of step j - buffers + 1, which
+        # follows every read queued before that call, and not for the other buffer's write (so step j's
+        # write may still start under step j - 1's)
+        started = T.cuda.Event()
+        started.record(main)
+        self._started = (getattr(self, "_started", []) + [started])[-max(self.out_buffers, 1):]
         if self.out_buffers > 1:
             if self._outs is None:
                 self._outs = [self.out, self._alloc_out(None)]
@@ -1168,20 +1317,22 @@ class KnitPipeline:
                 self.sweep_events.append((s0, s1))
             if self.out is None:
                 self.out = self._alloc_out(None)
-            p = self._prep_slice(qs) if self.mode == "slice" else self._prep_dev_rank(qs)
+            p = self._prep_step(qs)
             done = T.cuda.Event(enable_timing=self.record_events)
             done.record(S)
         if self.record_events:
             self.prep_events.append((s1, done))
         with T.cuda.stream(W):
             W.wait_event(done)
+            if W is not main and len(self._started) == max(self.out_buffers, 1):
+                W.wait_event(self._started[0])
             be.bind()
             for k in ("A2", "B2", "k_eff"):
                 p[k].record_stream(W)
             for m in p["mats"]:
                 if m is not None:
                     m.record_stream(W)
-            out = self._launch_slice(p) if self.mode == "slice" else self._launch_dev_rank(p)
+            out = self._launch_step(p)
         if W is not main:
             main.wait_stream(W)
         be.bind()
@@ -1221,6 +1372,11 @@ class KnitPipeline:
         finisher returned instead — called on the stream that needs the operands, it makes that
         stream wait for them (their column reorder runs on a helper stream that waits for the gather,
         so it overlaps whatever runs meanwhile, the write in pipelined steps)."""
+        if not self.sharded:  # replicated preparation: whole operands on every rank, the slice's columns in place
+            parts = []
+            for X, (base, n, _, keys) in zip((XA, XB), self._slice_exact_plan()):
+                parts += [X[:, base:base + n], keys]
+            return tuple(parts)
         import torch.distributed as dist
 
         T, P = self.T, self.world
@@ -1269,6 +1425,10 @@ class KnitPipeline:
             return tuple(parts)
 
         return finish
+
+    def _exact_mats(self, p: dict):
+        """(X_A, X_B): the transformed operands of a prepared step, row side first."""
+        return p["mats"][self.order[0]], p["mats"][self.order[-1]]
 
     def _slice_exact(self, XA, XB, cA, cB):
         """Exact contraction of this rank's output slice (K terms) from the transformed column blocks
@@ -1521,6 +1681,8 @@ class KnitPipeline:
         qk_threshold_count + qk_npd."""
         if qs is None:
             qs = self.sweep()
+        if self.mode == "slice":
+            return self._knit_dict_slice(accuracy, qs)
         pair = self._select_pair()
         if pair is not None and self.dev_rank:
             p = self._prep_dev_rank(qs)
@@ -1548,6 +1710,68 @@ class KnitPipeline:
         finally:
             self.out = keep
 
+
+    def _knit_dict_slice(self, accuracy: float, qs):
+        """knit_dict in slice mode (multi-GPU; every rank returns the whole result, ``run.py:71``): each
+        rank selects the entries above ``accuracy`` of its own output slice — from the compressed
+        operands (qk_knit_select on the slice's column ranges: its keys are the slice-local outputs'
+        keys plus the slice start, since the slice's fixed bits and the ranges' own bits are disjoint)
+        or, after a rejected compression, from its exact dense slice (qk_select_above) —, the kept
+        pairs of all ranks are all-gathered (their union is exactly the single-GPU selection: the
+        slices partition the outputs, the values are bit-identical), and every rank runs the NPD of
+        the union (qk_npd_pairs: sorted by key, then by value, so the order of the union does not
+        matter)."""
+        import torch.distributed as dist
+
+        T, be = self.T, self.be
+        ia, ib = self.order[0], self.order[-1]
+        o_begin, o_count = self.slice
+        p = self._prep_step(qs) if self.dev_rank else None
+        keys = vals = None
+        if p is not None and int(p["k_eff"].reshape(-1)[0]) > 0:
+            (bA, nA, _, _), (bB, nB, _, _) = self._slice_exact_plan()
+            cA, cB = list(self.ops.clbits[ia]), list(self.ops.clbits[ib])
+            # the column ranges are the low log2(n) bits of each side's index (aligned blocks)
+            keys, vals = be.knit_select(p["A2"][:, bA:bA + nA], p["B2"][:, bB:bB + nB], cA[:nA.bit_length() - 1],
+                                        cB[:nB.bit_length() - 1], self.N, accuracy, k_dev=p["k_eff"])
+            keys = keys + o_begin
+            self.last_kernel = "qk_knit_select_kernel"
+        else:
+            keep = self.out
+            self.out = be.zeros((o_count,), T.float64)
+            try:
+                if p is not None:
+                    self._launch_step(p)  # the write is skipped (k = 0), the exact slice runs
+                else:
+                    ia_, ib_ = self.order[0], self.order[-1]
+                    mats = self.operands(qs)
+                    self._slice_exact(mats[ia_], mats[ib_], self.ops.clbits[ia_], self.ops.clbits[ib_])
+                keys, vals = be.select_above(self.out, accuracy, key_base=o_begin)
+            finally:
+                self.out = keep
+            self.last_kernel = None
+        if p is not None:
+            self.sync_stats()
+        # all-gather the ranks' kept pairs (counts first, then padded buffers)
+        n = T.tensor([keys.numel()], dtype=T.int64, device=keys.device)
+        counts = T.empty(self.world, dtype=T.int64, device=keys.device)
+        dist.all_gather_into_tensor(counts, n, group=self.group)
+        cnt = counts.cpu().tolist()
+        top = max(max(cnt), 1)
+        kp = T.zeros(top, dtype=T.int64, device=keys.device)
+        vp = T.zeros(top, dtype=T.float64, device=keys.device)
+        kp[:keys.numel()] = keys
+        vp[:vals.numel()] = vals
+        kall = T.empty(self.world * top, dtype=T.int64, device=keys.device)
+        vall = T.empty(self.world * top, dtype=T.float64, device=keys.device)
+        dist.all_gather_into_tensor(kall, kp, group=self.group)
+        dist.all_gather_into_tensor(vall, vp, group=self.group)
+        sel = [slice(r * top, r * top + c) for r, c in enumerate(cnt) if c]
+        if not sel:
+            return np.zeros(0, dtype=np.int64), np.zeros(0)
+        ku = T.cat([kall[s] for s in sel]) if len(sel) > 1 else kall[sel[0]]
+        vu = T.cat([vall[s] for s in sel]) if len(sel) > 1 else vall[sel[0]]
+        return be.npd_pairs(ku, vu)
 
     def step(self):
         bind = getattr(self.be, "bind", None)

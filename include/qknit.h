@@ -380,6 +380,13 @@ int qk_threshold_count(qk_ctx* ctx, int64_t n, const double* vals, double acc, v
 int qk_npd(qk_ctx* ctx, int64_t n, const double* vals, double acc, int64_t count, void* ws, int64_t ws_bytes,
            int64_t* out_keys, double* out_vals, int64_t* n_out_dev);
 
+/* The entries |vals[i]| > acc of a dense vector as (i + key_base, vals[i]) pairs, unordered, into keys /
+ * out_vals (DEVICE, capacity entries); *count_dev (DEVICE int64, set here) = their number, which may
+ * exceed capacity (then call again with more room). The multi-GPU dict result's exact fallback: a
+ * rank's dense output slice starting at output key_base (pipeline.KnitPipeline.knit_dict). */
+int qk_select_above(qk_ctx* ctx, int64_t n, const double* vals, double acc, int64_t key_base, int64_t capacity,
+                    int64_t* keys, double* out_vals, int64_t* count_dev);
+
 /* ---- shot sampling (qknit_sample.hip; run.py:42 `backend.run(instantiations, shots)` +
  * quasi_distr.py:12-20 `from_counts`) ----------------------------------------------------------
  * An instance s owns the pjob rows [seg_off[s], seg_off[s+1]) (its branch jobs, width values each);

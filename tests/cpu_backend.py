@@ -47,6 +47,13 @@ class CpuBackend:
         enc = sweep_plan.encode(fs.prog)
         pjob[:n_jobs] = torch.from_numpy(emulate(enc, slot[:n_jobs], sign.numpy()[:n_jobs]))
 
+    def sweep_rows(self, fs):
+        """Every swept row [rows, 2^m] of fs (the plan's row-pruning bound): emulated jobs, label sums."""
+        enc = sweep_plan.encode(fs.prog)
+        pj = torch.from_numpy(emulate(enc, fs.jobs.slot_mats, fs.jobs.sign))
+        off = fs.jobs.label_offsets
+        return torch.stack([pj[off[l]:off[l + 1]].sum(0) for l in range(len(off) - 1)])
+
     def reduce_labels(self, pjob, off, n_labels, q):
         o = off.numpy()
         for l in range(n_labels):

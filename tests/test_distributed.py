@@ -106,10 +106,10 @@ def test_multi_rank_pipeline_matches_oracle(case, mode, factored, world):
     np.testing.assert_allclose(res, ref, atol=1e-12, rtol=0)
 
 
-def _slice_worker(rank, world, port, case, data_rank, q, veto_rank=None, row_jobs=None):
+def _slice_worker(rank, world, port, case, data_rank, q, veto_rank=None, row_jobs=None, prep="sharded"):
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), QKNIT_SLICE_PREP=prep)
     import torch
     import torch.distributed as dist
 
@@ -125,7 +125,7 @@ def _slice_worker(rank, world, port, case, data_rank, q, veto_rank=None, row_job
         _, cut = _slice_case(case)
         pipe = KnitPipeline(VirtualCircuit(cut), rank=rank, world=world, factored=True, backend=CpuBackend(),
                             data_rank=data_rank)
-        assert pipe.mode == "slice"
+        assert pipe.mode == "slice" and pipe.slice_prep == prep and pipe.sharded == (prep == "sharded")
         # pipelined steps alternate two output buffers at 4 ranks only (QKNIT_OUT_BUFFERS overrides)
         assert pipe.out_buffers == (2 if world == 4 else 1)
         if veto_rank == rank:  # this rank's probe check rejects every compression
@@ -155,24 +155,27 @@ def _slice_case(name):
     }[name]()
 
 
+@pytest.mark.parametrize("prep", ["sharded", "replicated"])
 @pytest.mark.parametrize("case,world,data_rank,row_jobs", [("hwe_p2", 2, True, None), ("hwe_p2", 4, True, None),
                                                            ("cx_8x8", 2, True, None), ("cx_6x5", 2, True, None),
                                                            ("hwe_p2", 2, False, None), ("cx_6x5", 2, True, 1)])
-def test_slice_mode_matches_oracle(case, world, data_rank, row_jobs):
+def test_slice_mode_matches_oracle(case, world, data_rank, row_jobs, prep):
     """slice mode: each rank writes the contiguous range [rank, rank + 1) * 2^N / world of the
     reference-ordered distribution; the slices concatenate (no permutation) to the oracle's dense
     knit within 1e-12, twice in a row. cx_8x8's knit has rank > 8 (the exact contraction of the
-    slice from all-gathered operands); the others compress on every step."""
+    slice: from all-gathered operands when sharded, from the rank's own whole operands when
+    replicated); the others compress on every step. Both preparations: rows dealt over the ranks with
+    collectives (sharded) and every rank sweeping and preparing everything (replicated: no collective)."""
     from oracle import dense
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_slice_worker, args=(r, world, port, case, data_rank, q, None, row_jobs))
+    procs = [ctx.Process(target=_slice_worker, args=(r, world, port, case, data_rank, q, None, row_jobs, prep))
              for r in range(world)]
     for p in procs:
         p.start()
-    outs, sl, last_rank, fallbacks, incompressible, dev, prep = q.get(timeout=300)
+    outs, sl, last_rank, fallbacks, incompressible, dev, last_prep = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -188,7 +191,8 @@ def test_slice_mode_matches_oracle(case, world, data_rank, row_jobs):
     if case == "cx_8x8":
         assert incompressible == 2 and last_rank is None
     if data_rank:  # 128-column blocks take the fused preparation (qk_prep_operands' contract), others torch
-        assert prep == ("fused" if (case, world) in (("hwe_p2", 2), ("cx_8x8", 2)) else "torch")
+        fused = (case, world) in (("hwe_p2", 2), ("cx_8x8", 2)) or (prep == "replicated" and case != "cx_6x5")
+        assert last_prep == ("fused" if fused else "torch")
 
 
 def _api_worker(rank, world, port, case, q):
@@ -248,20 +252,23 @@ def test_run_virtual_circuit_sharded_api(case, world):
         assert shards == [(r * n // world, n // world) for r in range(world)]
 
 
-def test_slice_mode_one_rank_rejects():
-    """A probe check that rejects on ONE rank only (that rank's tolerance forced below zero): the MIN
-    all-reduce of the accepted ranks sends every rank to the exact slice together (their
-    collectives match: no hang), and the slices still concatenate to the oracle's knit."""
+@pytest.mark.parametrize("prep", ["sharded", "replicated"])
+def test_slice_mode_one_rank_rejects(prep):
+    """A probe check that rejects on ONE rank only (that rank's tolerance forced below zero). Sharded:
+    the MIN all-reduce of the accepted ranks sends every rank to the exact slice together (their
+    collectives match: no hang). Replicated: no collective, so rank 0 keeps its accepted compression
+    and only rank 1 writes its slice exactly. Either way the slices concatenate to the oracle's knit."""
     from oracle import dense
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     world = 2
-    procs = [ctx.Process(target=_slice_worker, args=(r, world, port, "hwe_p2", True, q, 1)) for r in range(world)]
+    procs = [ctx.Process(target=_slice_worker, args=(r, world, port, "hwe_p2", True, q, 1, None, prep))
+             for r in range(world)]
     for p in procs:
         p.start()
-    outs, sl, last_rank, fallbacks, incompressible, dev, prep = q.get(timeout=300)
+    outs, sl, last_rank, fallbacks, incompressible, dev, _ = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -270,4 +277,7 @@ def test_slice_mode_one_rank_rejects():
     ref = dense.run_dense(cut)
     for got in outs:
         np.testing.assert_allclose(got, ref, atol=1e-12, rtol=0)
-    assert dev and fallbacks == 2 and last_rank is None  # rank 0 accepted locally, yet took the exact path
+    if prep == "sharded":
+        assert dev and fallbacks == 2 and last_rank is None  # rank 0 accepted locally, yet took the exact path
+    else:
+        assert dev and fallbacks == 0 and last_rank is not None  # rank 0's own verdict

@@ -130,8 +130,19 @@ def _run(target, world, *args, timeout=300, **kw):
     procs = [ctx.Process(target=target, args=(r, world, port, *args, q), kwargs=kw) for r in range(world)]
     for p in procs:
         p.start()
+    import queue
+    import time
+
     try:
-        got = q.get(timeout=timeout)
+        t_end = time.time() + timeout
+        while True:  # a worker that dies (an assertion, a crash) fails the test now, not at the timeout
+            try:
+                got = q.get(timeout=5)
+                break
+            except queue.Empty:
+                dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+                assert not dead, f"worker exited with {dead}"
+                assert time.time() < t_end, "no result before the timeout"
     finally:
         for p in procs:
             p.join(timeout=120)
@@ -196,11 +207,11 @@ def test_multi_rank_hip_overlapped_steps_match_oracle(case, world, veto, monkeyp
         assert incompressible == 2
 
 
-def _syc_worker(rank, world, port, q, overlap=False):
+def _syc_worker(rank, world, port, q, overlap=False, prep="auto"):
     log = _watchdog(rank, f"syc_32_5_{world}", after=700)
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), QKNIT_SLICE_PREP=prep)
     import torch
     import torch.distributed as dist
 
@@ -212,53 +223,145 @@ def _syc_worker(rank, world, port, q, overlap=False):
         torch.cuda.set_device(0)
         _, cut = _case("syc_32_5")
         virt = VirtualCircuit(cut)
-        pipe = KnitPipeline(virt, device=0, rank=rank, world=world, factored=True)
-        assert pipe.mode == "slice" and pipe.dev_rank
-        if overlap:  # pipelined steps (the multi-GPU bench default): a non-default caller stream
-            torch.cuda.set_stream(torch.cuda.Stream())
-            pipe.overlap = pipe.overlap_ok()
-            assert pipe.overlap
-        log("planned")
-        for it in range(3):  # plain first step, then pipelined (at 4 ranks: both output buffers)
-            sl = pipe.step()
-            torch.cuda.synchronize()
-            log(f"step {it}")
-        pipe.sync_stats()
-        assert pipe.rank_fallbacks == 0 and pipe.last_rank is not None
-        lo, cnt = pipe.slice
-        total = torch.tensor([float(sl.sum())], dtype=torch.float64)
-        mn = float(sl.min())
-        del pipe
-        torch.cuda.empty_cache()
-        # the single-GPU step of the same workload, computed one rank at a time (memory)
-        err = torch.zeros(1, dtype=torch.float64)
+        lo, cnt = rank * ((1 << 32) // world), (1 << 32) // world
+        # the single-GPU step of the same workload, one rank at a time (memory); each rank keeps its range
+        ref = None
         for r in range(world):
             dist.barrier()
             if r == rank:
                 one = KnitPipeline(virt, device=0, factored=True)
                 full = one.step()
-                err[0] = float((full[lo:lo + cnt] - sl).abs().max())
-                log("single-GPU step compared")
+                ref = full[lo:lo + cnt].clone()
+                log("single-GPU step done")
                 del one, full
                 torch.cuda.empty_cache()
+        dist.barrier()
+        pipe = KnitPipeline(virt, device=0, rank=rank, world=world, factored=True)
+        assert pipe.mode == "slice" and pipe.dev_rank and pipe.slice == (lo, cnt)
+        if prep != "auto":
+            assert pipe.slice_prep == prep
+        if overlap:  # pipelined steps (the multi-GPU bench default): a non-default caller stream
+            torch.cuda.set_stream(torch.cuda.Stream())
+            pipe.overlap = pipe.overlap_ok()
+            assert pipe.overlap
+        log(f"planned ({pipe.slice_prep})")
+        # plain first step, then pipelined (at 4 ranks: both output buffers, so every buffer is checked)
+        err = torch.zeros(1, dtype=torch.float64)
+        ptrs = set()
+        for it in range(4):
+            sl = pipe.step()
+            torch.cuda.synchronize()
+            err[0] = max(float(err[0]), float((sl - ref).abs().max()))
+            ptrs.add(sl.data_ptr())
+            log(f"step {it} compared")
+        pipe.sync_stats()
+        assert pipe.rank_fallbacks == 0 and pipe.last_rank is not None
+        total = torch.tensor([float(sl.sum())], dtype=torch.float64)
+        mn = float(sl.min())
+        n_buf = torch.tensor([float(len(ptrs))])
         dist.all_reduce(total)
         dist.all_reduce(err, op=dist.ReduceOp.MAX)
+        dist.all_reduce(n_buf, op=dist.ReduceOp.MIN)
         if rank == 0:
-            q.put((float(total[0]), float(err[0]), mn, (lo, cnt)))
+            q.put((float(total[0]), float(err[0]), mn, (lo, cnt), pipe.slice_prep, int(n_buf[0]), pipe.out_buffers))
+        del pipe
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(1000)
-@pytest.mark.parametrize("world,overlap", [(2, False), (4, True), (8, True)])
-def test_syc_32_5_slice_mode_equals_single_gpu(world, overlap):
+@pytest.mark.parametrize("world,overlap,prep", [(2, False, "auto"), (4, True, "auto"), (8, True, "auto"),
+                                                (8, True, "sharded")])
+def test_syc_32_5_slice_mode_equals_single_gpu(world, overlap, prep):
     """The bench workload's multi-GPU path (slice mode, device data rank) at 2 ranks (plain steps) and
     at 4 and 8 ranks with pipelined steps (the multi-GPU bench default, BASELINE config 5: syc 32 5
-    sharded over 8 GPUs; at 4 ranks two output buffers alternate, QKNIT_OUT_BUFFERS): each rank's 2^32 / world-entry slice equals the same range of the single-GPU step
-    within 1e-12, the slices sum to 1 and no entry is below -1e-13. The exact-slice fallback is
-    predicated on the device (no host sync in the step)."""
-    total, err, mn, sl = _run(_syc_worker, world, timeout=900, overlap=overlap)
+    sharded over 8 GPUs; at 4 ranks two output buffers alternate, QKNIT_OUT_BUFFERS), with the
+    preparation the cost model picks (replicated: no collective) and, at 8 ranks, the sharded one:
+    the slice returned by EVERY one of four steps (a plain one, then pipelined ones: both output buffers
+    at 4 ranks) equals the same range of the single-GPU step within 1e-12, the slices sum to 1 and no
+    entry is below -1e-13. The exact-slice fallback is predicated on the device (no host sync in the step)."""
+    total, err, mn, sl, chosen, n_buf, buffers = _run(_syc_worker, world, timeout=900, overlap=overlap, prep=prep)
     assert sl == (0, (1 << 32) // world)
     assert err <= TOL
     assert abs(total - 1.0) <= 1e-10
     assert mn >= -1e-13
+    assert chosen == ("replicated" if prep == "auto" else prep)
+    assert n_buf == (buffers if overlap else 1)
+
+
+def _nccl_worker(rank, world, port, case, prep, buffers, veto, q):
+    """One rank of a real RCCL group (world size 1: the test box has one GPU): slice mode forced,
+    pipelined steps on the CU-masked streams, so every collective of the sharded step (all_to_all,
+    Gram all_reduce, compressed-operand all_gather, MIN all_reduce, the async exact-operand
+    all_gather) runs on nccl beside the masked write streams."""
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), QKNIT_SLICE_PREP=prep,
+                      QKNIT_OUT_BUFFERS=str(buffers))
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    try:
+        from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit
+        from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+        _, cut = _case(case)
+        virt = VirtualCircuit(cut)
+        ref = None
+        if case == "syc_32_5":
+            one = KnitPipeline(virt, device=0, factored=True)
+            ref = one.step().clone()
+            del one
+            torch.cuda.empty_cache()
+        pipe = KnitPipeline(virt, device=0, rank=rank, world=world, mode="slice", factored=True,
+                            group=dist.group.WORLD, data_rank=True)
+        assert pipe.mode == "slice" and pipe.slice_prep == prep and pipe.dev_rank
+        if veto:  # the probe check rejects: the predicated exact slice from the gathered operands
+            pipe.rank_tol = pipe.rank_tol_rel = float("nan")
+        torch.cuda.set_stream(torch.cuda.Stream())
+        pipe.overlap = pipe.overlap_ok()
+        assert pipe.overlap
+        outs, errs = [], []
+        for _ in range(4):
+            out = pipe.step()
+            torch.cuda.synchronize()
+            if ref is not None:
+                errs.append(float((out - ref).abs().max()))
+            else:
+                outs.append(out.cpu().numpy().copy())
+        pipe.sync_stats()
+        q.put((outs, errs, pipe.rank_fallbacks, pipe.last_rank, pipe.rank_incompressible, pipe.overlap_cus))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("case,prep,buffers,veto", [
+    ("hwe_p2", "sharded", 1, False), ("hwe_p2", "sharded", 2, False), ("hwe_p2", "sharded", 1, True),
+    ("cx_8x8", "sharded", 2, False), ("hwe_p2", "replicated", 2, False), ("syc_32_5", "sharded", 1, False),
+    ("syc_32_5", "replicated", 2, False)])
+def test_slice_mode_through_rccl(case, prep, buffers, veto):
+    """Slice mode's collectives on RCCL (world size 1: one GPU per box; RCCL refuses two ranks on one
+    device), pipelined steps on CU-masked streams with one or two output buffers: four steps each equal
+    the oracle (small cases, 1e-12) or the single-GPU step (syc 32 5, all 2^32 entries, 1e-12);
+    a forced rejection and cx_8x8's rank > 8 take the predicated exact slice from the gathered operands."""
+    from oracle import dense
+
+    outs, errs, fallbacks, last_rank, incompressible, cus = _run(_nccl_worker, 1, case, prep, buffers, veto,
+                                                                 timeout=500)
+    assert cus is not None and cus[0] > 0
+    if case == "syc_32_5":
+        assert len(errs) == 4 and max(errs) <= TOL
+        assert fallbacks == 0 and last_rank is not None
+        return
+    ref = dense.run_dense(_case(case)[1])
+    for got in outs:
+        np.testing.assert_allclose(got, ref, atol=TOL, rtol=0)
+    if veto:
+        assert fallbacks == 4 and last_rank is None
+    elif case == "cx_8x8":
+        assert incompressible == 4
+    else:
+        assert fallbacks == 0 and last_rank is not None

@@ -46,10 +46,13 @@ def main():
     ap.add_argument("--xgmi-gbs", type=float, default=0.0, help="modelled per-link xGMI GB/s (0: no delay)")
     ap.add_argument("--coll-lat-us", type=float, default=20.0, help="modelled latency per collective")
     ap.add_argument("--overlap", action="store_true", help="pipelined steps (CU-masked prep stream)")
+    ap.add_argument("--prep", default="auto", choices=["auto", "replicated", "sharded"],
+                    help="slice-mode preparation (QKNIT_SLICE_PREP): replicated = no collective at all")
     ap.add_argument("--cprofile", action="store_true", help="cProfile the timed steps (top host functions to stderr)")
     ap.add_argument("--host-profile", action="store_true",
                     help="host time per pipeline phase (sweep / preparation / launch), to find blocking calls")
     args = ap.parse_args()
+    os.environ["QKNIT_SLICE_PREP"] = args.prep
     import torch
     import torch.distributed as dist
 
@@ -131,7 +134,7 @@ def main():
     # the stand-in all_reduce leaves each rank's partial Grams; factorise the TRUE Grams instead (taken
     # from a one-GPU step) so the simulated rank compresses to the real rank, with the same kernel
     one = KnitPipeline(VirtualCircuit(cut), factored=True)
-    mats = one.operands(one.sweep())
+    mats = one.operands(one.sweep())  # (the replicated preparation factors its own, true, Grams)
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import _mm_nt
 
     A, B = mats[one.order[0]], mats[one.order[-1]]
@@ -142,9 +145,10 @@ def main():
     for world in args.world:
         world_now[0] = world
         pipe = KnitPipeline(VirtualCircuit(cut), factored=True, rank=args.rank, world=world, mode="slice")
-        real = pipe.be.rank_factors
-        pipe.be.rank_factors = lambda GA, GB, real=real: real(*G_true)
-        pipe.rank_tol = float("inf")
+        if pipe.sharded:  # partial Grams from the stand-in all_reduce: factor the true ones, no check
+            real = pipe.be.rank_factors
+            pipe.be.rank_factors = lambda GA, GB, real=real: real(*G_true)
+            pipe.rank_tol = float("inf")
         if args.overlap:
             torch.cuda.set_stream(torch.cuda.Stream())
             pipe.overlap = pipe.overlap_ok()
@@ -198,7 +202,9 @@ def main():
         sweep = sum(s.elapsed_time(e) for s, e in pipe.sweep_events) / max(len(pipe.sweep_events), 1)
         prep = sum(s.elapsed_time(e) for s, e in pipe.prep_events) / max(len(pipe.prep_events), 1)
         M, N, K = pipe.gemm_shape()
-        print(json.dumps({"workload": args.workload, "mode": pipe.mode, "world": world, "rank": args.rank,
+        print(json.dumps({"workload": args.workload, "mode": pipe.mode, "prep": pipe.slice_prep,
+                          "cost_model_ms": pipe.slice_costs, "out_buffers": pipe.out_buffers,
+                          "world": world, "rank": args.rank,
                           "slice": list(pipe.slice), "ms_per_step_no_xgmi": round(ms, 3), "host_ms_per_step": round(host / args.steps * 1e3, 3), "drain_ms": round(drain * 1e3, 3),
                           "sweep_ms": round(sweep, 3), "prep_ms": round(prep, 3), "knit_ms": round(knit, 3),
                           "knit_GBs": round(8 * M * N / (knit * 1e-3) / 1e9, 1), "accepted_rank": pipe.last_rank,
