@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -207,7 +208,9 @@ int qk_knit(qk_ctx* ctx, const qk_knit_plan* plan, const double* const* q, void*
 }  // extern "C"
 
 // ---- qk_knit_lowrank: the benched single-GPU knit (KnitPipeline's device data rank) in one call -----
-// Steps, all on ctx->stream with no host synchronisation (DESIGN.md §2 "Data-rank compression"):
+// Steps, all on ctx->stream with no host synchronisation (DESIGN.md §2 "Data-rank compression"); with at
+// most 80 swept rows per side steps 1, 3 and 4 are the q-space chain (qk_qprep_grams, qk_qprep_compress_check
+// and two transforms X = Wt^T q predicated on k == 0 for step 6), as the benched pipeline takes them:
 //   1. qk_prep_operands   X_A = Wt_A^T q_A, X_B = Wt_B^T q_B, G_A, G_B, U = X_B P^T
 //   2. qk_rank_factors    T_A, T_B, r from the Grams (r = 0: no factorisation of rank <= 8)
 //   3. qk_compress_operands  A'' = T_A X_A, B'' = T_B X_B  (8 rows)
@@ -222,7 +225,15 @@ constexpr int LR_PROBES = 16;
 struct LowrankLayout {
     int64_t xa, xb, g, u, prep, ta, tb, r, a2, b2, e2, k, err, probe, ka, kb, total;
     int64_t prep_bytes, probe_bytes;
+    bool qspace;  // the q-space chain (qk_qprep_*): at most 80 swept rows per side, widths % 256
 };
+
+// as KnitPipeline._qspace_prep / engine.qprep_ok: the chain the benched step takes for these shapes
+bool lowrank_qspace(const qk_lowrank_plan* p) {
+    const int64_t NA = int64_t(1) << __builtin_popcountll(p->mask_a), NB = int64_t(1) << __builtin_popcountll(p->mask_b);
+    const char* env = getenv("QKNIT_QPREP");  // opt-in, as engine.QPREP (the X path measured faster)
+    return env && env[0] == '1' && p->rows_a <= 80 && p->rows_b <= 80 && NA % 512 == 0 && NB % 512 == 0;
+}
 
 int lowrank_layout(qk_ctx* ctx, const qk_lowrank_plan* p, LowrankLayout& L, std::string& why) {
     if (!p || p->terms < 2 || p->terms > 64 || (p->terms & 1) || p->rows_a < 1 || p->rows_b < 1 || !p->wt_a ||
@@ -248,6 +259,10 @@ int lowrank_layout(qk_ctx* ctx, const qk_lowrank_plan* p, LowrankLayout& L, std:
     int64_t prep = 0, probe = 0;
     int rc = qk_prep_workspace_bytes(ctx, NA, NB, &prep);
     if (!rc) rc = qk_probe_workspace_bytes(ctx, NA, &probe);
+    int64_t qprep = 0;
+    if (!rc) rc = qk_qprep_workspace_bytes(ctx, NA, NB, &qprep);
+    L.qspace = lowrank_qspace(p);
+    if (L.qspace && qprep > prep) prep = qprep;
     if (rc) {
         why = "qk_knit_lowrank: workspace queries failed";
         return rc;
@@ -309,13 +324,27 @@ int qk_knit_lowrank(qk_ctx* ctx, const qk_lowrank_plan* p, const double* q_a, co
     double *XA = D(L.xa), *XB = D(L.xb), *G = D(L.g), *U = D(L.u);
     int32_t* r = reinterpret_cast<int32_t*>(ws + L.r);
     int32_t* k = reinterpret_cast<int32_t*>(ws + L.k);
-    rc = qk_prep_operands(ctx, K, (int)p->rows_a, p->wt_a, q_a, NA, NA, XA, (int)p->rows_b, p->wt_b, q_b, NB, NB, XB,
-                          p->probes, G, G + K * K, U, D(L.prep), L.prep_bytes);
-    if (!rc) rc = qk_rank_factors(ctx, K, G, G + K * K, p->lam_tol, p->s_tol, p->s_abs, LR_RMAX, D(L.ta), D(L.tb), r);
-    if (!rc) rc = qk_compress_operands(ctx, K, LR_RMAX, D(L.ta), XA, NA, D(L.a2), D(L.tb), XB, NB, D(L.b2));
-    if (!rc)
-        rc = qk_probe_errors(ctx, K, LR_RMAX, XA, NA, NA, D(L.a2), NA, U, D(L.b2), NB, NB, p->probes, NB, D(L.e2), r,
-                             p->rank_tol, p->rank_tol_rel, k, D(L.err), D(L.probe), L.probe_bytes);
+    if (L.qspace) {
+        // q-space chain (qknit_prep.hip): X is formed only by the predicated transforms of the exact path
+        const int RA = (int)p->rows_a, RB = (int)p->rows_b;
+        rc = qk_qprep_grams(ctx, K, RA, p->wt_a, q_a, NA, NA, RB, p->wt_b, q_b, NB, NB, p->probes, G, G + K * K, U,
+                            D(L.prep), L.prep_bytes);
+        if (!rc) rc = qk_rank_factors(ctx, K, G, G + K * K, p->lam_tol, p->s_tol, p->s_abs, LR_RMAX, D(L.ta), D(L.tb), r);
+        if (!rc)
+            rc = qk_qprep_compress_check(ctx, K, LR_RMAX, RA, p->wt_a, q_a, NA, NA, RB, p->wt_b, q_b, NB, NB, D(L.ta),
+                                         D(L.tb), U, p->probes, D(L.a2), D(L.b2), D(L.e2), r, p->rank_tol,
+                                         p->rank_tol_rel, k, D(L.err), D(L.prep), L.prep_bytes);
+        if (!rc) rc = qk_gemm_keyed_pred(ctx, K, NA, RA, p->wt_a, K, q_a, NA, nullptr, NA, nullptr, 1, XA, 0, k);
+        if (!rc) rc = qk_gemm_keyed_pred(ctx, K, NB, RB, p->wt_b, K, q_b, NB, nullptr, NB, nullptr, 1, XB, 0, k);
+    } else {
+        rc = qk_prep_operands(ctx, K, (int)p->rows_a, p->wt_a, q_a, NA, NA, XA, (int)p->rows_b, p->wt_b, q_b, NB, NB,
+                              XB, p->probes, G, G + K * K, U, D(L.prep), L.prep_bytes);
+        if (!rc) rc = qk_rank_factors(ctx, K, G, G + K * K, p->lam_tol, p->s_tol, p->s_abs, LR_RMAX, D(L.ta), D(L.tb), r);
+        if (!rc) rc = qk_compress_operands(ctx, K, LR_RMAX, D(L.ta), XA, NA, D(L.a2), D(L.tb), XB, NB, D(L.b2));
+        if (!rc)
+            rc = qk_probe_errors(ctx, K, LR_RMAX, XA, NA, NA, D(L.a2), NA, U, D(L.b2), NB, NB, p->probes, NB, D(L.e2),
+                                 r, p->rank_tol, p->rank_tol_rel, k, D(L.err), D(L.probe), L.probe_bytes);
+    }
     if (!rc)
         rc = qk_knit_outer_stream_range(ctx, p->nbits, LR_RMAX, D(L.a2), NA, D(L.b2), NB, p->mask_a, p->mask_b, 0,
                                         int64_t(1) << p->nbits, k, out);

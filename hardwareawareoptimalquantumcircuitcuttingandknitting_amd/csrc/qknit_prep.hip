@@ -646,6 +646,481 @@ __global__ __launch_bounds__(256) void qk_probe_accept_kernel(const double* __re
     }
 }
 
+// ================================================================================================
+// q-space preparation (round 5): the same step without materialising X_s = W_s q_s (W_s = Wt_s^T).
+// Every quantity the chain needs is a product of the swept rows q_s with small matrices:
+//   G_s = X_s X_s^T = W_s (q_s q_s^T) W_s^T       Gq_s = q_s q_s^T  [R_s][R_s]   (qk_qgram_kernel)
+//   U   = X_B P^T   = W_B (q_B P^T)               Pq   = q_B P^T    [R_B][16]
+//   A'' = T_A X_A   = (T_A W_A) q_A = M_A q_A     M_s  = T_s W_s    [rmax][R_s]   (per workgroup, LDS)
+//   R p = X_A^T U   = q_A^T (W_A^T U) = q_A^T Z_A Z_A  = W_A^T U    [R_A][16]
+// so one pass over q gives the Grams (an MFMA SYRK over 128-column tiles, R <= 80 rows), and the
+// compression and the probe check read q once more each: ~0.2 GB of HBM per syc 32 5 step instead of
+// ~0.45 GB, and no 1.1-GFLOP transform. The check still runs on the MATERIALISED compressed operands
+// (V = B'' P^T from the B'' the write reads; d = R p - A''^T V from the A'' it reads), as before.
+constexpr int QG_T = 512;       // threads per qk_qgram workgroup (8 waves)
+// LDS row stride (doubles) of a staged q tile: 146 = 292 dwords = 4 banks past a multiple of 32, so the
+// MFMA operand reads (16 rows x 2 adjacent columns per 16-lane group, ds_read_b128) spread over the banks
+// (2-way at most); a stride that is a multiple of 32 banks put all 16 rows on one bank group (16-way)
+constexpr int QG_LD = PCT + 18;
+constexpr int QG_NB = 5;        // 16-row blocks: R <= 80
+constexpr int QG_RMAX = 16 * QG_NB;
+constexpr int QG_UP = QG_NB * (QG_NB + 1) / 2;       // upper-triangle Gram blocks
+constexpr int QG_PART = (QG_UP + QG_NB) * 256;        // one workgroup's partial sums per side (+ probe blocks)
+
+// Global -> LDS staging of n doubles by nthreads threads, 16 loads of a thread in flight per round (a
+// plain loop waits for each load in turn: ~40 dependent L2 round trips per thread, tens of us)
+template <typename F>
+__device__ __forceinline__ void stage16(const double* __restrict__ src, int n, int nthreads, F store) {
+    for (int e0 = threadIdx.x; e0 < n; e0 += 16 * nthreads) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = e0 + u * nthreads;
+            v[u] = e < n ? src[e] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = e0 + u * nthreads;
+            if (e < n) store(e, v[u]);
+        }
+    }
+}
+
+struct QGramSide {
+    const double* q;  // [R][ldq], columns [0, N)
+    int64_t ldq, N;
+    int R;
+    const double* P;  // probes [16][N] (B side) or nullptr
+};
+
+struct QGramArgs {
+    QGramSide s[2];
+    int split;      // 1: even workgroups take side 0's tiles, odd ones side 1's
+    int slots;      // partial slots per side
+    double* part;   // [2][slots][QG_PART]
+};
+
+__device__ __forceinline__ void qg_block(int b, int& bi, int& bj) {  // upper block b -> (bi <= bj)
+    bi = 0;
+    int n = QG_NB;
+    while (b >= n) {
+        b -= n;
+        ++bi;
+        --n;
+    }
+    bj = bi + b;
+}
+
+__global__ __launch_bounds__(QG_T, 2) void qk_qgram_kernel(QGramArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double qs[];  // [R][QG_LD]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l16 = lane & 15, l4 = lane >> 4;
+    const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+    for (int sd = 0; sd < 2; ++sd) {
+        const QGramSide& S = a.s[sd];
+        const int R = S.R, nb = (R + 15) / 16;
+        // this wave's blocks: slots wave, wave + 8, wave + 16 of [upper blocks | probe blocks]
+        int bi[3], bj[3];
+        bool live[3], probe[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int b = wave + 8 * t;
+            probe[t] = b >= QG_UP;
+            if (!probe[t]) qg_block(b, bi[t], bj[t]);
+            else bi[t] = b - QG_UP, bj[t] = 0;
+            live[t] = b < QG_UP + QG_NB && bi[t] < nb && (probe[t] ? S.P != nullptr : bj[t] < nb);
+        }
+        d4_t acc[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) acc[t] = (d4_t){0, 0, 0, 0};
+        const bool mine = !a.split || (int)(blockIdx.x & 1) == sd;
+        const int64_t t_first = a.split ? (int64_t)(blockIdx.x >> 1) : (int64_t)blockIdx.x;
+        const int64_t t_step = a.split ? (int64_t)(gridDim.x >> 1) : (int64_t)gridDim.x;
+        const int64_t tiles = S.N / PCT;
+        const bool want_p = (live[0] && probe[0]) || (live[1] && probe[1]) || (live[2] && probe[2]);
+        for (int64_t t = mine ? t_first : tiles; t < tiles; t += t_step) {
+            const int64_t c0 = t * PCT;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // the previous tile's readers are done with the LDS
+            for (int r = wave_s; r < R; r += QG_T / 64) prep_glds(S.q + (int64_t)r * S.ldq + c0 + 2 * lane, &qs[r * QG_LD]);
+            // this lane's probe operands (the B operand of a probe block: columns 8 s + 2 l4 and + 1 of P row l16)
+            d2_t pv[PCT / 8];
+            if (want_p) {
+                const double* pp = S.P + (int64_t)l16 * S.N + c0 + 2 * l4;
+#pragma unroll
+                for (int s8 = 0; s8 < PCT / 8; ++s8) pv[s8] = *reinterpret_cast<const d2_t*>(pp + 8 * s8);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // every wave's rows landed
+            // a k-step pair per 16-B read: lane (l16, l4) takes columns 8 s + 2 l4, + 1 (the Gram sums over
+            // columns in any order; A and B operands take the same columns)
+#pragma unroll
+            for (int t3 = 0; t3 < 3; ++t3) {
+                if (!live[t3]) continue;  // wave-uniform
+                const int ra = 16 * bi[t3] + l16, rb = 16 * bj[t3] + l16;
+                const d2_t* xa = reinterpret_cast<const d2_t*>(&qs[(ra < R ? ra : R - 1) * QG_LD + 2 * l4]);
+                const d2_t* xb = reinterpret_cast<const d2_t*>(&qs[(rb < R ? rb : R - 1) * QG_LD + 2 * l4]);
+                const double ma = ra < R ? 1.0 : 0.0, mb = rb < R ? 1.0 : 0.0;
+                d4_t g = acc[t3];
+                if (probe[t3]) {
+#pragma unroll
+                    for (int s8 = 0; s8 < PCT / 8; ++s8) {
+                        const d2_t x = xa[4 * s8];
+                        g = __builtin_amdgcn_mfma_f64_16x16x4f64(ma * x.x, pv[s8].x, g, 0, 0, 0);
+                        g = __builtin_amdgcn_mfma_f64_16x16x4f64(ma * x.y, pv[s8].y, g, 0, 0, 0);
+                    }
+                } else {
+#pragma unroll 4
+                    for (int s8 = 0; s8 < PCT / 8; ++s8) {
+                        const d2_t x = xa[4 * s8], y = xb[4 * s8];
+                        g = __builtin_amdgcn_mfma_f64_16x16x4f64(ma * x.x, mb * y.x, g, 0, 0, 0);
+                        g = __builtin_amdgcn_mfma_f64_16x16x4f64(ma * x.y, mb * y.y, g, 0, 0, 0);
+                    }
+                }
+                acc[t3] = g;
+            }
+        }
+        const int slot = a.split ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
+        if (a.split && !mine) continue;  // a split workgroup owns one side's slot only
+        double* p = a.part + ((int64_t)sd * a.slots + slot) * QG_PART;
+#pragma unroll
+        for (int t3 = 0; t3 < 3; ++t3) {
+            const int b = wave + 8 * t3;
+            if (b >= QG_UP + QG_NB) continue;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) p[b * 256 + (l4 + 4 * rr) * 16 + l16] = live[t3] ? acc[t3][rr] : 0.0;
+        }
+    }
+}
+
+// gq (zero-padded): Gq_A [QG_RMAX][QG_RMAX], Gq_B [QG_RMAX][QG_RMAX], Pq [QG_RMAX][16]; sums over the
+// partial slots in a fixed order (as qk_prep_reduce_kernel), mirrored from the upper blocks
+__global__ __launch_bounds__(64 * PRW) void qk_qgram_reduce_kernel(const double* __restrict__ part, int slots,
+                                                                   double* __restrict__ gq) {
+    __shared__ double acc[PRW][64];
+    const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + lane;  // [0, 2 * QG_PART): side e / QG_PART, entry e % QG_PART
+    const int sd = e / QG_PART, f = e % QG_PART;
+    double s = 0.0;
+    if (sd < 2) {
+        const double* p = part + (int64_t)sd * slots * QG_PART + f;
+        double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int b = grp;
+        for (; b + 31 * PRW < slots; b += 32 * PRW) {
+            double v[32];
+#pragma unroll
+            for (int u = 0; u < 32; ++u) v[u] = p[(int64_t)(b + PRW * u) * QG_PART];
+#pragma unroll
+            for (int u = 0; u < 32; ++u) t[u & 7] += v[u];
+        }
+        for (; b < slots; b += PRW) t[0] += p[(int64_t)b * QG_PART];
+        s = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+    }
+    acc[grp][lane] = s;
+    __syncthreads();
+    if (grp == 0 && sd < 2) {
+        double v[PRW];
+#pragma unroll
+        for (int w = 0; w < PRW; ++w) v[w] = acc[w][lane];
+#pragma unroll
+        for (int h = PRW / 2; h >= 1; h >>= 1)
+#pragma unroll
+            for (int w = 0; w < h; ++w) v[w] += v[w + h];
+        const int blk = f / 256, in = f % 256, r = in / 16, c = in % 16;
+        if (blk < QG_UP) {
+            int bi, bj;
+            qg_block(blk, bi, bj);
+            double* G = gq + (int64_t)sd * QG_RMAX * QG_RMAX;
+            G[(16 * bi + r) * QG_RMAX + 16 * bj + c] = v[0];
+            if (bi != bj) G[(16 * bj + c) * QG_RMAX + 16 * bi + r] = v[0];
+        } else if (sd == 1) {
+            gq[2 * QG_RMAX * QG_RMAX + (16 * (blk - QG_UP) + r) * 16 + c] = v[0];
+        }
+    }
+}
+
+// The projections, 2 x (K / 16) + 1 workgroups: workgroup (s, cb) forms columns 16 cb .. 16 cb + 15 of
+// H_s = Gq_s Wt_s [R][K] and of G_s = Wt_s^T H_s [K][K]; the last one U = Wt_B^T Pq [K][16]. Operands
+// staged in LDS (16 loads in flight per thread), every sum in a fixed order.
+constexpr int QP_CB = PK / 16;  // column blocks per side
+__global__ __launch_bounds__(256) void qk_qproject_kernel(int K, int RA, const double* __restrict__ WtA, int RB,
+                                                          const double* __restrict__ WtB, const double* __restrict__ gq,
+                                                          double* __restrict__ GA, double* __restrict__ GB,
+                                                          double* __restrict__ U) {
+    __shared__ double Wt[QG_RMAX][PK + 1];
+    __shared__ double Gs[QG_RMAX][QG_RMAX + 1];
+    __shared__ double H[QG_RMAX][17];
+    const int tid = threadIdx.x;
+    const int bx = blockIdx.x;
+    const bool proj_u = bx == 2 * QP_CB;
+    const int sd = proj_u ? 1 : bx / QP_CB, cb = bx % QP_CB;
+    if (!proj_u && 16 * cb >= K) return;
+    const int R = sd ? RB : RA;
+    const double* W = sd ? WtB : WtA;
+    stage16(W, R * K, 256, [&](int e, double v) { Wt[e / K][e % K] = v; });
+    if (!proj_u) {
+        const double* Gq = gq + (int64_t)sd * QG_RMAX * QG_RMAX;
+        stage16(Gq, R * QG_RMAX, 256, [&](int e, double v) { Gs[e / QG_RMAX][e % QG_RMAX] = v; });
+    } else {
+        const double* Pq = gq + 2 * QG_RMAX * QG_RMAX;
+        stage16(Pq, R * PNP, 256, [&](int e, double v) { Gs[e / PNP][e % PNP] = v; });
+    }
+    __syncthreads();
+    if (!proj_u) {
+        const int nc = K - 16 * cb < 16 ? K - 16 * cb : 16;
+        for (int e = tid; e < R * 16; e += 256) {  // H[:, 16 cb + y] = Gq Wt[:, 16 cb + y]
+            const int i = e >> 4, y = e & 15;
+            double h = 0.0;
+            if (y < nc)
+                for (int j = 0; j < R; ++j) h = fma(Gs[i][j], Wt[j][16 * cb + y], h);
+            H[i][y] = h;
+        }
+        __syncthreads();
+        double* G = sd ? GB : GA;
+        for (int e = tid; e < K * 16; e += 256) {  // G[x][16 cb + y] = Wt[:, x]^T H[:, y]
+            const int x = e >> 4, y = e & 15;
+            if (y >= nc) continue;
+            double g = 0.0;
+            for (int i = 0; i < R; ++i) g = fma(Wt[i][x], H[i][y], g);
+            G[x * K + 16 * cb + y] = g;
+        }
+    } else {
+        for (int e = tid; e < K * PNP; e += 256) {  // U = Wt_B^T Pq  [K][16]
+            const int x = e / PNP, p = e % PNP;
+            double u = 0.0;
+            for (int i = 0; i < R; ++i) u = fma(Wt[i][x], Gs[i][p], u);
+            U[e] = u;
+        }
+    }
+}
+
+// The staged operands of a compress workgroup: T [8][K] and Wt [R][K] (then M^T [R][8] = (T Wt^T)^T), and
+// on the A side U [K][16] (then Z = Wt U [R][16]); loaded with 16 loads in flight per thread, then formed
+// from LDS. Rows j >= rmax of M are zero.
+struct QcStage {
+    double T[8][PK + 1];
+    double W[QG_RMAX][PK + 1];
+    double U[PK][PNP + 1];
+};
+
+__device__ __forceinline__ void qc_stage(int K, int rmax, int R, const double* __restrict__ T,
+                                         const double* __restrict__ Wt, const double* __restrict__ U, QcStage& st,
+                                         double (*Mt)[8], double (*Zt)[PNP], int nthreads) {
+    stage16(T, rmax * K, nthreads, [&](int e, double v) { st.T[e / K][e % K] = v; });
+    stage16(Wt, R * K, nthreads, [&](int e, double v) { st.W[e / K][e % K] = v; });
+    if (U) stage16(U, K * PNP, nthreads, [&](int e, double v) { st.U[e / PNP][e % PNP] = v; });
+    __syncthreads();
+    for (int e = threadIdx.x; e < R * 8; e += nthreads) {
+        const int i = e >> 3, j = e & 7;
+        double m = 0.0;
+        if (j < rmax)
+            for (int x = 0; x < K; ++x) m = fma(st.T[j][x], st.W[i][x], m);
+        Mt[i][j] = m;
+    }
+    if (U)
+        for (int e = threadIdx.x; e < R * PNP; e += nthreads) {
+            const int i = e / PNP, p = e % PNP;
+            double z = 0.0;
+            for (int x = 0; x < K; ++x) z = fma(st.W[i][x], st.U[x][p], z);
+            Zt[i][p] = z;
+        }
+}
+
+constexpr int QC_CH = 16;            // q rows per load chunk
+constexpr int QV_PART = 8 * PNP;     // one workgroup's V partial [8][16]
+constexpr int QB_T = 256;            // compress_b: threads (4 waves), 2 columns per lane per iteration
+constexpr int QB_COLS = 2 * QB_T;    // columns per iteration
+constexpr int QB_SPAN = 2 * QB_COLS; // columns per workgroup (2 iterations): few V partials to fold
+constexpr int QA_T = 128;            // compress_a: threads (2 waves), 2 columns per lane
+constexpr int QA_COLS = 2 * QA_T;
+
+// B'' = M_B q_B (written) and this workgroup's V partial = B'' P^T over its columns, from the B'' just
+// formed (staged in LDS per iteration; thread t sums (j, p) = (t / 16 % 8, t % 16) over half h = t / 128 of
+// each iteration's columns, the halves added at the end: a fixed order)
+__global__ __launch_bounds__(QB_T) void qk_qcompress_b_kernel(int K, int rmax, int R, const double* __restrict__ T,
+                                                              const double* __restrict__ Wt, const double* __restrict__ q,
+                                                              int64_t ldq, int64_t N, const double* __restrict__ P,
+                                                              double* __restrict__ B2, double* __restrict__ vpart) {
+    __shared__ double Mt[QG_RMAX][8];
+    __shared__ __attribute__((aligned(16))) double b2s[8][QB_COLS];
+    __shared__ __attribute__((aligned(16))) double ps[PNP][QB_COLS];
+    __shared__ QcStage st;
+    __shared__ double vh[QV_PART];
+    const int tid = threadIdx.x;
+    qc_stage(K, rmax, R, T, Wt, nullptr, st, Mt, nullptr, QB_T);
+    __syncthreads();
+    const int vj = (tid >> 4) & 7, vp = tid & 15, vhalf = tid >> 7;
+    double vacc = 0.0;
+    const int nch = (R + QC_CH - 1) / QC_CH;
+    const int64_t s0 = (int64_t)blockIdx.x * QB_SPAN, s1 = s0 + QB_SPAN < N ? s0 + QB_SPAN : N;
+    for (int64_t c0 = s0; c0 < s1; c0 += QB_COLS) {
+        const int64_t c = c0 + 2 * tid;
+        // the iteration's probes (coalesced 16-B rows) in flight with the q loads
+        d2_t pvv[PNP * QB_COLS / 2 / QB_T];
+#pragma unroll
+        for (int u = 0; u < PNP * QB_COLS / 2 / QB_T; ++u) {
+            const int e = tid + u * QB_T, p = e / (QB_COLS / 2), cc = 2 * (e % (QB_COLS / 2));
+            pvv[u] = *reinterpret_cast<const d2_t*>(P + (int64_t)p * N + c0 + cc);
+        }
+        d2_t acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = (d2_t){0.0, 0.0};
+        d2_t buf[2][QC_CH];
+        auto load = [&](int ch, d2_t (&bb)[QC_CH]) {
+#pragma unroll
+            for (int u = 0; u < QC_CH; ++u) {
+                const int i = min(ch * QC_CH + u, R - 1);
+                bb[u] = *reinterpret_cast<const d2_t*>(q + (int64_t)i * ldq + c);
+            }
+        };
+        load(0, buf[0]);
+#pragma unroll
+        for (int ch = 0; ch < QG_RMAX / QC_CH; ++ch) {  // compile-time buffer indices (no scratch)
+            if (ch >= nch) break;
+            if (ch + 1 < nch) load(ch + 1, buf[(ch + 1) & 1]);
+#pragma unroll
+            for (int u = 0; u < QC_CH; ++u) {
+                const int i = ch * QC_CH + u;
+                const double w = i < R ? 1.0 : 0.0;  // rows past R re-read row R - 1: zero weight
+                const d2_t x = buf[ch & 1][u];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const double m = w * Mt[i < R ? i : R - 1][j];
+                    acc[j].x = fma(m, x.x, acc[j].x);
+                    acc[j].y = fma(m, x.y, acc[j].y);
+                }
+            }
+        }
+        __syncthreads();  // the previous iteration's V readers are done with b2s / ps
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j < rmax) *reinterpret_cast<d2_t*>(B2 + (int64_t)j * N + c) = acc[j];
+            *reinterpret_cast<d2_t*>(&b2s[j][2 * tid]) = acc[j];
+        }
+#pragma unroll
+        for (int u = 0; u < PNP * QB_COLS / 2 / QB_T; ++u) {
+            const int e = tid + u * QB_T, p = e / (QB_COLS / 2), cc = 2 * (e % (QB_COLS / 2));
+            *reinterpret_cast<d2_t*>(&ps[p][cc]) = pvv[u];
+        }
+        __syncthreads();
+        const int h0 = vhalf * (QB_COLS / 2);
+        double v0 = 0.0, v1 = 0.0;
+        for (int cc = h0; cc < h0 + QB_COLS / 2; cc += 2) {
+            v0 = fma(b2s[vj][cc], ps[vp][cc], v0);
+            v1 = fma(b2s[vj][cc + 1], ps[vp][cc + 1], v1);
+        }
+        vacc += v0 + v1;
+    }
+    if (vhalf) vh[vj * PNP + vp] = vacc;
+    __syncthreads();
+    if (!vhalf) vpart[(int64_t)blockIdx.x * QV_PART + vj * PNP + vp] = vj < rmax ? vacc + vh[vj * PNP + vp] : 0.0;
+}
+
+// A'' = M_A q_A (written) and the probe check over these columns: ref = q_A^T Z_A (= (R p)_c, Z_A = W_A^T U)
+// and d = ref - A''^T V (V: the fixed-order fold of the B-side partials); epart[wg] = (sum d^2, sum ref^2)
+__global__ __launch_bounds__(QA_T) void qk_qcompress_a_kernel(int K, int rmax, int R, const double* __restrict__ T,
+                                                              const double* __restrict__ Wt, const double* __restrict__ q,
+                                                              int64_t ldq, int64_t N, const double* __restrict__ U,
+                                                              const double* __restrict__ vpart, int gv,
+                                                              double* __restrict__ A2, double* __restrict__ epart) {
+    __shared__ double Mt[QG_RMAX][8];
+    __shared__ double Zt[QG_RMAX][PNP];
+    __shared__ double Vs[8][PNP];
+    __shared__ double red[QA_T / 64][2 * PNP];
+    __shared__ QcStage st;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t c = (int64_t)blockIdx.x * QA_COLS + 2 * tid;
+    {  // V = sum of the gv partials, fixed order: thread t < 128 takes entry t over every partial
+        const int e = tid;
+        double t8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int b = 0;
+        for (; b + 31 < gv; b += 32) {
+            double v[32];
+#pragma unroll
+            for (int u = 0; u < 32; ++u) v[u] = vpart[(int64_t)(b + u) * QV_PART + e];
+#pragma unroll
+            for (int u = 0; u < 32; ++u) t8[u & 7] += v[u];
+        }
+        for (; b < gv; ++b) t8[0] += vpart[(int64_t)b * QV_PART + e];
+        Vs[e / PNP][e % PNP] = ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
+    }
+    qc_stage(K, rmax, R, T, Wt, U, st, Mt, Zt, QA_T);  // Z = Wt_A U  [R][16]
+    __syncthreads();
+    d2_t a2[8], ref[PNP];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a2[j] = (d2_t){0.0, 0.0};
+#pragma unroll
+    for (int p = 0; p < PNP; ++p) ref[p] = (d2_t){0.0, 0.0};
+    d2_t buf[2][QC_CH];
+    auto load = [&](int ch, d2_t (&bb)[QC_CH]) {
+#pragma unroll
+        for (int u = 0; u < QC_CH; ++u) {
+            const int i = min(ch * QC_CH + u, R - 1);
+            bb[u] = *reinterpret_cast<const d2_t*>(q + (int64_t)i * ldq + c);
+        }
+    };
+    const int nch = (R + QC_CH - 1) / QC_CH;
+    load(0, buf[0]);
+#pragma unroll
+    for (int ch = 0; ch < QG_RMAX / QC_CH; ++ch) {  // compile-time buffer indices (no scratch)
+        if (ch >= nch) break;
+        if (ch + 1 < nch) load(ch + 1, buf[(ch + 1) & 1]);
+#pragma unroll
+        for (int u = 0; u < QC_CH; ++u) {
+            const int i = ch * QC_CH + u;
+            const double w = i < R ? 1.0 : 0.0;
+            const int ii = i < R ? i : R - 1;
+            const d2_t x = buf[ch & 1][u];
+            const d2_t xw = (d2_t){w * x.x, w * x.y};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const double m = Mt[ii][j];
+                a2[j].x = fma(m, xw.x, a2[j].x);
+                a2[j].y = fma(m, xw.y, a2[j].y);
+            }
+#pragma unroll
+            for (int p = 0; p < PNP; ++p) {
+                const double z = Zt[ii][p];
+                ref[p].x = fma(z, xw.x, ref[p].x);
+                ref[p].y = fma(z, xw.y, ref[p].y);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (j < rmax) *reinterpret_cast<d2_t*>(A2 + (int64_t)j * N + c) = a2[j];
+    // d = ref - A''^T V per probe, squared; the reference products squared
+    double e2[PNP], f2[PNP];
+#pragma unroll
+    for (int p = 0; p < PNP; ++p) {
+        d2_t d = ref[p];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            d.x = fma(-a2[j].x, Vs[j][p], d.x);
+            d.y = fma(-a2[j].y, Vs[j][p], d.y);
+        }
+        e2[p] = fma(d.x, d.x, d.y * d.y);
+        f2[p] = fma(ref[p].x, ref[p].x, ref[p].y * ref[p].y);
+    }
+#pragma unroll
+    for (int p = 0; p < PNP; ++p) {
+#pragma unroll
+        for (int s = 1; s < 64; s <<= 1) {
+            e2[p] += __shfl_xor(e2[p], s, 64);
+            f2[p] += __shfl_xor(f2[p], s, 64);
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int p = 0; p < PNP; ++p) {
+            red[wave][p] = e2[p];
+            red[wave][PNP + p] = f2[p];
+        }
+    }
+    __syncthreads();
+    if (tid < 2 * PNP) epart[(int64_t)blockIdx.x * PE + tid] = red[0][tid] + red[1][tid];
+}
+
 int probe_grid_d(qk_ctx* ctx, int64_t NA) {
     const int64_t blocks = (NA + 63) / 64;  // 4 waves x 16 columns
     const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 2;
@@ -715,6 +1190,89 @@ int qk_prep_operands(qk_ctx* ctx, int K, int RA, const double* WtA, const double
                        GB, U);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_prep_operands: ") + hipGetErrorString(e)).c_str());
+    return QK_OK;
+}
+
+/* q-space preparation (rows R <= 80 per side): the Grams G_A, G_B [K][K] and U = X_B P^T [K][16] of
+ * X_s = Wt_s^T q_s without forming X (qknit_prep.hip "q-space preparation"). */
+int qk_qprep_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes) {
+    if (!ctx || !bytes) return QK_EARG;
+    const int G = prep_grid(ctx, NA, NB);
+    const int64_t gb = (NB + QB_SPAN - 1) / QB_SPAN, ga = (NA + QA_COLS - 1) / QA_COLS;
+    const int64_t grams = (int64_t)2 * G * QG_PART + 2 * QG_RMAX * QG_RMAX + QG_RMAX * PNP;
+    const int64_t check = gb * QV_PART + ga * PE;
+    *bytes = (grams > check ? grams : check) * (int64_t)sizeof(double);
+    return QK_OK;
+}
+
+int qk_qprep_grams(qk_ctx* ctx, int K, int RA, const double* WtA, const double* qA, int64_t ldqA, int64_t NA, int RB,
+                   const double* WtB, const double* qB, int64_t ldqB, int64_t NB, const double* probes, double* GA,
+                   double* GB, double* U, double* work, int64_t work_bytes) {
+    if (!ctx) return QK_EARG;
+    if (K < 1 || K > PK || RA < 1 || RB < 1 || RA > QG_RMAX || RB > QG_RMAX)
+        return fail(ctx, QK_EARG, "qk_qprep_grams: need 1 <= K <= 64 and 1 <= R <= 80 on both sides");
+    if (((reinterpret_cast<uintptr_t>(qA) | reinterpret_cast<uintptr_t>(qB) | reinterpret_cast<uintptr_t>(probes)) & 15) ||
+        (ldqA & 1) || (ldqB & 1))
+        return fail(ctx, QK_EARG, "qk_qprep_grams: 16-B aligned q / probes and even ldq required");
+    if (NA < PCT || NB < PCT || NA % PCT || NB % PCT || ldqA < NA || ldqB < NB)
+        return fail(ctx, QK_EARG, "qk_qprep_grams: columns must be a positive multiple of 128 (ldq >= N)");
+    if (!WtA || !qA || !WtB || !qB || !probes || !GA || !GB || !U || !work)
+        return fail(ctx, QK_EARG, "qk_qprep_grams: null buffer");
+    int64_t need = 0;
+    qk_qprep_workspace_bytes(ctx, NA, NB, &need);
+    if (work_bytes < need) return fail(ctx, QK_EARG, "qk_qprep_grams: workspace too small (qk_qprep_workspace_bytes)");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_qprep_grams: hipSetDevice");
+    const int G = prep_grid(ctx, NA, NB);
+    QGramArgs args;
+    args.s[0] = QGramSide{qA, ldqA, NA, RA, nullptr};
+    args.s[1] = QGramSide{qB, ldqB, NB, RB, probes};
+    args.split = prep_split(ctx, NA, NB) ? 1 : 0;
+    args.slots = args.split ? G / 2 : G;
+    args.part = work;
+    double* gq = work + (int64_t)2 * G * QG_PART;
+    const size_t lds = (size_t)(RA > RB ? RA : RB) * QG_LD * sizeof(double);
+    hipLaunchKernelGGL(qk_qgram_kernel, dim3(G), dim3(QG_T), lds, ctx->stream, args);
+    hipLaunchKernelGGL(qk_qgram_reduce_kernel, dim3((2 * QG_PART + 63) / 64), dim3(64 * PRW), 0, ctx->stream, work,
+                       args.slots, gq);
+    hipLaunchKernelGGL(qk_qproject_kernel, dim3(2 * QP_CB + 1), dim3(256), 0, ctx->stream, K, RA, WtA, RB, WtB, gq, GA,
+                       GB, U);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_qprep_grams: ") + hipGetErrorString(e)).c_str());
+    return QK_OK;
+}
+
+/* q-space compression + acceptance check: A2 = TA Wt_A^T q_A, B2 = TB Wt_B^T q_B ([rmax][N], rmax <= 8),
+ * e2 / accepted rank exactly as qk_probe_errors over every column of A (U from qk_qprep_grams). */
+int qk_qprep_compress_check(qk_ctx* ctx, int K, int rmax, int RA, const double* WtA, const double* qA, int64_t ldqA,
+                            int64_t NA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB,
+                            const double* TA, const double* TB, const double* U, const double* probes, double* A2,
+                            double* B2, double* e2, const int32_t* r_dev, double tol, double rel_tol, int32_t* k_out,
+                            double* err_out, double* work, int64_t work_bytes) {
+    if (!ctx) return QK_EARG;
+    if (K < 1 || K > PK || rmax < 1 || rmax > 8 || RA < 1 || RB < 1 || RA > QG_RMAX || RB > QG_RMAX)
+        return fail(ctx, QK_EARG, "qk_qprep_compress_check: need 1 <= K <= 64, 1 <= rmax <= 8, 1 <= R <= 80");
+    if (NA % QA_COLS || NB % QB_COLS || NA < QA_COLS || NB < QB_COLS || ldqA < NA || ldqB < NB || (ldqA & 1) || (ldqB & 1))
+        return fail(ctx, QK_EARG, "qk_qprep_compress_check: column counts must be positive multiples of 512");
+    if (((reinterpret_cast<uintptr_t>(qA) | reinterpret_cast<uintptr_t>(qB) | reinterpret_cast<uintptr_t>(A2) |
+          reinterpret_cast<uintptr_t>(B2) | reinterpret_cast<uintptr_t>(probes)) & 15))
+        return fail(ctx, QK_EARG, "qk_qprep_compress_check: 16-B aligned buffers required");
+    if (!WtA || !qA || !WtB || !qB || !TA || !TB || !U || !probes || !A2 || !B2 || !work || (k_out && !r_dev))
+        return fail(ctx, QK_EARG, "qk_qprep_compress_check: null buffer");
+    const int64_t gb = (NB + QB_SPAN - 1) / QB_SPAN, ga = NA / QA_COLS;
+    if (work_bytes < (gb * QV_PART + ga * PE) * (int64_t)sizeof(double))
+        return fail(ctx, QK_EARG, "qk_qprep_compress_check: workspace too small (qk_qprep_workspace_bytes)");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_qprep_compress_check: hipSetDevice");
+    double* vpart = work;
+    double* epart = work + gb * QV_PART;
+    hipLaunchKernelGGL(qk_qcompress_b_kernel, dim3((unsigned)gb), dim3(QB_T), 0, ctx->stream, K, rmax, RB, TB, WtB, qB,
+                       ldqB, NB, probes, B2, vpart);
+    hipLaunchKernelGGL(qk_qcompress_a_kernel, dim3((unsigned)ga), dim3(QA_T), 0, ctx->stream, K, rmax, RA, TA, WtA, qA,
+                       ldqA, NA, U, vpart, (int)gb, A2, epart);
+    hipLaunchKernelGGL(qk_probe_accept_kernel, dim3(1), dim3(256), 0, ctx->stream, epart, (int)ga, r_dev, tol, rel_tol,
+                       e2, k_out, err_out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(ctx, QK_EHIP, (std::string("qk_qprep_compress_check: ") + hipGetErrorString(e)).c_str());
     return QK_OK;
 }
 

@@ -195,6 +195,13 @@ class MappedOut:
         self._leases = [w for w in self._leases if w() is not None] + [weakref.ref(lease)]
         return t
 
+    def mapped_bytes(self) -> int:
+        """Device bytes the mapping holds (whole physical chunks: at least 8 n)."""
+        size = ctypes.c_int64()
+        if self.ptr is None or self.lib.qk_out_mapped_bytes(ctypes.c_void_p(self.ptr), ctypes.byref(size)) != 0:
+            return 8 * self.n
+        return size.value
+
     def in_use(self) -> bool:
         """Whether a tensor handed out by :meth:`tensor` (or a view of it) is still alive."""
         return any(w() is not None for w in self._leases)
@@ -1089,6 +1096,75 @@ def prep_operands(ctx: Context, WtA, qA, WtB, qB, probes, out=None):
                                        G[0].data_ptr(), G[1].data_ptr(), U.data_ptr(), work.data_ptr(),
                                        work.numel() * 8), "qk_prep_operands")
     return XA, XB, G, U
+
+
+QPREP_ROWS = 80  # qk_qprep_*: swept rows per side at most
+# the q-space preparation where it applies (QKNIT_QPREP=1; default the X path). Measured on syc 32 5 and
+# not kept (profiles/r05h_*): its chain took 0.235 ms of kernels against 0.143 for the X
+# path (qk_qgram 53 us, qk_qcompress_b 74, qk_qcompress_a 53, qk_qproject 17, + two predicated transforms
+# for the exact fallback) and 0.94 vs 0.91 ms per 8-rank pipelined step: the transform it removes (~30 us
+# of MFMA) does not pay for the extra launches and the latency-bound VALU compress passes.
+QPREP = os.environ.get("QKNIT_QPREP", "0") == "1"
+_QPREP_WORK: dict = {}
+
+
+def qprep_ok(K: int, RA: int, RB: int, NA: int, NB: int) -> bool:
+    """Whether the q-space preparation (qk_qprep_grams / qk_qprep_compress_check) takes these shapes:
+    K <= 64 terms, at most QPREP_ROWS swept rows per side, column counts multiples of 512."""
+    return (QPREP and 1 <= K <= 64 and 1 <= RA <= QPREP_ROWS and 1 <= RB <= QPREP_ROWS and NA >= 512 and NB >= 512
+            and NA % 512 == 0 and NB % 512 == 0)
+
+
+def _qprep_work(ctx: Context, NA: int, NB: int, dev):
+    T = torch()
+    need = ctypes.c_int64()
+    ctx.check(ctx.lib.qk_qprep_workspace_bytes(ctx.handle, NA, NB, ctypes.byref(need)), "qk_qprep_workspace_bytes")
+    key = (str(dev), T.cuda.current_stream(dev).cuda_stream)
+    work = _QPREP_WORK.get(key)
+    if work is None or work.numel() * 8 < need.value:
+        work = _QPREP_WORK[key] = T.empty(max(need.value // 8, 1), dtype=T.float64, device=dev)
+    return work
+
+
+def qprep_grams(ctx: Context, WtA, qA, WtB, qB, probes):
+    """``qk_qprep_grams``: ``(G, U)`` — the Grams ``[X_A X_A^T, X_B X_B^T]`` ([2, K, K]) and
+    ``U = X_B probes^T`` ([K, 16]) of the light-cone operands ``X = Wt^T q``, without forming X."""
+    T = torch()
+    RA, K = WtA.shape
+    RB, K2 = WtB.shape
+    assert K == K2 and qA.shape[0] == RA and qB.shape[0] == RB and probes.shape == (N_PROBES, qB.shape[1])
+    assert all(t.is_contiguous() for t in (WtA, qA, WtB, qB, probes))
+    NA, NB = qA.shape[1], qB.shape[1]
+    dev = qA.device
+    gu = T.empty(2 * K * K + K * N_PROBES, dtype=T.float64, device=dev)
+    G, U = gu[:2 * K * K].view(2, K, K), gu[2 * K * K:].view(K, N_PROBES)
+    work = _qprep_work(ctx, NA, NB, dev)
+    ctx.check(ctx.lib.qk_qprep_grams(ctx.handle, K, RA, WtA.data_ptr(), qA.data_ptr(), NA, NA, RB, WtB.data_ptr(),
+                                     qB.data_ptr(), NB, NB, probes.data_ptr(), G[0].data_ptr(), G[1].data_ptr(),
+                                     U.data_ptr(), work.data_ptr(), work.numel() * 8), "qk_qprep_grams")
+    return G, U
+
+
+def qprep_compress_check(ctx: Context, WtA, qA, WtB, qB, TA, TB, U, probes, r, tol: float, rel_tol: float):
+    """``qk_qprep_compress_check``: ``(A2, B2, k, err)`` — the compressed operands ``T Wt^T q`` ([rmax, N])
+    and the accepted rank of their probe check (as :func:`probe_errors` with ``r``)."""
+    T = torch()
+    RA, K = WtA.shape
+    RB = WtB.shape[0]
+    rmax = TA.shape[0]
+    NA, NB = qA.shape[1], qB.shape[1]
+    dev = qA.device
+    ab = T.empty(rmax * (NA + NB), dtype=T.float64, device=dev)
+    A2, B2 = ab[:rmax * NA].view(rmax, NA), ab[rmax * NA:].view(rmax, NB)
+    k = T.empty(1, dtype=T.int32, device=dev)
+    err = T.empty(1, dtype=T.float64, device=dev)
+    work = _qprep_work(ctx, NA, NB, dev)
+    ctx.check(ctx.lib.qk_qprep_compress_check(ctx.handle, K, rmax, RA, WtA.data_ptr(), qA.data_ptr(), NA, NA, RB,
+                                              WtB.data_ptr(), qB.data_ptr(), NB, NB, TA.data_ptr(), TB.data_ptr(),
+                                              U.data_ptr(), probes.data_ptr(), A2.data_ptr(), B2.data_ptr(), None,
+                                              r.data_ptr(), tol, rel_tol, k.data_ptr(), err.data_ptr(), work.data_ptr(),
+                                              work.numel() * 8), "qk_qprep_compress_check")
+    return A2, B2, k, err
 
 
 def compress_operands(ctx: Context, TA, XA, TB, XB):

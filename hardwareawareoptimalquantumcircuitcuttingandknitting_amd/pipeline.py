@@ -367,6 +367,12 @@ class HipBackend:
     def npd_pairs(self, keys, vals):
         return engine.npd_pairs(self.ctx, keys, vals)
 
+    def qprep_grams(self, WtA, qA, WtB, qB, probes):
+        return engine.qprep_grams(self.ctx, WtA, qA, WtB, qB, probes)
+
+    def qprep_compress_check(self, WtA, qA, WtB, qB, TA, TB, U, probes, r, tol, rel_tol):
+        return engine.qprep_compress_check(self.ctx, WtA, qA, WtB, qB, TA, TB, U, probes, r, tol, rel_tol)
+
     def select_above(self, dense, accuracy, key_base=0):
         return engine.select_above(self.ctx, dense, accuracy, key_base=key_base)
 
@@ -990,6 +996,19 @@ class KnitPipeline:
                 and self.transforms[ib].shape[0] == qs[ib].shape[0]
                 and engine.prep_ok(K, qs[ia].shape[1], qs[ib].shape[1]))
 
+    def _qspace_prep(self, qs) -> bool:
+        """Whether the data-rank step takes the q-space chain (qk_qprep_grams -> qk_rank_factors ->
+        qk_qprep_compress_check; engine.qprep_ok shapes: at most 80 swept rows per side): a backend with
+        those entries, factored transforms on both sides, no speculative write (it checks beside the write
+        on the X path's operands)."""
+        ia, ib = self.order[0], self.order[-1]
+        if self.spec_write or not hasattr(self.be, "qprep_grams") or self.transforms[ia] is None \
+                or self.transforms[ib] is None:
+            return False
+        WA, WB = self.transforms[ia], self.transforms[ib]
+        return (WA.shape[1] == WB.shape[1] and WA.shape[0] == qs[ia].shape[0] and WB.shape[0] == qs[ib].shape[0]
+                and engine.qprep_ok(WA.shape[1], WA.shape[0], WB.shape[0], qs[ia].shape[1], qs[ib].shape[1]))
+
     def _prep_fused(self, qs, probes):
         """(mats, G, U): light-cone operands of the two sides, their Grams [2, K, K] and the B side
         against the probes [K, 16], from one qk_prep_operands call."""
@@ -1026,6 +1045,24 @@ class KnitPipeline:
         ranks / fallbacks later. The write (``_launch_dev_rank``) runs with the accepted rank and
         the exact contraction is predicated on it being 0."""
         ia, ib = self.order[0], self.order[-1]
+        if self._qspace_prep(qs):
+            # q-space chain (DESIGN §2): Grams and probe products from q q^T / q P^T, the compressed operands
+            # from (T Wt^T) q; X = Wt^T q is formed only by the predicated transforms of the exact path
+            T = self.T
+            x = self._probes(qs[ib].shape[1], qs[ib].device)
+            WA, WB = self.transforms[ia], self.transforms[ib]
+            qA, qB = qs[ia].contiguous(), qs[ib].contiguous()
+            G, U = self.be.qprep_grams(WA, qA, WB, qB, x)
+            TA, TB, r = self.be.rank_factors(G[0], G[1])
+            A2, B2, k_eff, _ = self.be.qprep_compress_check(WA, qA, WB, qB, TA, TB, U, x, r, self.rank_tol,
+                                                            self.rank_tol_rel)
+            self._note_rank(r, k_eff)
+            mats = [None] * len(qs)
+            for i, W, q in ((ia, WA, qA), (ib, WB, qB)):  # written only when the check rejected (k = 0)
+                mats[i] = T.empty((W.shape[1], q.shape[1]), dtype=T.float64, device=q.device)
+                self.be.gemm_keyed(W, q, out=mats[i], strideA=q.shape[1], skip=k_eff)
+            self.last_prep = "qspace"
+            return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
         if self._fused_prep(qs):
             x = self._probes(qs[ib].shape[1], qs[ib].device)
             mats, G, U = self._prep_fused(qs, x)
@@ -1576,6 +1613,7 @@ class KnitPipeline:
         alloc = getattr(self.be, "out_buffer", None)
         if alloc is None:
             self.out_alloc = "backend"
+            self._last_owner = None
             return self.be.zeros((n,), self.T.float64) if zero else self.be.empty((n,), self.T.float64)
         n_sel = len(engine.out_selections)
         out, owner = alloc(n)

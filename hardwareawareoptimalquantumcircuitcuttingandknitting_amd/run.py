@@ -165,19 +165,35 @@ def _build_plan(virt: VirtualCircuit, device: int):
     return KnitPipeline(virt, device=device, factored=True)
 
 
-def cached_plan(virt: VirtualCircuit, device: int = 0):
+def cached_plan(virt: VirtualCircuit, device: int = 0, group=None, backend=None):
     """The compiled plan (``KnitPipeline``) of ``virt`` on ``device`` for the calling thread: built on
     the first call, reused while the circuit's fingerprint is unchanged (LRU of PLAN_CACHE_SIZE;
     plans above PLAN_CACHE_MAX_BYTES of device buffers are rebuilt per call instead).
     Plans are per thread: a plan owns its sweep buffers, and the reference calls
-    ``run_virtual_circuit`` from concurrent threads (``Utilities.py:85-89``)."""
+    ``run_virtual_circuit`` from concurrent threads (``Utilities.py:85-89``). ``group`` (a
+    ``torch.distributed`` process group, or ``"WORLD"``): this rank's plan of the multi-GPU run
+    (:func:`_build_sharded_plan`), keyed by the group as well. ``backend``: a pipeline backend other
+    than the HIP one (CPU tests), part of the key."""
     key = (circuit_fingerprint(virt), device, threading.get_ident())
+    if group is not None:
+        import torch.distributed as dist
+
+        g = None if group == "WORLD" else group
+        gid = "WORLD" if g is None else (getattr(g, "group_name", None) or id(g))
+        key += ("sharded", gid, dist.get_rank(g), dist.get_world_size(g))
+    if backend is not None:
+        key += ("backend", id(backend))
     with _PLANS_LOCK:
         pipe = _PLANS.get(key)
         if pipe is not None:
             _PLANS.move_to_end(key)
+            pipe.plan_reused = True
             return pipe
-    pipe = _build_plan(virt, device)
+    if group is None:
+        pipe = _build_plan(virt, device)
+    else:
+        pipe = _build_sharded_plan(virt, device, None if group == "WORLD" else group, backend)
+    pipe.plan_reused = False
     if pipe.plan_bytes() > PLAN_CACHE_MAX_BYTES:
         return pipe
     with _PLANS_LOCK:
@@ -190,9 +206,15 @@ def cached_plan(virt: VirtualCircuit, device: int = 0):
 
 
 def _plan_held_bytes(pipe) -> int:
-    """Device bytes a cached plan holds: its buffers and the output mapping it keeps for reuse."""
+    """Device bytes a cached plan holds: its buffers, the output mapping it keeps for reuse (the mapped
+    bytes: whole 1-GiB chunks) and the output buffers of pipelined steps, if any."""
+    total = pipe.plan_bytes()
     own = getattr(pipe, "_call_owner", None)
-    return pipe.plan_bytes() + (8 * own.n if own is not None else 0)
+    if own is not None:
+        total += own.mapped_bytes() if hasattr(own, "mapped_bytes") else 8 * own.n
+    for t in getattr(pipe, "_outs", None) or []:
+        total += t.numel() * t.element_size()
+    return total
 
 
 def clear_plan_cache() -> None:
@@ -301,38 +323,88 @@ def run_virtual_circuit_sharded(virt: VirtualCircuit, group=None, *, device: int
     ``run_virtual_circuit(sample=True)``)."""
     import torch.distributed as dist
 
-    from .pipeline import KnitPipeline
-
     T = engine.torch()
-    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    rank = dist.get_rank(group)
     if device is None:
         device = T.cuda.current_device() if backend is None else 0
     log.info("Running virtualizer with %d %s fragments and %d vgates on %d ranks...",
              len(virt.fragment_circuits), tuple(len(f) for f in virt.fragment_circuits),
-             len(virt.vgate_instructions), world)
-    kw = {"backend": backend} if backend is not None else {}
-    pipe = None
-    if engine.factored_ok(virt):  # else (both endpoints of a gate in one fragment): direct knit, reduce mode
-        pipe = KnitPipeline(virt, device=device, factored=True, rank=rank, world=world, group=group, **kw)
-    if pipe is None or pipe.mode != "slice":
-        pipe = KnitPipeline(virt, device=device, factored=False, rank=rank, world=world, group=group,
-                            mode="reduce", **kw)
+             len(virt.vgate_instructions), dist.get_world_size(group))
     on_gpu = backend is None
     now = perf_counter()
-    qs = pipe.sweep()
-    if on_gpu:
-        _sync(device)
-    run_time = perf_counter() - now
-    now = perf_counter()
-    out = pipe.knit(qs)
-    if on_gpu:
-        _sync(device)
+    pipe = cached_plan(virt, device, group="WORLD" if group is None else group, backend=backend)
+    bind = getattr(pipe.be, "bind", None)
+    if bind is not None:
+        bind()
+    # slice mode: the previous call's output mapping again once the caller dropped it (take_out);
+    # reduce mode: a fresh (small) buffer per call, as the reference returns a new result per call
+    pipe.out = pipe.take_out() if pipe.mode == "slice" else None
+    try:
+        qs = pipe.sweep()
+        if on_gpu:
+            _sync(device)
+        run_time = perf_counter() - now
+        now = perf_counter()
+        out = pipe.knit(qs)
+        if on_gpu:
+            _sync(device)
+    finally:
+        pipe.out = None
+    pipe.sync_stats()
     knit_time = perf_counter() - now
     log.info("Knitted in %.2fs.", knit_time)
     if pipe.mode == "slice":
         return out, RunTimeInfo(run_time, knit_time, tuple(pipe.slice))
     n = 1 << pipe.N
     return (out if rank == 0 else None), RunTimeInfo(run_time, knit_time, (0, n) if rank == 0 else (0, 0))
+
+
+def _build_sharded_plan(virt: VirtualCircuit, device: int, group, backend):
+    """This rank's plan of a multi-GPU run: slice mode for a factored two-fragment knit
+    whose fragments partition the output bits, else the direct knit in reduce mode (one RCCL reduce)."""
+    import torch.distributed as dist
+
+    from .pipeline import KnitPipeline
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    kw = {"backend": backend} if backend is not None else {}
+    if engine.factored_ok(virt):  # else (both endpoints of a gate in one fragment): direct knit, reduce mode
+        pipe = KnitPipeline(virt, device=device, factored=True, rank=rank, world=world, group=group, **kw)
+        if pipe.mode == "slice":
+            return pipe
+        del pipe
+    return KnitPipeline(virt, device=device, factored=False, rank=rank, world=world, group=group, mode="reduce", **kw)
+
+
+def _sharded_dict(virt: VirtualCircuit, group, device: int, accuracy: float):
+    """The reference-shaped dict of a multi-GPU run, every rank the whole of it (``run.py:71``): slice
+    mode selects the entries above ``accuracy`` per rank and runs the NPD of the gathered union
+    (``KnitPipeline.knit_dict``, any output width); reduce mode's distribution (at most the instance
+    tensors' size) is all-reduced and truncated as on one GPU."""
+    T = engine.torch()
+    now = perf_counter()
+    pipe = cached_plan(virt, device, group="WORLD" if group is None else group)
+    pipe.be.bind()
+    if pipe.mode == "slice":
+        e0, e1 = T.cuda.Event(enable_timing=True), T.cuda.Event(enable_timing=True)
+        host = perf_counter() - now
+        e0.record()
+        qs = pipe.sweep()
+        e1.record()
+        keys, vals = pipe.knit_dict(accuracy, qs)
+        wall = perf_counter() - now
+        run_time = host + e0.elapsed_time(e1) * 1e-3
+        return keys, vals, RunTimeInfo(run_time, max(wall - run_time, 0.0), tuple(pipe.slice))
+    import torch.distributed as dist
+
+    out, info = run_virtual_circuit_sharded(virt, group, device=device)
+    full = T.zeros(1 << virt.circuit.num_clbits, dtype=T.float64, device=T.device("cuda", device))
+    lo, cnt = info.shard
+    if out is not None and cnt:
+        full[lo:lo + cnt] = out[:cnt]
+    dist.all_reduce(full, group=group)  # shards are disjoint: the sum assembles the distribution
+    keys, vals = engine.nearest_probability_distribution(engine.get_context(device), full, accuracy)
+    return keys, vals, info
 
 
 def _run_reference_truncated(virt: VirtualCircuit, device: int, dense: bool):
@@ -360,8 +432,10 @@ def run_virtual_circuit(virt: VirtualCircuit, shots: int = 20000, *, device: int
                         group=None, truncation: str = "final"):
     """Reference-compatible entry point (``run.py:23-71``). ``group`` (a ``torch.distributed``
     process group, e.g. ``dist.group.WORLD``) runs it on every rank of the group
-    (:func:`run_virtual_circuit_sharded`): ``dense=True`` returns the rank's shard, otherwise every
-    rank returns the whole reference-shaped dict (outputs of at most 24 clbits).
+    (:func:`run_virtual_circuit_sharded`, the plan cached per group like the single-GPU one):
+    ``dense=True`` returns the rank's shard, otherwise every rank returns the whole reference-shaped
+    dict (slice mode: the entries above ``ACCURACY`` selected per rank, gathered, then the NPD — any
+    output width, syc 32 included).
 
     ``truncation``: ``"final"`` (default) knits exactly and applies ``ACCURACY`` once, to the result;
     ``"reference"`` applies it after every operation as the reference's ``QuasiDistr`` dicts do
@@ -378,21 +452,11 @@ def run_virtual_circuit(virt: VirtualCircuit, shots: int = 20000, *, device: int
     if group is not None:
         if sample:
             raise ValueError("multi-GPU runs sweep exact instances (sample=True: single GPU)")
-        out, info = run_virtual_circuit_sharded(virt, group, device=device)
         if dense:
-            return out, info
-        import torch.distributed as dist
-
-        n_bits = virt.circuit.num_clbits
-        if n_bits > 24:
-            raise ValueError(f"a dict of 2^{n_bits} outcomes: use dense=True (each rank gets its shard)")
-        T = engine.torch()
-        full = T.zeros(1 << n_bits, dtype=T.float64, device=T.device("cuda", device))
-        lo, cnt = info.shard
-        if out is not None and cnt:
-            full[lo:lo + cnt] = out[:cnt]
-        dist.all_reduce(full, group=group)  # shards are disjoint: the sum assembles the distribution
-        out = full
+            return run_virtual_circuit_sharded(virt, group, device=device)
+        keys, vals, info = _sharded_dict(virt, group, device, _qd.ACCURACY)
+        log.info("Knitted in %.2fs.", info.knit_time)
+        return dict(zip(keys.tolist(), vals.tolist())), info
     else:
         native = all(isinstance(virt.get_backend(f), MI355XBackend) for f in virt.fragment_circuits if len(f))
         if not dense and factored is None and native and not sample:

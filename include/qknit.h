@@ -340,6 +340,23 @@ int qk_prep_operands(qk_ctx* ctx, int K, int RA, const double* WtA, const double
                      double* XA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB, double* XB,
                      const double* probes, double* GA, double* GB, double* U, double* work, int64_t work_bytes);
 
+/* The same preparation without materialising X_s (round 5, "q-space"; swept rows R_s <= 80 per side):
+ * qk_qprep_grams forms G_A, G_B [K][K] and U [K][16] from Gq_s = q_s q_s^T and Pq = q_B P^T (one MFMA
+ * pass over q, a fixed-order reduction, G_s = Wt_s^T Gq_s Wt_s); qk_qprep_compress_check forms
+ * A2 = (TA Wt_A^T) q_A, B2 = (TB Wt_B^T) q_B ([rmax][N], rmax <= 8) and the acceptance check of
+ * qk_probe_errors over every column of A from the materialised A2 / B2 (e2: 32 doubles or NULL; with
+ * k_out the accepted rank as qk_probe_errors). NA, NB multiples of 512 for the check, 128 for the
+ * Grams. work: qk_qprep_workspace_bytes (covers both calls). All pointers DEVICE. */
+int qk_qprep_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes);
+int qk_qprep_grams(qk_ctx* ctx, int K, int RA, const double* WtA, const double* qA, int64_t ldqA, int64_t NA, int RB,
+                   const double* WtB, const double* qB, int64_t ldqB, int64_t NB, const double* probes, double* GA,
+                   double* GB, double* U, double* work, int64_t work_bytes);
+int qk_qprep_compress_check(qk_ctx* ctx, int K, int rmax, int RA, const double* WtA, const double* qA, int64_t ldqA,
+                            int64_t NA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB,
+                            const double* TA, const double* TB, const double* U, const double* probes, double* A2,
+                            double* B2, double* e2, const int32_t* r_dev, double tol, double rel_tol, int32_t* k_out,
+                            double* err_out, double* work, int64_t work_bytes);
+
 /* A2 = TA X_A ([rmax][NA]), B2 = TB X_B ([rmax][NB]) for [rmax][K] factors (rmax <= 8), one launch. */
 int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, double* A2,
                          const double* TB, const double* XB, int64_t NB, double* B2);

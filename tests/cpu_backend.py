@@ -123,6 +123,21 @@ class CpuBackend:
         XA, XB = WtA.T @ qA, WtB.T @ qB
         return XA, XB, torch.stack([XA @ XA.T, XB @ XB.T]), XB @ probes.T
 
+    def qprep_grams(self, WtA, qA, WtB, qB, probes):
+        """qk_qprep_grams' contract: (G = [XA XA^T, XB XB^T] via Wt^T (q q^T) Wt, U = Wt_B^T (q_B probes^T))."""
+        GA = WtA.T @ (qA @ qA.T) @ WtA
+        GB = WtB.T @ (qB @ qB.T) @ WtB
+        return torch.stack([GA, GB]), WtB.T @ (qB @ probes.T)
+
+    def qprep_compress_check(self, WtA, qA, WtB, qB, TA, TB, U, probes, r, tol, rel_tol):
+        """qk_qprep_compress_check's contract: (A2 = (TA Wt_A^T) q_A, B2, accepted rank, error)."""
+        A2, B2 = ((TA @ WtA.T) @ qA).contiguous(), ((TB @ WtB.T) @ qB).contiguous()
+        ref = qA.T @ (WtA @ U)
+        d = ref - A2.T @ (B2 @ probes.T)
+        e2 = torch.cat([(d * d).sum(dim=0), (ref * ref).sum(dim=0)])
+        k, err = self.probe_accept(e2, r, tol, rel_tol)
+        return A2, B2, k, err
+
     def probe_errors(self, XA, A2, U, B2, probes, r=None, tol=0.0, a2_cols=None, rel_tol=0.0):
         """qk_probe_errors' contract: squared probe errors and squared reference products ([32]) over
         XA's columns (+ accepted rank)."""

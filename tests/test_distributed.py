@@ -24,6 +24,22 @@ def _free_port():
     return p
 
 
+def _collect(procs, q, timeout):
+    """The result rank 0 puts on ``q``; a worker that dies fails the test at once instead of at the
+    timeout."""
+    import queue
+    import time
+
+    t_end = time.time() + timeout
+    while True:
+        try:
+            return q.get(timeout=5)
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"worker exited with {dead}"
+            assert time.time() < t_end, "no result before the timeout"
+
+
 def _case(name):
     import circuits
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import cutting
@@ -93,7 +109,7 @@ def test_multi_rank_pipeline_matches_oracle(case, mode, factored, world):
              for r in range(world)]
     for p in procs:
         p.start()
-    got_mode, res, data_rank, last_rank, terms = q.get(timeout=240)
+    got_mode, res, data_rank, last_rank, terms = _collect(procs, q, 240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -175,7 +191,7 @@ def test_slice_mode_matches_oracle(case, world, data_rank, row_jobs, prep):
              for r in range(world)]
     for p in procs:
         p.start()
-    outs, sl, last_rank, fallbacks, incompressible, dev, last_prep = q.get(timeout=300)
+    outs, sl, last_rank, fallbacks, incompressible, dev, last_prep = _collect(procs, q, 300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -238,7 +254,7 @@ def test_run_virtual_circuit_sharded_api(case, world):
     procs = [ctx.Process(target=_api_worker, args=(r, world, port, case, q)) for r in range(world)]
     for p in procs:
         p.start()
-    full, shards = q.get(timeout=300)
+    full, shards = _collect(procs, q, 300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -268,7 +284,7 @@ def test_slice_mode_one_rank_rejects(prep):
              for r in range(world)]
     for p in procs:
         p.start()
-    outs, sl, last_rank, fallbacks, incompressible, dev, _ = q.get(timeout=300)
+    outs, sl, last_rank, fallbacks, incompressible, dev, _ = _collect(procs, q, 300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0

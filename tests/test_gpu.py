@@ -1116,6 +1116,43 @@ def test_prep_operands_matches_torch(T, K, RA, RB, NA, NB):
             engine.prep_operands(ctx, WtA[:, :5].contiguous(), qA, WtB[:, :5].contiguous(), qB, P)
 
 
+@pytest.mark.parametrize("K,RA,RB,NA,NB,rmax", [(64, 65, 65, 65536, 65536, 8), (64, 80, 17, 1024, 2048, 8),
+                                                (6, 1, 9, 512, 512, 3), (64, 64, 64, 8192, 1536, 1), (32, 33, 48, 512, 4096, 8)])
+def test_qprep_matches_torch(T, K, RA, RB, NA, NB, rmax):
+    """The q-space preparation (qk_qprep_grams, qk_qprep_compress_check: no X = Wt^T q materialised) against
+    torch fp64 on the X path's definitions: the Grams of X, U = X_B P^T, A2 = TA X_A, B2 = TB X_B and the
+    probe check's squared errors (via the accepted rank at a tolerance set around them); deterministic.
+    Shapes: syc 32 5's two sides (65 swept rows each), the 80-row maximum, one row, K < 16, rmax < 8."""
+    ctx = engine.get_context(0)
+    g = T.Generator(device="cuda").manual_seed(K + RA + RB + NA)
+    WtA = T.randn(RA, K, dtype=T.float64, device="cuda", generator=g)
+    WtB = T.randn(RB, K, dtype=T.float64, device="cuda", generator=g)
+    qA = T.randn(RA, NA, dtype=T.float64, device="cuda", generator=g)
+    qB = T.randn(RB, NB, dtype=T.float64, device="cuda", generator=g)
+    P = T.randn(16, NB, dtype=T.float64, device="cuda", generator=g)
+    G, U = engine.qprep_grams(ctx, WtA, qA, WtB, qB, P)
+    T.cuda.synchronize()
+    XA, XB = WtA.T @ qA, WtB.T @ qB
+    close = lambda a, b: float((a - b).abs().max()) <= 1e-13 * max(float(b.abs().max()), 1.0) * 64  # noqa: E731
+    assert close(G[0], XA @ XA.T) and close(G[1], XB @ XB.T)
+    assert close(U, XB @ P.T)
+    TA = T.randn(rmax, K, dtype=T.float64, device="cuda", generator=g)
+    TB = T.randn(rmax, K, dtype=T.float64, device="cuda", generator=g)
+    r = T.tensor([rmax], dtype=T.int32, device="cuda")
+    A2, B2, k, err = engine.qprep_compress_check(ctx, WtA, qA, WtB, qB, TA, TB, U, P, r, 1e300, 0.0)
+    T.cuda.synchronize()
+    assert close(A2, TA @ XA) and close(B2, TB @ XB)
+    d = XA.T @ (XB @ P.T) - A2.T @ (B2 @ P.T)
+    ref_err = float((d * d).sum(dim=0).max().sqrt())
+    assert int(k) == rmax and abs(float(err) - ref_err) <= 1e-9 * ref_err
+    _, _, k2, _ = engine.qprep_compress_check(ctx, WtA, qA, WtB, qB, TA, TB, U, P, r, 0.5 * ref_err, 0.0)
+    assert int(k2) == 0  # the same error against half of it: rejected
+    G2, U2 = engine.qprep_grams(ctx, WtA, qA, WtB, qB, P)
+    A22, B22, _, err2 = engine.qprep_compress_check(ctx, WtA, qA, WtB, qB, TA, TB, U, P, r, 1e300, 0.0)
+    T.cuda.synchronize()
+    assert T.equal(G, G2) and T.equal(U, U2) and T.equal(A2, A22) and T.equal(B2, B22) and T.equal(err, err2)
+
+
 @pytest.mark.parametrize("K,NA,NB,rmax", [(64, 4096, 1001, 8), (24, 129, 8192, 8), (64, 65536, 65536, 8),
                                           (24, 4096, 2048, 3), (17, 2050, 130, 8), (64, 2048, 4096, 1)])
 def test_compress_operands_matches_torch(T, K, NA, NB, rmax):
@@ -1467,14 +1504,19 @@ def test_knit_lowrank_c_entry_matches_oracle(T, case, reject):
 
 
 @pytest.mark.slow
-def test_knit_lowrank_c_entry_syc_32_5_equals_bench_step(T):
+@pytest.mark.parametrize("qprep", [False, True])
+def test_knit_lowrank_c_entry_syc_32_5_equals_bench_step(T, qprep, monkeypatch):
     """The one-call C entry on the headline workload writes the bench step's distribution bit for bit
-    (same kernels, same probes and tolerances, chained in C instead of Python)."""
+    (same kernels, same probes and tolerances, chained in C instead of Python) — with the default
+    X-path preparation and with the opt-in q-space chain (QKNIT_QPREP=1) on both sides."""
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
 
+    monkeypatch.setattr(engine, "QPREP", qprep)
+    monkeypatch.setenv("QKNIT_QPREP", "1" if qprep else "0")
     cut = cutting.config_cut_circuit("syc", 32, 5, 2, "ref")[1]
     pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
     ref = pipe.step()
+    assert pipe.last_prep == ("qspace" if qprep else "fused")
     out, rank = engine.knit_lowrank_c(engine.get_context(0), pipe, pipe.sweep())
     assert 1 <= int(rank.item()) <= 8
     assert _chunked_max_abs_diff(out, ref) == 0.0

@@ -365,3 +365,73 @@ def test_slice_mode_through_rccl(case, prep, buffers, veto):
         assert incompressible == 4
     else:
         assert fallbacks == 0 and last_rank is not None
+
+
+def _dict_worker(rank, world, port, q):
+    """run_virtual_circuit(virt, group=WORLD) on syc 32 5 (2^32 outcomes): the reference-shaped dict on
+    every rank, from the cached sharded plan, against the single-GPU result (computed first on rank 0)."""
+    log = _watchdog(rank, f"dict_syc_32_5_{world}", after=800)
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit
+        from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import run as runmod
+        from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+        torch.cuda.set_device(0)
+        _, cut = _case("syc_32_5")
+        ref = {}
+        if rank == 0:  # the single-GPU dict result (ACCURACY 1e-5) and the thresholded one at 3e-9
+            one = KnitPipeline(VirtualCircuit(cut), device=0, factored=True)
+            for acc in (1e-5, 3e-9):
+                ref[acc] = one.knit_dict(acc)
+            del one
+            torch.cuda.empty_cache()
+            log("single-GPU dicts done")
+        dist.barrier()
+        res, reused, digests = {}, [], []
+        d, info = runmod.run_virtual_circuit(VirtualCircuit(cut), group=dist.group.WORLD)
+        res[1e-5] = d
+        plans = [p for k, p in runmod._PLANS.items() if "sharded" in k]
+        assert len(plans) == 1
+        reused.append(plans[0].plan_reused)
+        log(f"dict 1e-5: {len(d)} entries, prep {plans[0].slice_prep}")
+        d2, _ = runmod.run_virtual_circuit(VirtualCircuit(cut), group=dist.group.WORLD)  # second call: cached
+        reused.append(plans[0].plan_reused)
+        assert d2 == d
+        keys, vals, _ = runmod._sharded_dict(VirtualCircuit(cut), None, 0, 3e-9)
+        log(f"dict 3e-9: {keys.size} entries")
+        digests = torch.tensor([float(keys.size), float(np.sum(keys % 1000003)), float(np.sum(vals))],
+                               dtype=torch.float64)
+        alld = [torch.zeros(3, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(alld, digests)
+        same = all(bool(torch.equal(a, alld[0])) for a in alld)
+        if rank == 0:
+            ok_acc = d == dict(zip(ref[1e-5][0].tolist(), ref[1e-5][1].tolist()))
+            ok_small = bool(np.array_equal(keys, ref[3e-9][0]) and np.array_equal(vals, ref[3e-9][1]))
+            q.put((ok_acc, len(d), ok_small, int(keys.size), reused, same, info.shard))
+        del keys, vals
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(1000)
+def test_syc_32_5_sharded_dict_equals_single_gpu():
+    """BASELINE config 5's reference-shaped result through run_virtual_circuit(virt, group=...) at 8
+    ranks (gloo over the one test GPU): every rank returns the dict; it equals the single-GPU
+    run_virtual_circuit(virt) result at ACCURACY 1e-5 (empty: no outcome of 2^32 reaches it) and, through
+    the same sharded path at 3e-9 (2^28 kept entries: per-rank qk_knit_select of the slice, gathered,
+    qk_npd_pairs), the single-GPU thresholded dict key for key and bit for bit; the second call reuses
+    the cached plan (no re-planning, as the reference's per-call VirtualCircuit rebuild would need)."""
+    ok_acc, n_acc, ok_small, n_small, reused, same, shard = _run(_dict_worker, 8, timeout=950)
+    assert ok_acc and n_acc == 0
+    assert ok_small and n_small > (1 << 27)
+    assert reused == [False, True]
+    assert same
+    assert shard == (0, (1 << 32) // 8)
