@@ -8,8 +8,10 @@
 // mapped at 1-GiB-aligned virtual addresses makes every buffer fast — 4.83-4.86 ms for 24 buffers
 // covering all 280 GB of the device in order, interleaved and permuted (tools/write_probe10) — so the
 // slow mode follows the virtual-to-physical mapping (the translation granularity a hipMalloc block
-// happens to get), not the physical memory. qk_out_alloc maps every large output this way; the
-// pipeline no longer times candidate allocations (round 3's placement search).
+// happens to get), not the physical memory. qk_out_alloc maps every large output this way. Later
+// probes (round 4) found the slow mode in such mappings too once several are made, so
+// for full 2^32 outputs engine.out_buffer still times a new mapping's write rate (qk_out_write_rate)
+// and keeps the fastest of at most three.
 //
 //   qk_out_alloc(ctx, bytes, &ptr)  device memory of at least `bytes`, 1-GiB physical chunks (the
 //                                   last rounded up to the allocation granularity) mapped
@@ -113,7 +115,8 @@ int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr) {
         while (align < want) align <<= 1;
     }
     const size_t n_chunks = (want + chunk - 1) / chunk;
-    OutMapping m{n_chunks * chunk, ctx->device, {}};
+    // the last chunk holds only the rest (a multiple of the granularity): 1.1 GiB maps 1.1, not 2 GiB
+    OutMapping m{want, ctx->device, {}};
     void* va = nullptr;
     e = hipMemAddressReserve(&va, m.bytes, align, nullptr, 0);
     if (e != hipSuccess && free_retired() > 0) e = hipMemAddressReserve(&va, m.bytes, align, nullptr, 0);
@@ -121,9 +124,10 @@ int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr) {
     size_t mapped = 0;
     for (size_t i = 0; i < n_chunks; ++i) {
         hipMemGenericAllocationHandle_t h;
-        e = hipMemCreate(&h, chunk, &prop, 0);
+        const size_t sz = i + 1 < n_chunks ? chunk : want - i * chunk;
+        e = hipMemCreate(&h, sz, &prop, 0);
         if (e == hipSuccess) {
-            e = hipMemMap((char*)va + i * chunk, chunk, 0, h, 0);
+            e = hipMemMap((char*)va + i * chunk, sz, 0, h, 0);
             if (e != hipSuccess) (void)hipMemRelease(h);
         }
         if (e != hipSuccess) {
@@ -133,7 +137,7 @@ int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr) {
             return mem_fail(ctx, QK_EHIP, "qk_out_alloc: hipMemCreate / hipMemMap", e);
         }
         m.chunks.push_back(h);
-        mapped += chunk;
+        mapped += sz;
     }
     hipMemAccessDesc acc = {};
     acc.location = prop.location;

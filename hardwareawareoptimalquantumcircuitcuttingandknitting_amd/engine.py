@@ -21,6 +21,7 @@ import atexit
 import ctypes
 import dataclasses
 import hashlib
+import logging
 import os
 import threading
 from dataclasses import dataclass, field
@@ -417,13 +418,18 @@ def _compile_module(device: int, src: str, names: list):
             arr = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
             h = ctypes.c_void_p()
             path = jit_cache_path(src)
+            loaded = False
             if os.path.exists(path):
+                # a cached object that does not load (truncated, or built by another ROCm / hipcc) is
+                # compiled again and rewritten, not an error
                 img = open(path, "rb").read()
-                ctx.check(ctx.lib.qk_module_load(ctx.handle, img, len(img), arr, len(names), ctypes.byref(h)),
-                          "qk_module_load")
-            else:
+                loaded = ctx.lib.qk_module_load(ctx.handle, img, len(img), arr, len(names), ctypes.byref(h)) == 0
+                if not loaded:
+                    logging.getLogger(__name__).warning("jit cache %s did not load: compiling again", path)
+            if not loaded:
                 ctx.check(ctx.lib.qk_module_compile(ctx.handle, src.encode(), arr, len(names), ctypes.byref(h)),
                           "qk_module_compile")
+                _MODULES[key] = h  # kept (and so freed with the others) even if writing the cache fails
                 _write_cache(ctx, h, path)
             _MODULES[key] = h
         return _MODULES[key]
@@ -443,7 +449,7 @@ def _write_cache(ctx, module, path: str) -> None:
         with open(tmp, "wb") as f:
             f.write(buf.raw[: n.value])
         os.replace(tmp, path)
-    except OSError:
+    except (OSError, _lib.QknitError):
         pass
 
 

@@ -493,8 +493,13 @@ class KnitPipeline:
         # only: rank_sim (modelled xGMI, 20 steps, 4 runs each) 1.56-1.64 vs 1.70-1.80 ms per step at 4
         # ranks, 2.71 vs 2.67-2.74 at 2, 0.94-1.21 vs 0.90-1.13 at 8; 5.00-5.03 vs 4.97-5.06 pipelined
         # on one GPU (profiles/r04bq_*)
+        # Round 5 (replicated slice preparation, rank_sim with modelled xGMI, same box, two rounds each,
+        # profiles/r05i-k_*): 8 ranks 0.92 / 0.90 / 0.82-0.86 ms per step with 1 / 2 / 3 buffers (96
+        # preparation CUs), 0.82-0.85 with 3 buffers and 128 CUs, 1.06-1.18 with 4 (more write streams than
+        # hardware queues: GPU_MAX_HW_QUEUES = 4); 4 ranks 1.38 (2) / 1.37-1.40 (3); 2 ranks 2.58 (2).
+        # Default: 3 buffers from 8 ranks on, 2 at 2-4 ranks, 1 on one GPU
         ob = os.environ.get("QKNIT_OUT_BUFFERS", "")
-        self.out_buffers = int(ob) if ob else (2 if world == 4 else 1)
+        self.out_buffers = int(ob) if ob else (3 if world >= 8 else 2 if world >= 2 else 1)
         self._outs = None
         self._wstreams = None
         self._flip = 0
@@ -1266,7 +1271,9 @@ class KnitPipeline:
         if self._prep_stream is None:
             T = self.T
             dev = self.be.dev.index or 0
-            env = os.environ.get("QKNIT_PREP_CUS", str(self.PREP_CUS))
+            # 8+ ranks: 128 preparation CUs (the replicated sweep + chain on 96 left the write waiting:
+            # 0.82-0.86 vs 0.82-0.85 ms per step with three buffers, profiles/r05j_*), else PREP_CUS
+            env = os.environ.get("QKNIT_PREP_CUS", str(128 if self.world >= 8 else self.PREP_CUS))
             total = engine.device_cu_count(dev)
             if env == "all":
                 # no CU split: both streams may use every CU (their own hardware queues); the write's
@@ -1274,7 +1281,7 @@ class KnitPipeline:
                 # takes the others
                 every = tuple(range(total))
                 self._prep_stream = engine.cu_masked_stream(dev, every)
-                self._write_stream = engine.cu_masked_stream(dev, every, tag=2)
+                self._write_stream = engine.cu_masked_stream(dev, every, tag=100)
                 self._write_cus = every
                 self.overlap_cus = (total, total)
                 self._prep_stream.wait_stream(T.cuda.current_stream())
@@ -1333,15 +1340,16 @@ class KnitPipeline:
         started.record(main)
         self._started = (getattr(self, "_started", []) + [started])[-max(self.out_buffers, 1):]
         if self.out_buffers > 1:
+            nb = self.out_buffers
             if self._outs is None:
-                self._outs = [self.out, self._alloc_out(None)]
+                self._outs = [self.out] + [self._alloc_out(None) for _ in range(nb - 1)]
                 dev = self.be.dev.index or 0
-                self._wstreams = ([W, engine.cu_masked_stream(dev, self._write_cus, tag=1)] if self._write_cus
-                                  else [T.cuda.Stream(device=self.be.dev), T.cuda.Stream(device=self.be.dev)])
+                self._wstreams = ([W] + [engine.cu_masked_stream(dev, self._write_cus, tag=t) for t in range(1, nb)]
+                                  if self._write_cus else [T.cuda.Stream(device=self.be.dev) for _ in range(nb)])
                 for w in self._wstreams:
                     w.wait_stream(main)
             k = self._flip
-            self._flip ^= 1
+            self._flip = (self._flip + 1) % nb
             self.out, W = self._outs[k], self._wstreams[k]
         with T.cuda.stream(S):
             be.bind()

@@ -32,6 +32,7 @@ from .fragment_program import BranchMeasure
 from .knit_plan import deposit_keys
 
 MAX_KEY_BITS = 26
+MAX_MERGE_ITEMS = 1 << 34  # products one merge of a dense vector with a fragment row may form (per label)
 
 
 class DenseQD:
@@ -139,6 +140,13 @@ def knit_reference_truncated(virt, device: int = 0, accuracy: float | None = Non
         row = {lab: int(r) for lab, r in zip(fs.labels, fs.row_of_label())}
         parts.append((J.view(max(n_rows, 1), -1), T.from_numpy(np.ascontiguousarray(keys)).to(dev), row, fs.touches))
     n_keys = 1 << (N + V)
+    # after the first merge the vector is dense over 2^(N + V) keys, and every further merge forms
+    # 2^(N + V) x (the next fragment's 2^(c + m)) products per label: refused when that is beyond
+    # MAX_MERGE_ITEMS (three fragments near the key-bit limit would run for hours)
+    for J, _, _, _ in parts[2:]:
+        if n_keys * J.shape[1] > MAX_MERGE_ITEMS:
+            raise ValueError(f"truncation='reference': merging a third fragment forms 2^{N + V} x {J.shape[1]} "
+                             f"products per label (at most {MAX_MERGE_ITEMS}); use the default truncation")
     one = T.ones(1, dtype=T.float64, device=dev)
     zero_key = T.zeros(1, dtype=T.int64, device=dev)
 

@@ -142,8 +142,8 @@ def _slice_worker(rank, world, port, case, data_rank, q, veto_rank=None, row_job
         pipe = KnitPipeline(VirtualCircuit(cut), rank=rank, world=world, factored=True, backend=CpuBackend(),
                             data_rank=data_rank)
         assert pipe.mode == "slice" and pipe.slice_prep == prep and pipe.sharded == (prep == "sharded")
-        # pipelined steps alternate two output buffers at 4 ranks only (QKNIT_OUT_BUFFERS overrides)
-        assert pipe.out_buffers == (2 if world == 4 else 1)
+        # pipelined steps rotate 2 output buffers at 2-4 ranks, 3 from 8 on (QKNIT_OUT_BUFFERS overrides)
+        assert pipe.out_buffers == (3 if world >= 8 else 2 if world >= 2 else 1)
         if veto_rank == rank:  # this rank's probe check rejects every compression
             pipe.rank_tol = pipe.rank_tol_rel = float("nan")
         outs = []
