@@ -597,6 +597,7 @@ def main():
         # the latency of one full knit (plain steps: nothing of the next step runs under the write), and
         # the sweep / preparation times on the whole chip
         pipelined = {"prep_cus": pipe.overlap_cus[0], "write_cus": pipe.overlap_cus[1],
+                     "out_buffers": pipe.out_buffers,
                      "ms_per_step_pipelined": elapsed / args.steps * 1e3,
                      "pipelined_write_ms": gemm_ms}
         pipe.overlap = False

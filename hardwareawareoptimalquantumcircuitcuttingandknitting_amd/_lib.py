@@ -100,6 +100,9 @@ SIGNATURES = {
     "qk_probe_errors": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64,
                                 c_i64, c_vp, c_i64, c_vp, c_vp, ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp,
                                 c_i64]),
+    "qk_probe_errors_tally": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64,
+                                c_i64, c_vp, c_i64, c_vp, c_vp, ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp,
+                                c_i64, c_vp]),
     "qk_probe_accept": (c_i32, [c_vp, c_vp, ctypes.c_int, c_vp, ctypes.c_double, ctypes.c_double, c_vp, c_vp]),
     "qk_rank_tally": (c_i32, [c_vp, c_vp, c_vp, c_vp]),
     "qk_knit_workspace_bytes": (c_i32, [ctypes.POINTER(QkKnitPlan), ctypes.POINTER(c_i64)]),

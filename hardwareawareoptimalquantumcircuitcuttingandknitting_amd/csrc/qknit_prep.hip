@@ -609,7 +609,8 @@ constexpr int PE = 2 * PNP;
 __global__ __launch_bounds__(256) void qk_probe_accept_kernel(const double* __restrict__ epart, int n,
                                                               const int32_t* __restrict__ r_dev, double tol,
                                                               double rel_tol, double* __restrict__ e2_out,
-                                                              int32_t* __restrict__ k_out, double* __restrict__ err_out) {
+                                                              int32_t* __restrict__ k_out, double* __restrict__ err_out,
+                                                              int64_t* __restrict__ tally = nullptr) {
     __shared__ double acc[256];
     const int tid = threadIdx.x, p = tid % PE;
     // eight independent partial sums (loads in flight together), combined in a fixed order
@@ -642,7 +643,14 @@ __global__ __launch_bounds__(256) void qk_probe_accept_kernel(const double* __re
         const double bound = fmax(tol, rel_tol * sqrt(f));
         const int r = *r_dev;
         if (err_out) *err_out = err;
-        *k_out = (r > 0 && err <= bound) ? r : 0;
+        const int k = (r > 0 && err <= bound) ? r : 0;
+        *k_out = k;
+        if (tally) {  // qk_rank_tally's update, fused (one dependent launch fewer per step)
+            tally[0] += r == 0 ? 1 : 0;
+            tally[1] += (r > 0 && k == 0) ? 1 : 0;
+            tally[2] = k;
+            tally[3] += 1;
+        }
     }
 }
 
@@ -1313,10 +1321,19 @@ int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx,
                     int64_t lda2, const double* U, const double* B2, int64_t ldb2, int64_t NB, const double* probes,
                     int64_t ldp, double* e2, const int32_t* r_dev, double tol, double rel_tol, int32_t* k_out,
                     double* err_out, double* work, int64_t work_bytes) {
+    return qk_probe_errors_tally(ctx, K, rmax, XA, ldx, NA, A2, lda2, U, B2, ldb2, NB, probes, ldp, e2, r_dev, tol,
+                                 rel_tol, k_out, err_out, work, work_bytes, nullptr);
+}
+
+int qk_probe_errors_tally(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx, int64_t NA, const double* A2,
+                          int64_t lda2, const double* U, const double* B2, int64_t ldb2, int64_t NB,
+                          const double* probes, int64_t ldp, double* e2, const int32_t* r_dev, double tol,
+                          double rel_tol, int32_t* k_out, double* err_out, double* work, int64_t work_bytes,
+                          int64_t* tally) {
     if (!ctx) return QK_EARG;
     if (K < 1 || K > PK || rmax < 1 || rmax > 8 || NA < 16 || NA % 16 || NB < 4 || NB % 4)
         return fail(ctx, QK_EARG, "qk_probe_errors: need 1 <= K <= 64, 1 <= rmax <= 8, NA % 16 == 0, NB % 4 == 0");
-    if (!XA || !A2 || !U || !B2 || !probes || !work || (k_out && !r_dev))
+    if (!XA || !A2 || !U || !B2 || !probes || !work || (k_out && !r_dev) || (tally && !k_out))
         return fail(ctx, QK_EARG, "qk_probe_errors: null buffer");
     if (ldx < NA || ldb2 < NB || ldp < NB) return fail(ctx, QK_EARG, "qk_probe_errors: leading dimension");
     const int gd = probe_grid_d(ctx, NA);
@@ -1330,7 +1347,7 @@ int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx,
     hipLaunchKernelGGL(qk_probe_d_kernel, dim3(gd), dim3(256), 0, ctx->stream, K, rmax, XA, ldx, NA, A2, lda2, U, vpart,
                        PV_GRID, epart);
     hipLaunchKernelGGL(qk_probe_accept_kernel, dim3(1), dim3(256), 0, ctx->stream, epart, gd, r_dev, tol, rel_tol, e2,
-                       k_out, err_out);
+                       k_out, err_out, tally);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(ctx, QK_EHIP, (std::string("qk_probe_errors: ") + hipGetErrorString(e)).c_str());
     return QK_OK;

@@ -1190,7 +1190,7 @@ def compress_operands(ctx: Context, TA, XA, TB, XB):
 
 _PROBE_WORK: dict = {}
 def probe_errors(ctx: Context, XA, A2, U, B2, probes, r=None, tol: float = 0.0, a2_cols: tuple | None = None,
-                 rel_tol: float = 0.0):
+                 rel_tol: float = 0.0, tally=None):
     """``qk_probe_errors``: ``e2`` ([32]) = the squared probe errors of the compressed knit ([:16]) and the
     squared reference products ``||R p||^2`` ([16:]) over the columns of ``XA`` ([K, NA]); ``A2`` ([rmax, *])
     holds those columns at ``a2_cols = (offset, count)`` of its rows (default: all). ``U = XB probes^T`` and
@@ -1214,10 +1214,12 @@ def probe_errors(ctx: Context, XA, A2, U, B2, probes, r=None, tol: float = 0.0, 
     e2 = T.empty(2 * N_PROBES, dtype=T.float64, device=dev)
     k = T.empty(1, dtype=T.int32, device=dev) if r is not None else None
     err = T.empty(1, dtype=T.float64, device=dev) if r is not None else None
-    ctx.check(ctx.lib.qk_probe_errors(ctx.handle, K, rmax, XA.data_ptr(), NA, NA, A2.data_ptr() + 8 * off,
-                                      A2.shape[1], U.data_ptr(), B2.data_ptr(), NB, NB, probes.data_ptr(), NB,
-                                      e2.data_ptr(), _ptr(r), tol, rel_tol, _ptr(k), _ptr(err), work.data_ptr(),
-                                      work.numel() * 8), "qk_probe_errors")
+    # tally (device int64[4], with r): the step's data-rank statistics updated by the accept kernel itself
+    assert tally is None or (r is not None and tally.dtype == T.int64 and tally.numel() == 4)
+    ctx.check(ctx.lib.qk_probe_errors_tally(ctx.handle, K, rmax, XA.data_ptr(), NA, NA, A2.data_ptr() + 8 * off,
+                                            A2.shape[1], U.data_ptr(), B2.data_ptr(), NB, NB, probes.data_ptr(), NB,
+                                            e2.data_ptr(), _ptr(r), tol, rel_tol, _ptr(k), _ptr(err), work.data_ptr(),
+                                            work.numel() * 8, _ptr(tally)), "qk_probe_errors_tally")
     return e2, k, err
 
 

@@ -347,8 +347,11 @@ class HipBackend:
     def prep_operands(self, WtA, qA, WtB, qB, probes):
         return engine.prep_operands(self.ctx, WtA, qA, WtB, qB, probes)
 
-    def probe_errors(self, XA, A2, U, B2, probes, r=None, tol=0.0, a2_cols=None, rel_tol=0.0):
-        return engine.probe_errors(self.ctx, XA, A2, U, B2, probes, r=r, tol=tol, a2_cols=a2_cols, rel_tol=rel_tol)
+    fuses_tally = True  # probe_errors(..., tally=) updates the data-rank statistics in its accept kernel
+
+    def probe_errors(self, XA, A2, U, B2, probes, r=None, tol=0.0, a2_cols=None, rel_tol=0.0, tally=None):
+        return engine.probe_errors(self.ctx, XA, A2, U, B2, probes, r=r, tol=tol, a2_cols=a2_cols, rel_tol=rel_tol,
+                                   tally=tally)
 
     def probe_accept(self, e2, r, tol, rel_tol=0.0):
         return engine.probe_accept(self.ctx, e2, r, tol, rel_tol)
@@ -1092,9 +1095,14 @@ class KnitPipeline:
                 for t in (mats[ia], A2, U, B2, x, r, k_eff):
                     t.record_stream(S2)
                 return {"A2": A2, "B2": B2, "k_eff": k_eff, "k_write": r, "check": S2, "mats": mats}
-            _, k_eff, _ = self.be.probe_errors(mats[ia], A2, U, B2, x, r=r, tol=self.rank_tol,
-                                               rel_tol=self.rank_tol_rel)
-            self._note_rank(r, k_eff)
+            if getattr(self.be, "fuses_tally", False):  # the statistics in the accept kernel: one launch fewer
+                _, k_eff, _ = self.be.probe_errors(mats[ia], A2, U, B2, x, r=r, tol=self.rank_tol,
+                                                   rel_tol=self.rank_tol_rel, tally=self._tally_for(r.device))
+                self._pending += 1
+            else:
+                _, k_eff, _ = self.be.probe_errors(mats[ia], A2, U, B2, x, r=r, tol=self.rank_tol,
+                                                   rel_tol=self.rank_tol_rel)
+                self._note_rank(r, k_eff)
             return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
         mats = self.operands(qs)
         self.last_prep = "torch"
@@ -1482,14 +1490,19 @@ class KnitPipeline:
         self.last_kernel = None
         return self.be.gemm_keyed(A, B, keyA=kA, keyB=kB, out=self.out)
 
+    def _tally_for(self, device):
+        """The device tally of the data-rank statistics (_note_rank), created on first use."""
+        if self._tally is None or self._tally.device != device:
+            self._tally = self.T.zeros(4, dtype=self.T.int64, device=device)
+        return self._tally
+
     def _note_rank(self, r, k_eff):
         """A device-rank step's verdict into the device-side tally (no host read: the loop of steps never
         waits for the device; round 4 read every 32 steps back, which drained the pipelined multi-GPU
         queue each time). In slice mode k_eff is MIN-all-reduced in place afterwards, so the tally is
         queued there after that reduction (_prep_slice)."""
         T = self.T
-        if self._tally is None or self._tally.device != k_eff.device:
-            self._tally = T.zeros(4, dtype=T.int64, device=k_eff.device)
+        self._tally_for(k_eff.device)
         tally = getattr(self.be, "rank_tally", None)
         if tally is not None:
             tally(r, k_eff, self._tally)

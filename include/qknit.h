@@ -375,6 +375,13 @@ int qk_probe_errors(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx,
                     int64_t lda2, const double* U, const double* B2, int64_t ldb2, int64_t NB, const double* probes,
                     int64_t ldp, double* e2, const int32_t* r_dev, double tol, double rel_tol, int32_t* k_out,
                     double* err_out, double* work, int64_t work_bytes);
+/* qk_probe_errors with the step's data-rank statistics updated in the same launch (qk_rank_tally's
+ * contract on tally, DEVICE int64[4]; needs k_out): one dependent launch fewer per step. */
+int qk_probe_errors_tally(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx, int64_t NA, const double* A2,
+                          int64_t lda2, const double* U, const double* B2, int64_t ldb2, int64_t NB,
+                          const double* probes, int64_t ldp, double* e2, const int32_t* r_dev, double tol,
+                          double rel_tol, int32_t* k_out, double* err_out, double* work, int64_t work_bytes,
+                          int64_t* tally);
 int qk_probe_accept(qk_ctx* ctx, const double* e2, int n, const int32_t* r_dev, double tol, double rel_tol,
                     int32_t* k_out, double* err_out);
 /* Device-side statistics of a step's data rank (r: factorisation rank, k: accepted rank, both DEVICE

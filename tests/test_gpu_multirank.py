@@ -21,6 +21,26 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 TOL = 1e-12
 
 
+@pytest.fixture(autouse=True)
+def _parent_releases_device_memory():
+    """The ranks are spawned processes sharing the test box's one GPU; the pytest process itself may
+    still hold device memory from earlier in-process GPU tests (cached plans with their 34-GB output
+    mappings, torch's caching allocator). Release it first, so the ranks' allocations never compete
+    with a parent that no longer needs its memory."""
+    import gc
+
+    import torch
+
+    if torch.cuda.is_initialized():
+        from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import run as runmod
+
+        runmod.clear_plan_cache()
+        gc.collect()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    yield
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -54,6 +74,7 @@ def _watchdog(rank, tag, after=100):
 
     os.makedirs(d, exist_ok=True)
     f = open(os.path.join(d, f"{tag}_rank{rank}.tb"), "w")
+    after = float(os.environ.get("QKNIT_TB_AFTER", after))  # a shorter fuse for a hang hunt
     faulthandler.dump_traceback_later(after, exit=True, file=f)
     t0 = time.time()
 
@@ -64,11 +85,11 @@ def _watchdog(rank, tag, after=100):
     return log
 
 
-def _worker(rank, world, port, case, mode, factored, q, overlap=False, veto_rank=None):
+def _worker(rank, world, port, case, mode, factored, q, overlap=False, veto_rank=None, prep="auto"):
     log = _watchdog(rank, f"{case}_{mode}_{world}")
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), QKNIT_SLICE_PREP=prep)
     import torch
     import torch.distributed as dist
 
@@ -180,26 +201,28 @@ def test_multi_rank_hip_matches_oracle(case, mode, factored, world):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("case,world,veto", [("hwe_p2", 8, None), ("cx_8x8", 4, None), ("hwe_p2", 4, 2)])
-def test_multi_rank_hip_overlapped_steps_match_oracle(case, world, veto, monkeypatch):
-    """Pipelined steps (step i+1's sweep, preparation and collectives on a CU-masked stream under step
-    i's write: the multi-GPU bench default) in slice mode on 4-8 ranks sharing the GPU, twice in a
-    row, against the oracle at 1e-12: hwe (compressed every step), cx_8x8 (rank > 8: the exact slice
-    with its all-gathers), and a probe check rejecting on one rank only (every rank takes the exact
-    slice together). Every rank's slice is a qk_out_alloc mapping (QKNIT_OUT_MAPPED_MIN_BYTES=0: small
-    outputs mapped too)."""
+@pytest.mark.parametrize("case,world,veto,prep", [("hwe_p2", 8, None, "auto"), ("cx_8x8", 4, None, "auto"),
+                                                  ("hwe_p2", 4, 2, "sharded"), ("hwe_p2", 4, 0, "replicated")])
+def test_multi_rank_hip_overlapped_steps_match_oracle(case, world, veto, prep, monkeypatch):
+    """Pipelined steps (step i+1's sweep, preparation (and, sharded, its collectives) on a CU-masked
+    stream under step i's write: the multi-GPU bench default) in slice mode on 4-8 ranks sharing the
+    GPU, twice in a row, against the oracle at 1e-12: hwe (compressed every step), cx_8x8 (rank > 8:
+    the exact slice), and a probe check rejecting on one rank only — sharded: every rank takes the exact
+    slice together (MIN all-reduce); replicated: only that rank does (no collective), its slice still
+    exact. Every rank's slice is a qk_out_alloc mapping (QKNIT_OUT_MAPPED_MIN_BYTES=0: small outputs
+    mapped too)."""
     monkeypatch.setenv("QKNIT_OUT_MAPPED_MIN_BYTES", "0")
     sys.path.insert(0, HERE)
     from oracle import dense
 
     got_mode, outs, last_rank, fallbacks, incompressible, dev, kernel, terms = _run(
-        _worker, world, case, "slice", True, timeout=360, overlap=True, veto_rank=veto)
+        _worker, world, case, "slice", True, timeout=360, overlap=True, veto_rank=veto, prep=prep)
     assert got_mode == "slice" and dev
     _, cut = _case(case)
     ref = dense.run_dense(cut)
     for full in outs:
         np.testing.assert_allclose(full, ref, atol=TOL, rtol=0)
-    if veto is not None:
+    if veto is not None:  # rank 0 reports: sharded, the shared verdict; replicated, its own (vetoed) one
         assert fallbacks == 2 and last_rank is None
     elif case == "hwe_p2":
         assert fallbacks == 0 and last_rank is not None
@@ -388,8 +411,10 @@ def _dict_worker(rank, world, port, q):
         ref = {}
         if rank == 0:  # the single-GPU dict result (ACCURACY 1e-5) and the thresholded one at 3e-9
             one = KnitPipeline(VirtualCircuit(cut), device=0, factored=True)
+            log("single-GPU plan built")
             for acc in (1e-5, 3e-9):
                 ref[acc] = one.knit_dict(acc)
+                log(f"single-GPU dict at {acc}: {ref[acc][0].size} entries")
             del one
             torch.cuda.empty_cache()
             log("single-GPU dicts done")
