@@ -318,9 +318,9 @@ __global__ __launch_bounds__(64 * PRW) void qk_prep_reduce_kernel(const double* 
 // before T is staged, and the grid is one 64-column block per workgroup (4 per CU per side: every
 // load of the kernel in flight at once, no second round trip)
 __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const double* __restrict__ TA,
-                                                          const double* __restrict__ XA, int64_t NA,
+                                                          const double* __restrict__ XA, int64_t NA, int64_t lda,
                                                           double* __restrict__ A2, const double* __restrict__ TB,
-                                                          const double* __restrict__ XB, int64_t NB,
+                                                          const double* __restrict__ XB, int64_t NB, int64_t ldb,
                                                           double* __restrict__ B2) {
     __shared__ double T[8][PK];
     __shared__ double part[4][8][64];
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
     const double* Tg = bs ? TB : TA;
     const double* X = bs ? XB : XA;
     double* out = bs ? B2 : A2;
-    const int64_t N = bs ? NB : NA;
+    const int64_t N = bs ? NB : NA, ld = bs ? ldb : lda;
     const int l = threadIdx.x & 63;
     const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR row bases
     auto load = [&](int64_t c0, double (&xv)[16]) {
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
             const int k = 16 * q + u;
-            const double* row = X + (int64_t)k * N;  // uniform
+            const double* row = X + (int64_t)k * ld;  // uniform
             xv[u] = (k < K && c < N) ? row[c] : 0.0;
         }
     };
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
         for (int e = threadIdx.x; e < 8 * 64; e += 256) {
             const int j = e >> 6, cc = e & 63;
             if (j < rmax && c0 + cc < N)
-                out[(int64_t)j * N + c0 + cc] = (part[0][j][cc] + part[1][j][cc]) + (part[2][j][cc] + part[3][j][cc]);
+                out[(int64_t)j * ld + c0 + cc] = (part[0][j][cc] + part[1][j][cc]) + (part[2][j][cc] + part[3][j][cc]);
         }
         __syncthreads();
         if (c0 + (int64_t)gridDim.x * 64 < N) load(c0 + (int64_t)gridDim.x * 64, xv);
@@ -377,15 +377,15 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
 // in flight in 16-row chunks, the next chunk issued before the current one is summed.
 constexpr int PCW = 16;  // rows per load chunk
 __global__ __launch_bounds__(64) void qk_compress_cols_kernel(int K, int rmax, const double* __restrict__ TA,
-                                                              const double* __restrict__ XA, int64_t NA,
+                                                              const double* __restrict__ XA, int64_t NA, int64_t lda,
                                                               double* __restrict__ A2, const double* __restrict__ TB,
-                                                              const double* __restrict__ XB, int64_t NB,
+                                                              const double* __restrict__ XB, int64_t NB, int64_t ldb,
                                                               double* __restrict__ B2) {
     const bool bs = blockIdx.y == 1;
     const double* Tg = bs ? TB : TA;
     const double* X = bs ? XB : XA;
     double* out = bs ? B2 : A2;
-    const int64_t N = bs ? NB : NA;
+    const int64_t N = bs ? NB : NA, ld = bs ? ldb : lda;
     const int64_t c = ((int64_t)blockIdx.x * 64 + threadIdx.x) * 2;
     if ((int64_t)blockIdx.x * 128 >= N) return;  // the whole wave past this side's columns
     const int64_t cl = c < N ? c : N - 2;          // loads of lanes past the end: the last column pair
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(64) void qk_compress_cols_kernel(int K, int rmax, c
 #pragma unroll
         for (int u = 0; u < PCW; ++u) {
             const int k = min(ch * PCW + u, K - 1);
-            b[u] = *reinterpret_cast<const d2_t*>(X + (int64_t)k * N + cl);
+            b[u] = *reinterpret_cast<const d2_t*>(X + (int64_t)k * ld + cl);
         }
     };
     const int nch = (K + PCW - 1) / PCW;
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(64) void qk_compress_cols_kernel(int K, int rmax, c
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-        if (j < rmax) *reinterpret_cast<d2_t*>(out + (int64_t)j * N + c) = acc[j];
+        if (j < rmax) *reinterpret_cast<d2_t*>(out + (int64_t)j * ld + c) = acc[j];
 }
 
 constexpr int PV_GRID = 128;  // workgroups of the V = B'' P^T partial sums (probe_d sums their partials)
@@ -1286,24 +1286,30 @@ int qk_qprep_compress_check(qk_ctx* ctx, int K, int rmax, int RA, const double* 
 
 int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, double* A2,
                          const double* TB, const double* XB, int64_t NB, double* B2) {
+    return qk_compress_operands_ld(ctx, K, rmax, TA, XA, NA, NA, A2, TB, XB, NB, NB, B2);
+}
+
+int qk_compress_operands_ld(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, int64_t lda,
+                            double* A2, const double* TB, const double* XB, int64_t NB, int64_t ldb, double* B2) {
     if (!ctx) return QK_EARG;
     if (K < 1 || K > PK || rmax < 1 || rmax > 8 || NA < 1 || NB < 1)
         return fail(ctx, QK_EARG, "qk_compress_operands: need 1 <= K <= 64, 1 <= rmax <= 8, N >= 1");
+    if (lda < NA || ldb < NB) return fail(ctx, QK_EARG, "qk_compress_operands: leading dimension below the width");
     if (!TA || !XA || !A2 || !TB || !XB || !B2) return fail(ctx, QK_EARG, "qk_compress_operands: null buffer");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_compress_operands: hipSetDevice");
     const int64_t N = NA > NB ? NA : NB;
-    const bool cols = QK_COMPRESS_COLS && NA % 2 == 0 && NB % 2 == 0 &&
+    const bool cols = QK_COMPRESS_COLS && NA % 2 == 0 && NB % 2 == 0 && lda % 2 == 0 && ldb % 2 == 0 &&
                       !((reinterpret_cast<uintptr_t>(XA) | reinterpret_cast<uintptr_t>(XB) |
                          reinterpret_cast<uintptr_t>(A2) | reinterpret_cast<uintptr_t>(B2)) & 15);
     if (cols) {
         hipLaunchKernelGGL(qk_compress_cols_kernel, dim3((unsigned)((N + 127) / 128), 2), dim3(64), 0, ctx->stream, K,
-                           rmax, TA, XA, NA, A2, TB, XB, NB, B2);
+                           rmax, TA, XA, NA, lda, A2, TB, XB, NB, ldb, B2);
     } else {
         int64_t gx = (N + 63) / 64;
         const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 4;  // x 2 sides: up to 8 workgroups per CU
         gx = gx < cap ? gx : cap;
         hipLaunchKernelGGL(qk_compress_kernel, dim3((unsigned)gx, 2), dim3(256), 0, ctx->stream, K, rmax, TA, XA, NA,
-                           A2, TB, XB, NB, B2);
+                           lda, A2, TB, XB, NB, ldb, B2);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)

@@ -215,6 +215,11 @@ hipError_t excl_scan(hipStream_t s, int64_t n, const T* in, T* out, T* partial) 
 }
 
 // ---------------------------------------------------------------- count / select
+constexpr int CNT_U = 8;
+constexpr int64_t CNT_WG_PER_CU = 64;
+constexpr int64_t CNT_MAX_BLOCKS = 16384;
+constexpr int64_t SEL_WG_PER_CU = 16;
+
 template <bool VEC>
 __global__ __launch_bounds__(256) void cnt_kernel(int64_t n, const double* __restrict__ v, double acc,
                                                   unsigned long long* __restrict__ partial) {
@@ -226,14 +231,14 @@ __global__ __launch_bounds__(256) void cnt_kernel(int64_t n, const double* __res
         typedef double vd2 __attribute__((ext_vector_type(2)));
         const vd2* __restrict__ v2 = reinterpret_cast<const vd2*>(v);
         const int64_t n2 = n >> 1;
-        for (; i + 3 * stride < n2; i += 4 * stride) {
-            // nontemporal: the 2^32-entry vector is read once (tools/count_bench.hip: 5.33 ms vs 5.67 at 16
-            // workgroups per CU, 5.50 vs 5.78 at 8)
-            const vd2 a = __builtin_nontemporal_load(v2 + i), b = __builtin_nontemporal_load(v2 + i + stride),
-                      e = __builtin_nontemporal_load(v2 + i + 2 * stride),
-                      f = __builtin_nontemporal_load(v2 + i + 3 * stride);
-            c += (fabs(a.x) > acc) + (fabs(a.y) > acc) + (fabs(b.x) > acc) + (fabs(b.y) > acc) + (fabs(e.x) > acc) +
-                 (fabs(e.y) > acc) + (fabs(f.x) > acc) + (fabs(f.y) > acc);
+        // nontemporal: the 2^32-entry vector is read once; 8 loads in flight per lane at 64 workgroups per CU
+        // (tools/count_bench.hip, one box: 4.95 ms vs 5.17 at 4 loads / 16 per CU and 5.49 at 4 / 4 per CU)
+        for (; i + (CNT_U - 1) * stride < n2; i += CNT_U * stride) {
+            vd2 x[CNT_U];
+#pragma unroll
+            for (int u = 0; u < CNT_U; ++u) x[u] = __builtin_nontemporal_load(v2 + i + u * stride);
+#pragma unroll
+            for (int u = 0; u < CNT_U; ++u) c += (fabs(x[u].x) > acc) + (fabs(x[u].y) > acc);
         }
         for (; i < n2; i += stride) {
             const vd2 a = v2[i];
@@ -282,9 +287,6 @@ __global__ __launch_bounds__(256) void sel_kernel(int64_t n, const double* __res
         }
     }
 }
-
-constexpr int64_t CNT_WG_PER_CU = 16;
-constexpr int64_t CNT_MAX_BLOCKS = 4096;
 
 struct RsPlan {
     int64_t W, chunk;
@@ -375,7 +377,7 @@ hipError_t count_abs_above(hipStream_t s, int cus, int64_t n, const double* v, d
 hipError_t select_abs_above(hipStream_t s, int cus, int64_t n, const double* v, double acc, int64_t* idx,
                             double* vals, unsigned long long* count, int64_t capacity) {
     if (n <= 0) return hipSuccess;
-    int64_t G = (int64_t)(cus > 0 ? cus : 256) * CNT_WG_PER_CU;
+    int64_t G = (int64_t)(cus > 0 ? cus : 256) * SEL_WG_PER_CU;
     const int64_t need = (n + 255) / 256;
     G = G > need ? need : G;
     hipLaunchKernelGGL(sel_kernel, dim3((unsigned)(G < 1 ? 1 : G)), dim3(256), 0, s, n, v, acc, idx, vals, count,

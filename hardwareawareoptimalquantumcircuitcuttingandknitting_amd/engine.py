@@ -1173,18 +1173,34 @@ def qprep_compress_check(ctx: Context, WtA, qA, WtB, qB, TA, TB, U, probes, r, t
     return A2, B2, k, err
 
 
-def compress_operands(ctx: Context, TA, XA, TB, XB):
-    """``qk_compress_operands``: ``(TA XA, TB XB)`` ([rmax, N] each) in one launch."""
+# QKNIT_POISON_UNUSED=1 (tests): the A2 columns a column-range compression leaves unwritten are set to NaN,
+# so a write that read outside its slice's columns shows in the output
+POISON_UNUSED = os.environ.get("QKNIT_POISON_UNUSED", "0") == "1"
+
+
+def compress_operands(ctx: Context, TA, XA, TB, XB, a_cols: tuple | None = None):
+    """``qk_compress_operands``: ``(TA XA, TB XB)`` ([rmax, N] each) in one launch. ``a_cols = (base, n)``:
+    only A2's columns [base, base + n) are computed (the others are left unwritten; qk_compress_operands_ld)."""
     T = torch()
     rmax, K = TA.shape
     assert TB.shape == (rmax, K) and XA.shape[0] == K and XB.shape[0] == K
+    assert XA.is_contiguous() and XB.is_contiguous() and TA.is_contiguous() and TB.is_contiguous()
+    NA, NB = XA.shape[1], XB.shape[1]
     # A2 and B2 share one buffer (A2 first): a multi-GPU rank all-gathers them in one call
-    ab = T.empty(rmax * (XA.shape[1] + XB.shape[1]), dtype=T.float64, device=XA.device)
-    A2 = ab[:rmax * XA.shape[1]].view(rmax, XA.shape[1])
-    B2 = ab[rmax * XA.shape[1]:].view(rmax, XB.shape[1])
-    ctx.check(ctx.lib.qk_compress_operands(ctx.handle, K, rmax, TA.data_ptr(), XA.data_ptr(), XA.shape[1],
-                                           A2.data_ptr(), TB.data_ptr(), XB.data_ptr(), XB.shape[1], B2.data_ptr()),
-              "qk_compress_operands")
+    ab = T.empty(rmax * (NA + NB), dtype=T.float64, device=XA.device)
+    A2 = ab[:rmax * NA].view(rmax, NA)
+    B2 = ab[rmax * NA:].view(rmax, NB)
+    if a_cols is None:
+        ctx.check(ctx.lib.qk_compress_operands(ctx.handle, K, rmax, TA.data_ptr(), XA.data_ptr(), NA, A2.data_ptr(),
+                                               TB.data_ptr(), XB.data_ptr(), NB, B2.data_ptr()), "qk_compress_operands")
+        return A2, B2
+    base, n = a_cols
+    assert 0 <= base and n >= 1 and base + n <= NA
+    if POISON_UNUSED:
+        A2.fill_(float("nan"))
+    ctx.check(ctx.lib.qk_compress_operands_ld(ctx.handle, K, rmax, TA.data_ptr(), XA.data_ptr() + 8 * base, n, NA,
+                                              A2.data_ptr() + 8 * base, TB.data_ptr(), XB.data_ptr(), NB, NB,
+                                              B2.data_ptr()), "qk_compress_operands_ld")
     return A2, B2
 
 
@@ -1201,7 +1217,8 @@ def probe_errors(ctx: Context, XA, A2, U, B2, probes, r=None, tol: float = 0.0, 
     rmax = A2.shape[0]
     NB = B2.shape[1]
     assert U.shape == (K, N_PROBES) and probes.shape == (N_PROBES, NB) and B2.shape[0] == rmax
-    assert all(t.is_contiguous() for t in (XA, A2, U, B2, probes))
+    assert all(t.is_contiguous() for t in (A2, U, B2, probes))
+    assert XA.stride(1) == 1 and XA.stride(0) >= NA  # a column range of a wider operand (rows stride(0) apart)
     off = 0 if a2_cols is None else a2_cols[0]
     assert (a2_cols is None and A2.shape[1] == NA) or (a2_cols is not None and a2_cols[1] == NA)
     dev = XA.device
@@ -1216,7 +1233,7 @@ def probe_errors(ctx: Context, XA, A2, U, B2, probes, r=None, tol: float = 0.0, 
     err = T.empty(1, dtype=T.float64, device=dev) if r is not None else None
     # tally (device int64[4], with r): the step's data-rank statistics updated by the accept kernel itself
     assert tally is None or (r is not None and tally.dtype == T.int64 and tally.numel() == 4)
-    ctx.check(ctx.lib.qk_probe_errors_tally(ctx.handle, K, rmax, XA.data_ptr(), NA, NA, A2.data_ptr() + 8 * off,
+    ctx.check(ctx.lib.qk_probe_errors_tally(ctx.handle, K, rmax, XA.data_ptr(), XA.stride(0), NA, A2.data_ptr() + 8 * off,
                                             A2.shape[1], U.data_ptr(), B2.data_ptr(), NB, NB, probes.data_ptr(), NB,
                                             e2.data_ptr(), _ptr(r), tol, rel_tol, _ptr(k), _ptr(err), work.data_ptr(),
                                             work.numel() * 8, _ptr(tally)), "qk_probe_errors_tally")

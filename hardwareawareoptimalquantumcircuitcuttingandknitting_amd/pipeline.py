@@ -361,8 +361,8 @@ class HipBackend:
         self.ctx.check(self.ctx.lib.qk_rank_tally(self.ctx.handle, r.data_ptr(), k.data_ptr(), acc.data_ptr()),
                        "qk_rank_tally")
 
-    def compress(self, TA, XA, TB, XB):
-        return engine.compress_operands(self.ctx, TA, XA, TB, XB)
+    def compress(self, TA, XA, TB, XB, a_cols=None):
+        return engine.compress_operands(self.ctx, TA, XA, TB, XB, a_cols=a_cols)
 
     def knit_select(self, A, B, clbits_a, clbits_b, nbits, accuracy, k_dev=None):
         return engine.knit_select(self.ctx, A, B, clbits_a, clbits_b, nbits, accuracy, k_dev=k_dev)
@@ -1075,6 +1075,22 @@ class KnitPipeline:
             x = self._probes(qs[ib].shape[1], qs[ib].device)
             mats, G, U = self._prep_fused(qs, x)
             TA, TB, r = self.be.rank_factors(G[0], G[1])
+            a_cols = self._replicated_a_cols()
+            if a_cols is not None:
+                # replicated slice: this rank's output slice reads only A columns [base, base + n) (rows
+                # of R): it compresses those and checks those rows against every probe — its own slice's
+                # verdict, as each rank's rows in the sharded check (the Grams and factors stay whole)
+                base, n = a_cols
+                A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib], a_cols=a_cols)
+                XAc = mats[ia][:, base:base + n]
+                kw = {"tally": self._tally_for(r.device)} if getattr(self.be, "fuses_tally", False) else {}
+                _, k_eff, _ = self.be.probe_errors(XAc, A2, U, B2, x, r=r, tol=self.rank_tol, a2_cols=a_cols,
+                                                   rel_tol=self.rank_tol_rel, **kw)
+                if kw:
+                    self._pending += 1
+                else:
+                    self._note_rank(r, k_eff)
+                return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
             A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib])
             if self.spec_write and getattr(self.be, "dev", None) is not None and self.be.dev.type == "cuda":
                 # speculative write: the write runs at the factored rank r while the probe check runs
@@ -1243,7 +1259,9 @@ class KnitPipeline:
         if not self.sharded:
             # replicated preparation: every rank holds the whole transformed operands, so the exact
             # slice (predicated on the same device verdict, identical on every rank) reads its columns
-            # in place — no collective
+            # in place — no collective. Pipelined steps queue it before the write (_step_overlapped)
+            if p.get("exact_queued"):
+                return self.out
             A, kA, B, kB = self._slice_exact_operands(*self._exact_mats(p))
             be.gemm_keyed(A, B, keyA=kA, keyB=kB, out=self.out, skip=p["k_eff"])
             return self.out
@@ -1371,6 +1389,17 @@ class KnitPipeline:
             if self.out is None:
                 self.out = self._alloc_out(None)
             p = self._prep_step(qs)
+            if self._exact_before_write(W, main):
+                # replicated slice: the predicated exact slice (a no-op unless the check rejected) on the
+                # preparation stream ahead of the write, which then skips (device K = 0). Behind the write
+                # on its own stream it waited ~100 us per step for CU slots under the other buffers'
+                # writes and the buffer's next write waited for it (profiles/r05k_*); here it waits only
+                # for the caller to release the buffer, as the write does
+                if len(self._started) == max(self.out_buffers, 1):
+                    S.wait_event(self._started[0])
+                A, kA, B, kB = self._slice_exact_operands(*self._exact_mats(p))
+                be.gemm_keyed(A, B, keyA=kA, keyB=kB, out=self.out, skip=p["k_eff"])
+                p["exact_queued"] = True
             done = T.cuda.Event(enable_timing=self.record_events)
             done.record(S)
         if self.record_events:
@@ -1390,6 +1419,24 @@ class KnitPipeline:
             main.wait_stream(W)
         be.bind()
         return out
+
+    def _replicated_a_cols(self):
+        """(base, n): the A columns this rank's output slice reads in replicated slice mode, when that is
+        fewer than all of them (syc 32 5 at 8 ranks: 2^13 of 2^16) and the speculative write is off;
+        else None. QKNIT_SLICE_A_COLS=0 compresses and checks all columns (A/B)."""
+        if self.mode != "slice" or self.sharded or self.spec_write or os.environ.get("QKNIT_SLICE_A_COLS") == "0":
+            return None
+        base, n = self._slice_exact_plan()[0][:2]
+        width = 1 << len(self.ops.clbits[self.order[0]])
+        return (base, n) if n < width and n % 16 == 0 else None
+
+    def _exact_before_write(self, W, main) -> bool:
+        """Whether a pipelined step queues its predicated exact contraction on the preparation stream
+        before the write (replicated slice mode, the write on its own stream; QKNIT_EXACT_BEFORE_WRITE=0
+        keeps it behind the write). Valid because the write kernels skip all work at device K = 0,
+        the verdict on which the exact contraction runs."""
+        return (self.mode == "slice" and not self.sharded and W is not main and self.dev_rank
+                and os.environ.get("QKNIT_EXACT_BEFORE_WRITE", "1") != "0")
 
     def _group_rank0(self) -> int:
         import torch.distributed as dist

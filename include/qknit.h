@@ -360,6 +360,11 @@ int qk_qprep_compress_check(qk_ctx* ctx, int K, int rmax, int RA, const double* 
 /* A2 = TA X_A ([rmax][NA]), B2 = TB X_B ([rmax][NB]) for [rmax][K] factors (rmax <= 8), one launch. */
 int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, double* A2,
                          const double* TB, const double* XB, int64_t NB, double* B2);
+/* The same over column ranges of wider operands: X_A / A2 rows lda apart, X_B / B2 rows ldb apart (a
+ * replicated multi-GPU rank compresses only the A columns its output slice reads; the pointers are offset
+ * to the first column). */
+int qk_compress_operands_ld(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, int64_t lda,
+                            double* A2, const double* TB, const double* XB, int64_t NB, int64_t ldb, double* B2);
 
 /* Acceptance check of a compressed knit on the real operands (the probe products of the torch form,
  * not materialised): e2[p] = ||(X_A^T X_B - A2^T B2) P_p||^2 and e2[16 + p] = ||X_A^T X_B P_p||^2

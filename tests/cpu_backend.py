@@ -157,8 +157,15 @@ class CpuBackend:
         rv = int(r.reshape(-1)[0])
         return torch.tensor([rv if rv > 0 and err <= bound else 0], dtype=torch.int32), torch.tensor([err])
 
-    def compress(self, TA, XA, TB, XB):
-        return (TA @ XA).contiguous(), (TB @ XB).contiguous()
+    def compress(self, TA, XA, TB, XB, a_cols=None):
+        """qk_compress_operands' contract; a_cols = (base, n): only A2's columns [base, base + n) are
+        written, the others hold NaN (a read outside them shows in the output)."""
+        if a_cols is None:
+            return (TA @ XA).contiguous(), (TB @ XB).contiguous()
+        base, n = a_cols
+        A2 = torch.full((TA.shape[0], XA.shape[1]), float("nan"), dtype=XA.dtype)
+        A2[:, base:base + n] = TA @ XA[:, base:base + n]
+        return A2, (TB @ XB).contiguous()
 
     def khatri_rao(self, A, B):
         K = A.shape[0]

@@ -155,7 +155,7 @@ def _slice_worker(rank, world, port, case, data_rank, q, veto_rank=None, row_job
         pipe.sync_stats()
         if rank == 0:
             q.put((outs, pipe.slice, pipe.last_rank, pipe.rank_fallbacks, pipe.rank_incompressible, pipe.dev_rank,
-                   pipe.last_prep))
+                   pipe.last_prep, pipe._replicated_a_cols()))
     finally:
         dist.destroy_process_group()
 
@@ -191,10 +191,14 @@ def test_slice_mode_matches_oracle(case, world, data_rank, row_jobs, prep):
              for r in range(world)]
     for p in procs:
         p.start()
-    outs, sl, last_rank, fallbacks, incompressible, dev, last_prep = _collect(procs, q, 300)
+    outs, sl, last_rank, fallbacks, incompressible, dev, last_prep, a_cols = _collect(procs, q, 300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    # replicated: rank 0 compresses and checks only the A columns its slice reads (the others NaN in the
+    # CPU backend's A2, so a read outside them would show below)
+    if prep == "replicated" and case == "hwe_p2":
+        assert a_cols is not None and a_cols[1] < 1 << 8
     sys.path.insert(0, HERE)
     _, cut = _slice_case(case)
     ref = dense.run_dense(cut)
@@ -284,7 +288,7 @@ def test_slice_mode_one_rank_rejects(prep):
              for r in range(world)]
     for p in procs:
         p.start()
-    outs, sl, last_rank, fallbacks, incompressible, dev, _ = _collect(procs, q, 300)
+    outs, sl, last_rank, fallbacks, incompressible, dev, _, _ = _collect(procs, q, 300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0

@@ -89,7 +89,7 @@ def _worker(rank, world, port, case, mode, factored, q, overlap=False, veto_rank
     log = _watchdog(rank, f"{case}_{mode}_{world}")
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), QKNIT_SLICE_PREP=prep)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), QKNIT_SLICE_PREP=prep, QKNIT_POISON_UNUSED="1")
     import torch
     import torch.distributed as dist
 
@@ -234,7 +234,7 @@ def _syc_worker(rank, world, port, q, overlap=False, prep="auto"):
     log = _watchdog(rank, f"syc_32_5_{world}", after=700)
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), QKNIT_SLICE_PREP=prep)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), QKNIT_SLICE_PREP=prep, QKNIT_POISON_UNUSED="1")
     import torch
     import torch.distributed as dist
 
@@ -319,7 +319,7 @@ def _nccl_worker(rank, world, port, case, prep, buffers, veto, q):
     all_gather) runs on nccl beside the masked write streams."""
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), QKNIT_SLICE_PREP=prep,
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), QKNIT_SLICE_PREP=prep, QKNIT_POISON_UNUSED="1",
                       QKNIT_OUT_BUFFERS=str(buffers))
     import torch
     import torch.distributed as dist
@@ -364,12 +364,13 @@ def _nccl_worker(rank, world, port, case, prep, buffers, veto, q):
 @pytest.mark.parametrize("case,prep,buffers,veto", [
     ("hwe_p2", "sharded", 1, False), ("hwe_p2", "sharded", 2, False), ("hwe_p2", "sharded", 1, True),
     ("cx_8x8", "sharded", 2, False), ("hwe_p2", "replicated", 2, False), ("syc_32_5", "sharded", 1, False),
-    ("syc_32_5", "replicated", 2, False)])
+    ("syc_32_5", "replicated", 2, False), ("hwe_p2", "replicated", 3, True)])
 def test_slice_mode_through_rccl(case, prep, buffers, veto):
     """Slice mode's collectives on RCCL (world size 1: one GPU per box; RCCL refuses two ranks on one
     device), pipelined steps on CU-masked streams with one or two output buffers: four steps each equal
     the oracle (small cases, 1e-12) or the single-GPU step (syc 32 5, all 2^32 entries, 1e-12);
-    a forced rejection and cx_8x8's rank > 8 take the predicated exact slice from the gathered operands."""
+    a forced rejection and cx_8x8's rank > 8 take the predicated exact slice from the gathered operands
+    (replicated, three buffers: queued on the preparation stream ahead of the skipped write)."""
     from oracle import dense
 
     outs, errs, fallbacks, last_rank, incompressible, cus = _run(_nccl_worker, 1, case, prep, buffers, veto,

@@ -96,15 +96,24 @@ int main(int argc, char** argv) {
         fflush(stdout);
     };
     const d2_t* vv = reinterpret_cast<const d2_t*>(v);
-    for (int wg : {4, 8, 16}) {
+    const bool nt_only = argc > 2 && atoi(argv[2]) == 1;  // round 2: nontemporal variants only, wider grids
+    for (int wg : {4, 8, 16, 32, 64}) {
         const int G = cus * wg;
         char nm[64];
-        snprintf(nm, sizeof nm, "stride U4 wg%d", wg);
-        run(nm, [&] { hipLaunchKernelGGL((count_stride<4, false>), dim3(G), dim3(256), 0, 0, n2, vv, 1e-5, cnt); });
-        snprintf(nm, sizeof nm, "stride U8 wg%d", wg);
-        run(nm, [&] { hipLaunchKernelGGL((count_stride<8, false>), dim3(G), dim3(256), 0, 0, n2, vv, 1e-5, cnt); });
+        if (!nt_only && wg <= 16) {
+            snprintf(nm, sizeof nm, "stride U4 wg%d", wg);
+            run(nm, [&] { hipLaunchKernelGGL((count_stride<4, false>), dim3(G), dim3(256), 0, 0, n2, vv, 1e-5, cnt); });
+            snprintf(nm, sizeof nm, "stride U8 wg%d", wg);
+            run(nm, [&] { hipLaunchKernelGGL((count_stride<8, false>), dim3(G), dim3(256), 0, 0, n2, vv, 1e-5, cnt); });
+        }
         snprintf(nm, sizeof nm, "stride U4 nt wg%d", wg);
         run(nm, [&] { hipLaunchKernelGGL((count_stride<4, true>), dim3(G), dim3(256), 0, 0, n2, vv, 1e-5, cnt); });
+        if (nt_only) {
+            snprintf(nm, sizeof nm, "stride U2 nt wg%d", wg);
+            run(nm, [&] { hipLaunchKernelGGL((count_stride<2, true>), dim3(G), dim3(256), 0, 0, n2, vv, 1e-5, cnt); });
+            snprintf(nm, sizeof nm, "stride U8 nt wg%d", wg);
+            run(nm, [&] { hipLaunchKernelGGL((count_stride<8, true>), dim3(G), dim3(256), 0, 0, n2, vv, 1e-5, cnt); });
+        }
     }
     for (int64_t ck : {int64_t(1) << 12, int64_t(1) << 14, int64_t(1) << 16}) {  // d2 elements per workgroup
         char nm[64];

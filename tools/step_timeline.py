@@ -6,7 +6,7 @@
 Takes the write kernel launches (qk_knit_outer_*) as step markers and prints, for the step
 interval in the middle of the run, every kernel that started in it: its stream, start
 offset from the interval start, duration, and the gaps on each stream (time no kernel of that
-stream ran). Used for the 8-rank rank_sim step."""
+stream ran); then the time with 0, 1, 2, ... writes in flight over the middle half of the run. Used for the 8-rank rank_sim step."""
 import csv
 import sys
 from collections import defaultdict
@@ -30,6 +30,19 @@ def main():
             print(f"  stream {st:>3} q{q:>2} +{(s - t0) / 1e3:8.1f} us {(e - s) / 1e3:8.1f} us  {name[:90]}")
     for st, b in sorted(busy.items()):
         print(f"stream {st}: kernels {b:.1f} us of {(t1 - t0) / 1e3:.1f}")
+    # write concurrency over the middle half of the run (write launches n/4 .. 3n/4): the time with
+    # 0, 1, 2, ... write kernels in flight
+    a, b = writes[len(writes) // 4][0], writes[3 * len(writes) // 4][0]
+    ev = sorted([(max(s, a), 1) for s, e, *_ in writes if e > a and s < b] +
+                [(min(e, b), -1) for s, e, *_ in writes if e > a and s < b])
+    depth, last, hist = 0, a, defaultdict(float)
+    for t, d in ev:
+        hist[depth] += (t - last) / 1e3
+        depth, last = depth + d, t
+    hist[depth] += (b - last) / 1e3
+    n_w = 3 * len(writes) // 4 - len(writes) // 4
+    print(f"write concurrency over {n_w} writes ({(b - a) / 1e3:.1f} us, {(b - a) / 1e3 / n_w:.1f} us per write): " +
+          ", ".join(f"{k} in flight {v:.1f} us" for k, v in sorted(hist.items())))
 
 
 if __name__ == "__main__":
