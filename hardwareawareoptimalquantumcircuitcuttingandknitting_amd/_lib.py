@@ -88,6 +88,9 @@ SIGNATURES = {
     "qk_prep_workspace_bytes": (c_i32, [c_vp, c_i64, c_i64, ctypes.POINTER(c_i64)]),
     "qk_prep_operands": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_i64, c_vp, ctypes.c_int,
                                  c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64]),
+    "qk_prep_operands_cols": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_i64, c_vp, ctypes.c_int,
+                                      c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                      c_i64]),
     "qk_qprep_workspace_bytes": (c_i32, [c_vp, c_i64, c_i64, ctypes.POINTER(c_i64)]),
     "qk_qprep_grams": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_i64, ctypes.c_int, c_vp, c_vp,
                                c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64]),

@@ -38,7 +38,14 @@ constexpr int PCT = 128;        // columns per tile (8 waves x 16)
 constexpr int PNP = 16;         // probes
 constexpr int PTH = 512;        // threads per workgroup
 constexpr int XLD = PCT + 2;    // X tile row stride (doubles): a Gram k-step's 16 rows x 2 columns hit distinct banks
-constexpr int PPART = PK * PK + PK * PNP;  // doubles of one workgroup's partial sums per side
+// One workgroup's partial sums: the Gram's 10 upper 16 x 16 blocks (bi <= bj; the reduction mirrors the
+// lower ones), and on the B side the probe products after them. Round 4 stored all 16 blocks and a zero
+// U on the A side: 80 KiB per workgroup, 41 MiB per syc 32 5 step written and read back, now 48 KiB
+constexpr int PG_BLK = 10;
+constexpr int PPG = PG_BLK * 256;
+constexpr int PPA = PPG;              // doubles of one A-side partial
+constexpr int PPB = PPG + PK * PNP;   // doubles of one B-side partial
+__host__ __device__ constexpr int prep_tri(int bi, int bj) { return bi * 4 - bi * (bi - 1) / 2 + (bj - bi); }
 
 struct PrepSide {
     const double* Wt;  // [R][K]
@@ -48,13 +55,14 @@ struct PrepSide {
     int R;
     double* X;         // [K][N]
     const double* P;   // probes [16][N] (B side) or nullptr
+    int64_t x_lo, x_hi;  // X is stored only for the column tiles in [x_lo, x_hi) (Grams: every column)
 };
 
 struct PrepArgs {
     PrepSide s[2];
     int K;
     int split;     // 1: even workgroups take side 0's tiles, odd ones side 1's (prep_grid)
-    double* part;  // [2][gridDim.x][PPART]
+    double* part;  // [gridDim.x][PPA] (A side), then [gridDim.x][PPB] (B side)
 };
 
 // Stage ring of the transform phase: PRS instance rows of q (128 columns) and of Wt per stage, moved
@@ -236,7 +244,7 @@ __global__ __launch_bounds__(PTH, 2 * QK_PREP_WG_PER_CU) void qk_prep_operands_k
             // wave-instruction (16 B per lane). Round 2 gave each thread 16 consecutive columns of one
             // row — every store instruction scattered 64 x 16 B at a 128-B stride — and then waited
             // for the stores (vmcnt(0)); the two cost 30 of the kernel's 126 us (tools/prep_bench.py)
-            if (!(QK_PREP_EXP & 2)) {
+            if (!(QK_PREP_EXP & 2) && c0 >= S.x_lo && c0 < S.x_hi) {
                 d2_t z[8];  // all eight rows read first: distinct registers, no store-data waits
 #pragma unroll
                 for (int v = 0; v < 8; ++v) z[v] = *reinterpret_cast<const d2_t*>(&L.x[8 * wave_s + v][2 * lane]);
@@ -248,20 +256,23 @@ __global__ __launch_bounds__(PTH, 2 * QK_PREP_WG_PER_CU) void qk_prep_operands_k
             // memory operations complete in issue order, so the next tile's counted waits cover them
         }
         // ---- this workgroup's partial sums (zero if it took no tile)
-        double* p = a.part + ((int64_t)sd * gridDim.x + blockIdx.x) * PPART;
+        double* p = sd == 0 ? a.part + (int64_t)blockIdx.x * PPA
+                            : a.part + (int64_t)gridDim.x * PPA + (int64_t)blockIdx.x * PPB;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-            const int gr = 16 * bi + l4 + 4 * rr;
-            p[gr * PK + 16 * bj0 + l16] = g0[rr];
-            p[gr * PK + 16 * (bj0 + 1) + l16] = g1[rr];
-            if (wave < 4) p[PK * PK + (16 * wave + l4 + 4 * rr) * PNP + l16] = u[rr];
+            const int e = (l4 + 4 * rr) * 16 + l16;  // (row, column) inside the 16 x 16 block
+            if (bi <= bj0) p[prep_tri(bi, bj0) * 256 + e] = g0[rr];
+            if (bi <= bj0 + 1) p[prep_tri(bi, bj0 + 1) * 256 + e] = g1[rr];
+            if (sd == 1 && wave < 4) p[PPG + (16 * wave + l4 + 4 * rr) * PNP + l16] = u[rr];
         }
     }
 }
 
 // out (sums in a fixed order): GA [K][K], GB [K][K], U [K][16] (from the B side's partials). A
-// workgroup takes 64 consecutive outputs; its 4 waves sum every 4th partial row (coalesced 512-B row
-// segments, 4 x more loads in flight than one thread per output), then LDS adds the 4 sums.
+// workgroup takes 64 consecutive partial entries; its PRW waves sum every PRW-th partial (coalesced
+// 512-B segments, PRW x more loads in flight than one thread per output), then LDS adds the PRW sums.
+// Indexing the outputs by (row, column) instead read the mirrored blocks at a 128-B lane stride: 99 vs
+// 43 us beside the 8-rank writes (profiles/r05w_*).
 constexpr int PRW = 16;  // waves per reduction workgroup (each sums every 16th partial: 4 in-flight rounds
                          // of 8 loads at 512 partials; 4 waves took 16 rounds, 26 us)
 __global__ __launch_bounds__(64 * PRW) void qk_prep_reduce_kernel(const double* __restrict__ part, int nblk,
@@ -269,21 +280,33 @@ __global__ __launch_bounds__(64 * PRW) void qk_prep_reduce_kernel(const double* 
                                                                   double* __restrict__ GB, double* __restrict__ U) {
     __shared__ double acc[PRW][64];
     const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-    const int e = blockIdx.x * 64 + lane;  // [0, 2 K^2 + 16 K)
-    const int KK = K * K;
+    // outputs in the partials' own order (coalesced 512-B reads): the A Gram's upper blocks, the B Gram's,
+    // then U; an off-diagonal block entry is written to both (r, c) and (c, r)
+    const int e = blockIdx.x * 64 + lane;  // [0, 2 PPG + 16 K)
     int sd = -1, off = 0;
     double* dst = nullptr;
-    if (e < KK) {
-        sd = 0, off = (e / K) * PK + e % K, dst = GA + e;
-    } else if (e < 2 * KK) {
-        sd = 1, off = ((e - KK) / K) * PK + (e - KK) % K, dst = GB + (e - KK);
-    } else if (e < 2 * KK + PNP * K) {
-        const int f = e - 2 * KK;
-        sd = 1, off = PK * PK + f, dst = U + f;  // U rows k < K: [k][16]
+    double* mirror = nullptr;
+    if (e < 2 * PPG) {
+        sd = e < PPG ? 0 : 1;
+        off = e - sd * PPG;
+        const int blk = off >> 8;
+        const int bi = blk < 4 ? 0 : blk < 7 ? 1 : blk < 9 ? 2 : 3;
+        const int bj = bi + blk - prep_tri(bi, bi);
+        const int r = 16 * bi + ((off >> 4) & 15), c = 16 * bj + (off & 15);
+        if (r < K && c < K) {
+            double* G = sd == 0 ? GA : GB;
+            dst = G + r * K + c;
+            if (bi != bj) mirror = G + c * K + r;
+        }
+    } else if (e < 2 * PPG + PNP * K) {
+        const int f = e - 2 * PPG;
+        sd = 1, off = PPG + f, dst = U + f;  // U rows k < K: [k][16]
     }
+    if (!dst) sd = -1;  // entries past K: nothing to sum (the block stays uniform for the barrier)
     double s = 0.0;
     if (sd >= 0) {
-        const double* p = part + (int64_t)sd * nblk * PPART + off;
+        const int PPART = sd == 0 ? PPA : PPB;  // this side's partial stride
+        const double* p = part + (sd == 0 ? 0 : (int64_t)nblk * PPA) + off;
         // 32 loads in flight per thread (one memory round trip for 512 partials; batches of 8 took four),
         // fixed summation order
         double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -309,6 +332,7 @@ __global__ __launch_bounds__(64 * PRW) void qk_prep_reduce_kernel(const double* 
 #pragma unroll
             for (int w = 0; w < h; ++w) v[w] += v[w + h];
         *dst = v[0];
+        if (mirror) *mirror = v[0];
     }
 }
 
@@ -1165,14 +1189,24 @@ extern "C" {
 
 int qk_prep_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes) {
     if (!ctx || !bytes) return QK_EARG;
-    *bytes = (int64_t)2 * prep_grid(ctx, NA, NB) * PPART * (int64_t)sizeof(double);
+    *bytes = (int64_t)prep_grid(ctx, NA, NB) * (PPA + PPB) * (int64_t)sizeof(double);
     return QK_OK;
 }
 
 int qk_prep_operands(qk_ctx* ctx, int K, int RA, const double* WtA, const double* qA, int64_t ldqA, int64_t NA,
                      double* XA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB, double* XB,
                      const double* probes, double* GA, double* GB, double* U, double* work, int64_t work_bytes) {
+    return qk_prep_operands_cols(ctx, K, RA, WtA, qA, ldqA, NA, XA, RB, WtB, qB, ldqB, NB, XB, probes, GA, GB, U, work,
+                                 work_bytes, 0, NA);
+}
+
+int qk_prep_operands_cols(qk_ctx* ctx, int K, int RA, const double* WtA, const double* qA, int64_t ldqA, int64_t NA,
+                          double* XA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB, double* XB,
+                          const double* probes, double* GA, double* GB, double* U, double* work, int64_t work_bytes,
+                          int64_t xa_lo, int64_t xa_hi) {
     if (!ctx) return QK_EARG;
+    if (xa_lo < 0 || xa_hi > NA || xa_lo > xa_hi || xa_lo % PCT || xa_hi % PCT)
+        return fail(ctx, QK_EARG, "qk_prep_operands: X_A column window must be 128-aligned inside [0, NA]");
     if (K < 2 || K > PK || (K & 1) || RA < 1 || RB < 1)
         return fail(ctx, QK_EARG, "qk_prep_operands: need even 2 <= K <= 64 and R >= 1 on both sides");
     if (((reinterpret_cast<uintptr_t>(WtA) | reinterpret_cast<uintptr_t>(WtB) | reinterpret_cast<uintptr_t>(qA) |
@@ -1183,17 +1217,17 @@ int qk_prep_operands(qk_ctx* ctx, int K, int RA, const double* WtA, const double
     if (!WtA || !qA || !XA || !WtB || !qB || !XB || !probes || !GA || !GB || !U || !work)
         return fail(ctx, QK_EARG, "qk_prep_operands: null buffer");
     const int G = prep_grid(ctx, NA, NB);
-    if (work_bytes < (int64_t)2 * G * PPART * (int64_t)sizeof(double))
+    if (work_bytes < (int64_t)G * (PPA + PPB) * (int64_t)sizeof(double))
         return fail(ctx, QK_EARG, "qk_prep_operands: workspace too small (qk_prep_workspace_bytes)");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_prep_operands: hipSetDevice");
     PrepArgs args;
-    args.s[0] = PrepSide{WtA, qA, ldqA, NA, RA, XA, nullptr};
-    args.s[1] = PrepSide{WtB, qB, ldqB, NB, RB, XB, probes};
+    args.s[0] = PrepSide{WtA, qA, ldqA, NA, RA, XA, nullptr, xa_lo, xa_hi};
+    args.s[1] = PrepSide{WtB, qB, ldqB, NB, RB, XB, probes, 0, NB};
     args.K = K;
     args.split = prep_split(ctx, NA, NB) ? 1 : 0;
     args.part = work;
     hipLaunchKernelGGL(qk_prep_operands_kernel, dim3(G), dim3(PTH), 0, ctx->stream, args);
-    const int outs = 2 * K * K + PNP * K;
+    const int outs = 2 * PPG + PNP * K;
     hipLaunchKernelGGL(qk_prep_reduce_kernel, dim3((outs + 63) / 64), dim3(64 * PRW), 0, ctx->stream, work, G, K, GA,
                        GB, U);
     const hipError_t e = hipGetLastError();

@@ -1074,10 +1074,17 @@ def prep_ok(K: int, NA: int, NB: int) -> bool:
     return 2 <= K <= 64 and K % 2 == 0 and NA >= PREP_COLS and NB >= PREP_COLS and NA % PREP_COLS == 0 and NB % PREP_COLS == 0
 
 
-def prep_operands(ctx: Context, WtA, qA, WtB, qB, probes, out=None):
+# QKNIT_POISON_UNUSED=1 (tests): the X_A / A2 columns a column-range preparation leaves unwritten are set to NaN,
+# so a write that read outside its slice's columns shows in the output
+POISON_UNUSED = os.environ.get("QKNIT_POISON_UNUSED", "0") == "1"
+
+
+def prep_operands(ctx: Context, WtA, qA, WtB, qB, probes, out=None, xa_cols: tuple | None = None):
     """``qk_prep_operands``: ``(XA, XB, G, U)`` — the two light-cone operands ``X = Wt^T q`` ([K, N]
     each), their Grams stacked ``G = [XA XA^T, XB XB^T]`` ([2, K, K]) and ``U = XB probes^T`` ([K, 16]),
-    in one pass over the swept rows (plus a fixed-order reduction of per-workgroup partials)."""
+    in one pass over the swept rows (plus a fixed-order reduction of per-workgroup partials).
+    ``xa_cols = (base, n)`` (128-aligned): XA is stored only for those columns (qk_prep_operands_cols;
+    the others are left unwritten, NaN under QKNIT_POISON_UNUSED)."""
     T = torch()
     RA, K = WtA.shape
     RB, K2 = WtB.shape
@@ -1097,10 +1104,13 @@ def prep_operands(ctx: Context, WtA, qA, WtB, qB, probes, out=None):
     work = _PREP_WORK.get(key)
     if work is None or work.numel() * 8 < need.value:
         work = _PREP_WORK[key] = T.empty(max(need.value // 8, 1), dtype=T.float64, device=dev)
-    ctx.check(ctx.lib.qk_prep_operands(ctx.handle, K, RA, WtA.data_ptr(), qA.data_ptr(), NA, NA, XA.data_ptr(),
-                                       RB, WtB.data_ptr(), qB.data_ptr(), NB, NB, XB.data_ptr(), probes.data_ptr(),
-                                       G[0].data_ptr(), G[1].data_ptr(), U.data_ptr(), work.data_ptr(),
-                                       work.numel() * 8), "qk_prep_operands")
+    lo, hi = (0, NA) if xa_cols is None else (xa_cols[0], xa_cols[0] + xa_cols[1])
+    if xa_cols is not None and POISON_UNUSED:
+        XA.fill_(float("nan"))
+    ctx.check(ctx.lib.qk_prep_operands_cols(ctx.handle, K, RA, WtA.data_ptr(), qA.data_ptr(), NA, NA, XA.data_ptr(),
+                                            RB, WtB.data_ptr(), qB.data_ptr(), NB, NB, XB.data_ptr(), probes.data_ptr(),
+                                            G[0].data_ptr(), G[1].data_ptr(), U.data_ptr(), work.data_ptr(),
+                                            work.numel() * 8, lo, hi), "qk_prep_operands_cols")
     return XA, XB, G, U
 
 
@@ -1171,11 +1181,6 @@ def qprep_compress_check(ctx: Context, WtA, qA, WtB, qB, TA, TB, U, probes, r, t
                                               r.data_ptr(), tol, rel_tol, k.data_ptr(), err.data_ptr(), work.data_ptr(),
                                               work.numel() * 8), "qk_qprep_compress_check")
     return A2, B2, k, err
-
-
-# QKNIT_POISON_UNUSED=1 (tests): the A2 columns a column-range compression leaves unwritten are set to NaN,
-# so a write that read outside its slice's columns shows in the output
-POISON_UNUSED = os.environ.get("QKNIT_POISON_UNUSED", "0") == "1"
 
 
 def compress_operands(ctx: Context, TA, XA, TB, XB, a_cols: tuple | None = None):

@@ -344,8 +344,8 @@ class HipBackend:
     def rank_factors(self, GA, GB):
         return engine.rank_factors_device(self.ctx, GA, GB)
 
-    def prep_operands(self, WtA, qA, WtB, qB, probes):
-        return engine.prep_operands(self.ctx, WtA, qA, WtB, qB, probes)
+    def prep_operands(self, WtA, qA, WtB, qB, probes, xa_cols=None):
+        return engine.prep_operands(self.ctx, WtA, qA, WtB, qB, probes, xa_cols=xa_cols)
 
     fuses_tally = True  # probe_errors(..., tally=) updates the data-rank statistics in its accept kernel
 
@@ -1017,12 +1017,14 @@ class KnitPipeline:
         return (WA.shape[1] == WB.shape[1] and WA.shape[0] == qs[ia].shape[0] and WB.shape[0] == qs[ib].shape[0]
                 and engine.qprep_ok(WA.shape[1], WA.shape[0], WB.shape[0], qs[ia].shape[1], qs[ib].shape[1]))
 
-    def _prep_fused(self, qs, probes):
+    def _prep_fused(self, qs, probes, xa_cols=None):
         """(mats, G, U): light-cone operands of the two sides, their Grams [2, K, K] and the B side
-        against the probes [K, 16], from one qk_prep_operands call."""
+        against the probes [K, 16], from one qk_prep_operands call (``xa_cols``: X_A stored only for
+        those columns)."""
         ia, ib = self.order[0], self.order[-1]
+        kw = {} if xa_cols is None else {"xa_cols": xa_cols}
         XA, XB, G, U = self.be.prep_operands(self.transforms[ia], qs[ia].contiguous(), self.transforms[ib],
-                                             qs[ib].contiguous(), probes)
+                                             qs[ib].contiguous(), probes, **kw)
         mats = [None] * len(qs)
         mats[ia], mats[ib] = XA, XB
         self.last_prep = "fused"
@@ -1073,13 +1075,15 @@ class KnitPipeline:
             return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
         if self._fused_prep(qs):
             x = self._probes(qs[ib].shape[1], qs[ib].device)
-            mats, G, U = self._prep_fused(qs, x)
-            TA, TB, r = self.be.rank_factors(G[0], G[1])
             a_cols = self._replicated_a_cols()
+            mats, G, U = self._prep_fused(qs, x, xa_cols=a_cols if a_cols and a_cols[0] % 128 == 0
+                                          and a_cols[1] % 128 == 0 else None)
+            TA, TB, r = self.be.rank_factors(G[0], G[1])
             if a_cols is not None:
                 # replicated slice: this rank's output slice reads only A columns [base, base + n) (rows
-                # of R): it compresses those and checks those rows against every probe — its own slice's
-                # verdict, as each rank's rows in the sharded check (the Grams and factors stay whole)
+                # of R): X_A is stored, compressed and checked only there, each of those rows against every
+                # probe — its own slice's verdict, as each rank's rows in the sharded check (the Grams and
+                # factors stay whole)
                 base, n = a_cols
                 A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib], a_cols=a_cols)
                 XAc = mats[ia][:, base:base + n]

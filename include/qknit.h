@@ -339,6 +339,12 @@ int qk_prep_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes)
 int qk_prep_operands(qk_ctx* ctx, int K, int RA, const double* WtA, const double* qA, int64_t ldqA, int64_t NA,
                      double* XA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB, double* XB,
                      const double* probes, double* GA, double* GB, double* U, double* work, int64_t work_bytes);
+/* The same with X_A stored only for its columns [xa_lo, xa_hi) (128-aligned; the Grams still cover every
+ * column): a replicated multi-GPU rank needs X_A only where its output slice reads. */
+int qk_prep_operands_cols(qk_ctx* ctx, int K, int RA, const double* WtA, const double* qA, int64_t ldqA, int64_t NA,
+                          double* XA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB, double* XB,
+                          const double* probes, double* GA, double* GB, double* U, double* work, int64_t work_bytes,
+                          int64_t xa_lo, int64_t xa_hi);
 
 /* The same preparation without materialising X_s (round 5, "q-space"; swept rows R_s <= 80 per side):
  * qk_qprep_grams forms G_A, G_B [K][K] and U [K][16] from Gq_s = q_s q_s^T and Pq = q_B P^T (one MFMA

@@ -118,10 +118,17 @@ class CpuBackend:
             TA[:r], TB[:r] = torch.from_numpy(f[0]), torch.from_numpy(f[1])
         return TA, TB, torch.tensor([r], dtype=torch.int32)
 
-    def prep_operands(self, WtA, qA, WtB, qB, probes):
-        """qk_prep_operands' contract: (XA, XB, [GA, GB], U = XB probes^T)."""
+    def prep_operands(self, WtA, qA, WtB, qB, probes, xa_cols=None):
+        """qk_prep_operands' contract: (XA, XB, [GA, GB], U = XB probes^T); xa_cols = (base, n): the
+        returned XA holds NaN outside those columns (qk_prep_operands_cols leaves them unwritten)."""
         XA, XB = WtA.T @ qA, WtB.T @ qB
-        return XA, XB, torch.stack([XA @ XA.T, XB @ XB.T]), XB @ probes.T
+        G = torch.stack([XA @ XA.T, XB @ XB.T])
+        if xa_cols is not None:
+            XA = XA.clone()
+            keep = torch.zeros(XA.shape[1], dtype=torch.bool)
+            keep[xa_cols[0]:xa_cols[0] + xa_cols[1]] = True
+            XA[:, ~keep] = float("nan")
+        return XA, XB, G, XB @ probes.T
 
     def qprep_grams(self, WtA, qA, WtB, qB, probes):
         """qk_qprep_grams' contract: (G = [XA XA^T, XB XB^T] via Wt^T (q q^T) Wt, U = Wt_B^T (q_B probes^T))."""
