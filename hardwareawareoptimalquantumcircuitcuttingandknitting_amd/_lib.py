@@ -88,9 +88,6 @@ SIGNATURES = {
     "qk_prep_workspace_bytes": (c_i32, [c_vp, c_i64, c_i64, ctypes.POINTER(c_i64)]),
     "qk_prep_operands": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_i64, c_vp, ctypes.c_int,
                                  c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64]),
-    "qk_prep_operands_cols": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_i64, c_vp, ctypes.c_int,
-                                      c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
-                                      c_i64]),
     "qk_qprep_workspace_bytes": (c_i32, [c_vp, c_i64, c_i64, ctypes.POINTER(c_i64)]),
     "qk_qprep_grams": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_i64, ctypes.c_int, c_vp, c_vp,
                                c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64]),
@@ -99,8 +96,8 @@ SIGNATURES = {
                                         c_vp, c_vp, ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp, c_i64]),
     "qk_compress_operands": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                                      c_vp]),
-    "qk_compress_operands_ld": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp,
-                                        c_i64, c_i64, c_vp]),
+    "qk_compress_operands_ld": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,
+                                        c_vp, c_i64, c_i64, c_vp, c_i64]),
     "qk_probe_workspace_bytes": (c_i32, [c_vp, c_i64, ctypes.POINTER(c_i64)]),
     "qk_probe_errors": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64,
                                 c_i64, c_vp, c_i64, c_vp, c_vp, ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp,

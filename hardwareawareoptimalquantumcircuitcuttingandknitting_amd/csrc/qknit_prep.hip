@@ -55,7 +55,6 @@ struct PrepSide {
     int R;
     double* X;         // [K][N]
     const double* P;   // probes [16][N] (B side) or nullptr
-    int64_t x_lo, x_hi;  // X is stored only for the column tiles in [x_lo, x_hi) (Grams: every column)
 };
 
 struct PrepArgs {
@@ -244,7 +243,7 @@ __global__ __launch_bounds__(PTH, 2 * QK_PREP_WG_PER_CU) void qk_prep_operands_k
             // wave-instruction (16 B per lane). Round 2 gave each thread 16 consecutive columns of one
             // row — every store instruction scattered 64 x 16 B at a 128-B stride — and then waited
             // for the stores (vmcnt(0)); the two cost 30 of the kernel's 126 us (tools/prep_bench.py)
-            if (!(QK_PREP_EXP & 2) && c0 >= S.x_lo && c0 < S.x_hi) {
+            if (!(QK_PREP_EXP & 2)) {
                 d2_t z[8];  // all eight rows read first: distinct registers, no store-data waits
 #pragma unroll
                 for (int v = 0; v < 8; ++v) z[v] = *reinterpret_cast<const d2_t*>(&L.x[8 * wave_s + v][2 * lane]);
@@ -342,17 +341,18 @@ __global__ __launch_bounds__(64 * PRW) void qk_prep_reduce_kernel(const double* 
 // before T is staged, and the grid is one 64-column block per workgroup (4 per CU per side: every
 // load of the kernel in flight at once, no second round trip)
 __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const double* __restrict__ TA,
-                                                          const double* __restrict__ XA, int64_t NA, int64_t lda,
-                                                          double* __restrict__ A2, const double* __restrict__ TB,
-                                                          const double* __restrict__ XB, int64_t NB, int64_t ldb,
-                                                          double* __restrict__ B2) {
+                                                          const double* __restrict__ XA, int64_t NA, int64_t ldxa,
+                                                          double* __restrict__ A2, int64_t lda2,
+                                                          const double* __restrict__ TB,
+                                                          const double* __restrict__ XB, int64_t NB, int64_t ldxb,
+                                                          double* __restrict__ B2, int64_t ldb2) {
     __shared__ double T[8][PK];
     __shared__ double part[4][8][64];
     const bool bs = blockIdx.y == 1;
     const double* Tg = bs ? TB : TA;
     const double* X = bs ? XB : XA;
     double* out = bs ? B2 : A2;
-    const int64_t N = bs ? NB : NA, ld = bs ? ldb : lda;
+    const int64_t N = bs ? NB : NA, ld = bs ? ldxb : ldxa, ldo = bs ? ldb2 : lda2;
     const int l = threadIdx.x & 63;
     const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: SGPR row bases
     auto load = [&](int64_t c0, double (&xv)[16]) {
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
         for (int e = threadIdx.x; e < 8 * 64; e += 256) {
             const int j = e >> 6, cc = e & 63;
             if (j < rmax && c0 + cc < N)
-                out[(int64_t)j * ld + c0 + cc] = (part[0][j][cc] + part[1][j][cc]) + (part[2][j][cc] + part[3][j][cc]);
+                out[(int64_t)j * ldo + c0 + cc] = (part[0][j][cc] + part[1][j][cc]) + (part[2][j][cc] + part[3][j][cc]);
         }
         __syncthreads();
         if (c0 + (int64_t)gridDim.x * 64 < N) load(c0 + (int64_t)gridDim.x * 64, xv);
@@ -401,15 +401,16 @@ __global__ __launch_bounds__(256) void qk_compress_kernel(int K, int rmax, const
 // in flight in 16-row chunks, the next chunk issued before the current one is summed.
 constexpr int PCW = 16;  // rows per load chunk
 __global__ __launch_bounds__(64) void qk_compress_cols_kernel(int K, int rmax, const double* __restrict__ TA,
-                                                              const double* __restrict__ XA, int64_t NA, int64_t lda,
-                                                              double* __restrict__ A2, const double* __restrict__ TB,
-                                                              const double* __restrict__ XB, int64_t NB, int64_t ldb,
-                                                              double* __restrict__ B2) {
+                                                              const double* __restrict__ XA, int64_t NA, int64_t ldxa,
+                                                              double* __restrict__ A2, int64_t lda2,
+                                                              const double* __restrict__ TB,
+                                                              const double* __restrict__ XB, int64_t NB, int64_t ldxb,
+                                                              double* __restrict__ B2, int64_t ldb2) {
     const bool bs = blockIdx.y == 1;
     const double* Tg = bs ? TB : TA;
     const double* X = bs ? XB : XA;
     double* out = bs ? B2 : A2;
-    const int64_t N = bs ? NB : NA, ld = bs ? ldb : lda;
+    const int64_t N = bs ? NB : NA, ld = bs ? ldxb : ldxa, ldo = bs ? ldb2 : lda2;
     const int64_t c = ((int64_t)blockIdx.x * 64 + threadIdx.x) * 2;
     if ((int64_t)blockIdx.x * 128 >= N) return;  // the whole wave past this side's columns
     const int64_t cl = c < N ? c : N - 2;          // loads of lanes past the end: the last column pair
@@ -469,7 +470,7 @@ __global__ __launch_bounds__(64) void qk_compress_cols_kernel(int K, int rmax, c
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-        if (j < rmax) *reinterpret_cast<d2_t*>(out + (int64_t)j * ld + c) = acc[j];
+        if (j < rmax) *reinterpret_cast<d2_t*>(out + (int64_t)j * ldo + c) = acc[j];
 }
 
 constexpr int PV_GRID = 128;  // workgroups of the V = B'' P^T partial sums (probe_d sums their partials)
@@ -1196,17 +1197,7 @@ int qk_prep_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes)
 int qk_prep_operands(qk_ctx* ctx, int K, int RA, const double* WtA, const double* qA, int64_t ldqA, int64_t NA,
                      double* XA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB, double* XB,
                      const double* probes, double* GA, double* GB, double* U, double* work, int64_t work_bytes) {
-    return qk_prep_operands_cols(ctx, K, RA, WtA, qA, ldqA, NA, XA, RB, WtB, qB, ldqB, NB, XB, probes, GA, GB, U, work,
-                                 work_bytes, 0, NA);
-}
-
-int qk_prep_operands_cols(qk_ctx* ctx, int K, int RA, const double* WtA, const double* qA, int64_t ldqA, int64_t NA,
-                          double* XA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB, double* XB,
-                          const double* probes, double* GA, double* GB, double* U, double* work, int64_t work_bytes,
-                          int64_t xa_lo, int64_t xa_hi) {
     if (!ctx) return QK_EARG;
-    if (xa_lo < 0 || xa_hi > NA || xa_lo > xa_hi || xa_lo % PCT || xa_hi % PCT)
-        return fail(ctx, QK_EARG, "qk_prep_operands: X_A column window must be 128-aligned inside [0, NA]");
     if (K < 2 || K > PK || (K & 1) || RA < 1 || RB < 1)
         return fail(ctx, QK_EARG, "qk_prep_operands: need even 2 <= K <= 64 and R >= 1 on both sides");
     if (((reinterpret_cast<uintptr_t>(WtA) | reinterpret_cast<uintptr_t>(WtB) | reinterpret_cast<uintptr_t>(qA) |
@@ -1221,8 +1212,8 @@ int qk_prep_operands_cols(qk_ctx* ctx, int K, int RA, const double* WtA, const d
         return fail(ctx, QK_EARG, "qk_prep_operands: workspace too small (qk_prep_workspace_bytes)");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_prep_operands: hipSetDevice");
     PrepArgs args;
-    args.s[0] = PrepSide{WtA, qA, ldqA, NA, RA, XA, nullptr, xa_lo, xa_hi};
-    args.s[1] = PrepSide{WtB, qB, ldqB, NB, RB, XB, probes, 0, NB};
+    args.s[0] = PrepSide{WtA, qA, ldqA, NA, RA, XA, nullptr};
+    args.s[1] = PrepSide{WtB, qB, ldqB, NB, RB, XB, probes};
     args.K = K;
     args.split = prep_split(ctx, NA, NB) ? 1 : 0;
     args.part = work;
@@ -1320,30 +1311,33 @@ int qk_qprep_compress_check(qk_ctx* ctx, int K, int rmax, int RA, const double* 
 
 int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, double* A2,
                          const double* TB, const double* XB, int64_t NB, double* B2) {
-    return qk_compress_operands_ld(ctx, K, rmax, TA, XA, NA, NA, A2, TB, XB, NB, NB, B2);
+    return qk_compress_operands_ld(ctx, K, rmax, TA, XA, NA, NA, A2, NA, TB, XB, NB, NB, B2, NB);
 }
 
-int qk_compress_operands_ld(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, int64_t lda,
-                            double* A2, const double* TB, const double* XB, int64_t NB, int64_t ldb, double* B2) {
+int qk_compress_operands_ld(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, int64_t ldxa,
+                            double* A2, int64_t lda2, const double* TB, const double* XB, int64_t NB, int64_t ldxb,
+                            double* B2, int64_t ldb2) {
     if (!ctx) return QK_EARG;
     if (K < 1 || K > PK || rmax < 1 || rmax > 8 || NA < 1 || NB < 1)
         return fail(ctx, QK_EARG, "qk_compress_operands: need 1 <= K <= 64, 1 <= rmax <= 8, N >= 1");
-    if (lda < NA || ldb < NB) return fail(ctx, QK_EARG, "qk_compress_operands: leading dimension below the width");
+    if (ldxa < NA || lda2 < NA || ldxb < NB || ldb2 < NB)
+        return fail(ctx, QK_EARG, "qk_compress_operands: leading dimension below the width");
     if (!TA || !XA || !A2 || !TB || !XB || !B2) return fail(ctx, QK_EARG, "qk_compress_operands: null buffer");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_compress_operands: hipSetDevice");
     const int64_t N = NA > NB ? NA : NB;
-    const bool cols = QK_COMPRESS_COLS && NA % 2 == 0 && NB % 2 == 0 && lda % 2 == 0 && ldb % 2 == 0 &&
+    const bool cols = QK_COMPRESS_COLS && NA % 2 == 0 && NB % 2 == 0 && ldxa % 2 == 0 && lda2 % 2 == 0 &&
+                      ldxb % 2 == 0 && ldb2 % 2 == 0 &&
                       !((reinterpret_cast<uintptr_t>(XA) | reinterpret_cast<uintptr_t>(XB) |
                          reinterpret_cast<uintptr_t>(A2) | reinterpret_cast<uintptr_t>(B2)) & 15);
     if (cols) {
         hipLaunchKernelGGL(qk_compress_cols_kernel, dim3((unsigned)((N + 127) / 128), 2), dim3(64), 0, ctx->stream, K,
-                           rmax, TA, XA, NA, lda, A2, TB, XB, NB, ldb, B2);
+                           rmax, TA, XA, NA, ldxa, A2, lda2, TB, XB, NB, ldxb, B2, ldb2);
     } else {
         int64_t gx = (N + 63) / 64;
         const int64_t cap = (int64_t)(ctx->cus > 0 ? ctx->cus : 256) * 4;  // x 2 sides: up to 8 workgroups per CU
         gx = gx < cap ? gx : cap;
         hipLaunchKernelGGL(qk_compress_kernel, dim3((unsigned)gx, 2), dim3(256), 0, ctx->stream, K, rmax, TA, XA, NA,
-                           lda, A2, TB, XB, NB, ldb, B2);
+                           ldxa, A2, lda2, TB, XB, NB, ldxb, B2, ldb2);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)

@@ -1074,23 +1074,23 @@ def prep_ok(K: int, NA: int, NB: int) -> bool:
     return 2 <= K <= 64 and K % 2 == 0 and NA >= PREP_COLS and NB >= PREP_COLS and NA % PREP_COLS == 0 and NB % PREP_COLS == 0
 
 
-# QKNIT_POISON_UNUSED=1 (tests): the X_A / A2 columns a column-range preparation leaves unwritten are set to NaN,
+# QKNIT_POISON_UNUSED=1 (tests): the A2 columns a column-range compression leaves unwritten are set to NaN,
 # so a write that read outside its slice's columns shows in the output
 POISON_UNUSED = os.environ.get("QKNIT_POISON_UNUSED", "0") == "1"
 
 
-def prep_operands(ctx: Context, WtA, qA, WtB, qB, probes, out=None, xa_cols: tuple | None = None):
+def prep_operands(ctx: Context, WtA, qA, WtB, qB, probes, out=None):
     """``qk_prep_operands``: ``(XA, XB, G, U)`` — the two light-cone operands ``X = Wt^T q`` ([K, N]
     each), their Grams stacked ``G = [XA XA^T, XB XB^T]`` ([2, K, K]) and ``U = XB probes^T`` ([K, 16]),
-    in one pass over the swept rows (plus a fixed-order reduction of per-workgroup partials).
-    ``xa_cols = (base, n)`` (128-aligned): XA is stored only for those columns (qk_prep_operands_cols;
-    the others are left unwritten, NaN under QKNIT_POISON_UNUSED)."""
+    in one pass over the swept rows (plus a fixed-order reduction of per-workgroup partials). ``qA`` /
+    ``qB`` may be column windows of wider rows (unit column stride; ldq = their row stride)."""
     T = torch()
     RA, K = WtA.shape
     RB, K2 = WtB.shape
     assert K == K2 and qA.shape[0] == RA and qB.shape[0] == RB and probes.shape[0] == N_PROBES
     NA, NB = qA.shape[1], qB.shape[1]
-    assert probes.shape[1] == NB and all(t.is_contiguous() for t in (WtA, qA, WtB, qB, probes))
+    assert probes.shape[1] == NB and all(t.is_contiguous() for t in (WtA, WtB, probes))
+    assert qA.stride(1) == 1 and qB.stride(1) == 1
     dev = qA.device
     if out is None:
         # G and U share one buffer (views of it, G first): a multi-GPU rank all-reduces them in one call
@@ -1104,13 +1104,10 @@ def prep_operands(ctx: Context, WtA, qA, WtB, qB, probes, out=None, xa_cols: tup
     work = _PREP_WORK.get(key)
     if work is None or work.numel() * 8 < need.value:
         work = _PREP_WORK[key] = T.empty(max(need.value // 8, 1), dtype=T.float64, device=dev)
-    lo, hi = (0, NA) if xa_cols is None else (xa_cols[0], xa_cols[0] + xa_cols[1])
-    if xa_cols is not None and POISON_UNUSED:
-        XA.fill_(float("nan"))
-    ctx.check(ctx.lib.qk_prep_operands_cols(ctx.handle, K, RA, WtA.data_ptr(), qA.data_ptr(), NA, NA, XA.data_ptr(),
-                                            RB, WtB.data_ptr(), qB.data_ptr(), NB, NB, XB.data_ptr(), probes.data_ptr(),
-                                            G[0].data_ptr(), G[1].data_ptr(), U.data_ptr(), work.data_ptr(),
-                                            work.numel() * 8, lo, hi), "qk_prep_operands_cols")
+    ctx.check(ctx.lib.qk_prep_operands(ctx.handle, K, RA, WtA.data_ptr(), qA.data_ptr(), qA.stride(0), NA,
+                                       XA.data_ptr(), RB, WtB.data_ptr(), qB.data_ptr(), qB.stride(0), NB,
+                                       XB.data_ptr(), probes.data_ptr(), G[0].data_ptr(), G[1].data_ptr(),
+                                       U.data_ptr(), work.data_ptr(), work.numel() * 8), "qk_prep_operands")
     return XA, XB, G, U
 
 
@@ -1183,29 +1180,35 @@ def qprep_compress_check(ctx: Context, WtA, qA, WtB, qB, TA, TB, U, probes, r, t
     return A2, B2, k, err
 
 
-def compress_operands(ctx: Context, TA, XA, TB, XB, a_cols: tuple | None = None):
+def compress_operands(ctx: Context, TA, XA, TB, XB, a_cols: tuple | None = None, a_width: int | None = None):
     """``qk_compress_operands``: ``(TA XA, TB XB)`` ([rmax, N] each) in one launch. ``a_cols = (base, n)``:
-    only A2's columns [base, base + n) are computed (the others are left unwritten; qk_compress_operands_ld)."""
+    only A2's columns [base, base + n) are computed (the others are left unwritten; qk_compress_operands_ld)
+    from XA's columns [base, base + n), or from all of XA when it is that window already ([K, n]; A2 is
+    then ``a_width`` wide)."""
     T = torch()
     rmax, K = TA.shape
     assert TB.shape == (rmax, K) and XA.shape[0] == K and XB.shape[0] == K
-    assert XA.is_contiguous() and XB.is_contiguous() and TA.is_contiguous() and TB.is_contiguous()
-    NA, NB = XA.shape[1], XB.shape[1]
+    assert XA.stride(1) == 1 and XB.is_contiguous() and TA.is_contiguous() and TB.is_contiguous()
+    NA = XA.shape[1] if a_width is None else a_width
+    NB = XB.shape[1]
     # A2 and B2 share one buffer (A2 first): a multi-GPU rank all-gathers them in one call
     ab = T.empty(rmax * (NA + NB), dtype=T.float64, device=XA.device)
     A2 = ab[:rmax * NA].view(rmax, NA)
     B2 = ab[rmax * NA:].view(rmax, NB)
     if a_cols is None:
+        assert XA.is_contiguous() and XA.shape[1] == NA
         ctx.check(ctx.lib.qk_compress_operands(ctx.handle, K, rmax, TA.data_ptr(), XA.data_ptr(), NA, A2.data_ptr(),
                                                TB.data_ptr(), XB.data_ptr(), NB, B2.data_ptr()), "qk_compress_operands")
         return A2, B2
     base, n = a_cols
     assert 0 <= base and n >= 1 and base + n <= NA
+    src = XA.data_ptr() if XA.shape[1] == n else XA.data_ptr() + 8 * base
+    assert XA.shape[1] in (n, NA)
     if POISON_UNUSED:
         A2.fill_(float("nan"))
-    ctx.check(ctx.lib.qk_compress_operands_ld(ctx.handle, K, rmax, TA.data_ptr(), XA.data_ptr() + 8 * base, n, NA,
-                                              A2.data_ptr() + 8 * base, TB.data_ptr(), XB.data_ptr(), NB, NB,
-                                              B2.data_ptr()), "qk_compress_operands_ld")
+    ctx.check(ctx.lib.qk_compress_operands_ld(ctx.handle, K, rmax, TA.data_ptr(), src, n, XA.stride(0),
+                                              A2.data_ptr() + 8 * base, NA, TB.data_ptr(), XB.data_ptr(), NB, NB,
+                                              B2.data_ptr(), NB), "qk_compress_operands_ld")
     return A2, B2
 
 

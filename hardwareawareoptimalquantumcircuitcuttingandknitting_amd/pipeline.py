@@ -344,8 +344,8 @@ class HipBackend:
     def rank_factors(self, GA, GB):
         return engine.rank_factors_device(self.ctx, GA, GB)
 
-    def prep_operands(self, WtA, qA, WtB, qB, probes, xa_cols=None):
-        return engine.prep_operands(self.ctx, WtA, qA, WtB, qB, probes, xa_cols=xa_cols)
+    def prep_operands(self, WtA, qA, WtB, qB, probes):
+        return engine.prep_operands(self.ctx, WtA, qA, WtB, qB, probes)
 
     fuses_tally = True  # probe_errors(..., tally=) updates the data-rank statistics in its accept kernel
 
@@ -361,8 +361,8 @@ class HipBackend:
         self.ctx.check(self.ctx.lib.qk_rank_tally(self.ctx.handle, r.data_ptr(), k.data_ptr(), acc.data_ptr()),
                        "qk_rank_tally")
 
-    def compress(self, TA, XA, TB, XB, a_cols=None):
-        return engine.compress_operands(self.ctx, TA, XA, TB, XB, a_cols=a_cols)
+    def compress(self, TA, XA, TB, XB, a_cols=None, a_width=None):
+        return engine.compress_operands(self.ctx, TA, XA, TB, XB, a_cols=a_cols, a_width=a_width)
 
     def knit_select(self, A, B, clbits_a, clbits_b, nbits, accuracy, k_dev=None):
         return engine.knit_select(self.ctx, A, B, clbits_a, clbits_b, nbits, accuracy, k_dev=k_dev)
@@ -1017,14 +1017,13 @@ class KnitPipeline:
         return (WA.shape[1] == WB.shape[1] and WA.shape[0] == qs[ia].shape[0] and WB.shape[0] == qs[ib].shape[0]
                 and engine.qprep_ok(WA.shape[1], WA.shape[0], WB.shape[0], qs[ia].shape[1], qs[ib].shape[1]))
 
-    def _prep_fused(self, qs, probes, xa_cols=None):
+    def _prep_fused(self, qs, probes):
         """(mats, G, U): light-cone operands of the two sides, their Grams [2, K, K] and the B side
-        against the probes [K, 16], from one qk_prep_operands call (``xa_cols``: X_A stored only for
-        those columns)."""
+        against the probes [K, 16], from one qk_prep_operands call."""
         ia, ib = self.order[0], self.order[-1]
-        kw = {} if xa_cols is None else {"xa_cols": xa_cols}
-        XA, XB, G, U = self.be.prep_operands(self.transforms[ia], qs[ia].contiguous(), self.transforms[ib],
-                                             qs[ib].contiguous(), probes, **kw)
+        qa = qs[ia] if qs[ia].stride(1) == 1 else qs[ia].contiguous()
+        qb = qs[ib] if qs[ib].stride(1) == 1 else qs[ib].contiguous()
+        XA, XB, G, U = self.be.prep_operands(self.transforms[ia], qa, self.transforms[ib], qb, probes)
         mats = [None] * len(qs)
         mats[ia], mats[ib] = XA, XB
         self.last_prep = "fused"
@@ -1075,15 +1074,14 @@ class KnitPipeline:
             return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
         if self._fused_prep(qs):
             x = self._probes(qs[ib].shape[1], qs[ib].device)
-            a_cols = self._replicated_a_cols()
-            mats, G, U = self._prep_fused(qs, x, xa_cols=a_cols if a_cols and a_cols[0] % 128 == 0
-                                          and a_cols[1] % 128 == 0 else None)
+            mats, G, U = self._prep_fused(qs, x)
             TA, TB, r = self.be.rank_factors(G[0], G[1])
+            a_cols = self._replicated_a_cols()
             if a_cols is not None:
                 # replicated slice: this rank's output slice reads only A columns [base, base + n) (rows
-                # of R): X_A is stored, compressed and checked only there, each of those rows against every
-                # probe — its own slice's verdict, as each rank's rows in the sharded check (the Grams and
-                # factors stay whole)
+                # of R): it compresses those and checks those rows against every probe — its own slice's
+                # verdict, as each rank's rows in the sharded check. The Grams and factors stay whole, so
+                # every rank's compressed values are the single-GPU ones bit for bit
                 base, n = a_cols
                 A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib], a_cols=a_cols)
                 XAc = mats[ia][:, base:base + n]

@@ -339,12 +339,6 @@ int qk_prep_workspace_bytes(qk_ctx* ctx, int64_t NA, int64_t NB, int64_t* bytes)
 int qk_prep_operands(qk_ctx* ctx, int K, int RA, const double* WtA, const double* qA, int64_t ldqA, int64_t NA,
                      double* XA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB, double* XB,
                      const double* probes, double* GA, double* GB, double* U, double* work, int64_t work_bytes);
-/* The same with X_A stored only for its columns [xa_lo, xa_hi) (128-aligned; the Grams still cover every
- * column): a replicated multi-GPU rank needs X_A only where its output slice reads. */
-int qk_prep_operands_cols(qk_ctx* ctx, int K, int RA, const double* WtA, const double* qA, int64_t ldqA, int64_t NA,
-                          double* XA, int RB, const double* WtB, const double* qB, int64_t ldqB, int64_t NB, double* XB,
-                          const double* probes, double* GA, double* GB, double* U, double* work, int64_t work_bytes,
-                          int64_t xa_lo, int64_t xa_hi);
 
 /* The same preparation without materialising X_s (round 5, "q-space"; swept rows R_s <= 80 per side):
  * qk_qprep_grams forms G_A, G_B [K][K] and U [K][16] from Gq_s = q_s q_s^T and Pq = q_B P^T (one MFMA
@@ -366,11 +360,12 @@ int qk_qprep_compress_check(qk_ctx* ctx, int K, int rmax, int RA, const double* 
 /* A2 = TA X_A ([rmax][NA]), B2 = TB X_B ([rmax][NB]) for [rmax][K] factors (rmax <= 8), one launch. */
 int qk_compress_operands(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, double* A2,
                          const double* TB, const double* XB, int64_t NB, double* B2);
-/* The same over column ranges of wider operands: X_A / A2 rows lda apart, X_B / B2 rows ldb apart (a
- * replicated multi-GPU rank compresses only the A columns its output slice reads; the pointers are offset
- * to the first column). */
-int qk_compress_operands_ld(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, int64_t lda,
-                            double* A2, const double* TB, const double* XB, int64_t NB, int64_t ldb, double* B2);
+/* The same with leading dimensions: rows of X_A, A2, X_B, B2 ldxa / lda2 / ldxb / ldb2 apart (a replicated
+ * multi-GPU rank compresses only the A columns its output slice reads, into those columns of a full-width
+ * A2; the pointers are offset to the first column). */
+int qk_compress_operands_ld(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, int64_t ldxa,
+                            double* A2, int64_t lda2, const double* TB, const double* XB, int64_t NB, int64_t ldxb,
+                            double* B2, int64_t ldb2);
 
 /* Acceptance check of a compressed knit on the real operands (the probe products of the torch form,
  * not materialised): e2[p] = ||(X_A^T X_B - A2^T B2) P_p||^2 and e2[16 + p] = ||X_A^T X_B P_p||^2

@@ -118,17 +118,10 @@ class CpuBackend:
             TA[:r], TB[:r] = torch.from_numpy(f[0]), torch.from_numpy(f[1])
         return TA, TB, torch.tensor([r], dtype=torch.int32)
 
-    def prep_operands(self, WtA, qA, WtB, qB, probes, xa_cols=None):
-        """qk_prep_operands' contract: (XA, XB, [GA, GB], U = XB probes^T); xa_cols = (base, n): the
-        returned XA holds NaN outside those columns (qk_prep_operands_cols leaves them unwritten)."""
+    def prep_operands(self, WtA, qA, WtB, qB, probes):
+        """qk_prep_operands' contract: (XA, XB, [GA, GB], U = XB probes^T)."""
         XA, XB = WtA.T @ qA, WtB.T @ qB
-        G = torch.stack([XA @ XA.T, XB @ XB.T])
-        if xa_cols is not None:
-            XA = XA.clone()
-            keep = torch.zeros(XA.shape[1], dtype=torch.bool)
-            keep[xa_cols[0]:xa_cols[0] + xa_cols[1]] = True
-            XA[:, ~keep] = float("nan")
-        return XA, XB, G, XB @ probes.T
+        return XA, XB, torch.stack([XA @ XA.T, XB @ XB.T]), XB @ probes.T
 
     def qprep_grams(self, WtA, qA, WtB, qB, probes):
         """qk_qprep_grams' contract: (G = [XA XA^T, XB XB^T] via Wt^T (q q^T) Wt, U = Wt_B^T (q_B probes^T))."""
@@ -164,14 +157,16 @@ class CpuBackend:
         rv = int(r.reshape(-1)[0])
         return torch.tensor([rv if rv > 0 and err <= bound else 0], dtype=torch.int32), torch.tensor([err])
 
-    def compress(self, TA, XA, TB, XB, a_cols=None):
+    def compress(self, TA, XA, TB, XB, a_cols=None, a_width=None):
         """qk_compress_operands' contract; a_cols = (base, n): only A2's columns [base, base + n) are
-        written, the others hold NaN (a read outside them shows in the output)."""
+        written (from XA's, or from all of XA when it is [K, n]), the others hold NaN (a read outside
+        them shows in the output); A2 is a_width wide (default XA's width)."""
         if a_cols is None:
             return (TA @ XA).contiguous(), (TB @ XB).contiguous()
         base, n = a_cols
-        A2 = torch.full((TA.shape[0], XA.shape[1]), float("nan"), dtype=XA.dtype)
-        A2[:, base:base + n] = TA @ XA[:, base:base + n]
+        width = XA.shape[1] if a_width is None else a_width
+        A2 = torch.full((TA.shape[0], width), float("nan"), dtype=XA.dtype)
+        A2[:, base:base + n] = TA @ (XA if XA.shape[1] == n else XA[:, base:base + n])
         return A2, (TB @ XB).contiguous()
 
     def khatri_rao(self, A, B):
