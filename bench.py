@@ -722,6 +722,14 @@ def main():
     prep = [s.elapsed_time(e) for s, e in pipe.prep_events]
     if prep:
         line["rank_compress_ms"] = sum(prep) / len(prep)  # sweep end -> knit start (transforms, factors, probes)
+    if pipelined is not None and roof["bound"] == "hbm":
+        # pipelined steps overlap out_buffers writes, so one launch's duration spans several steps: the
+        # rank's HBM rate is the step's algorithmic bytes over the step time (the per-launch figure above
+        # follows the contract's definition)
+        per_step = gbytes / (ms_per_step * 1e-3) / 1e9
+        line["roofline"]["per_step"] = {"achieved": per_step, "frac": per_step / HBM_PEAK_GBS,
+                                        "concurrent_writes": pipe.out_buffers,
+                                        "note": "algorithmic bytes of one step's write / ms_per_step"}
     if pipelined is not None:
         pipelined["note"] = ("value / ms_per_step: pipelined steps (step i+1's sweep + data-rank preparation on "
                              f"{pipelined['prep_cus']} CUs under step i's write on the other {pipelined['write_cus']}); "
