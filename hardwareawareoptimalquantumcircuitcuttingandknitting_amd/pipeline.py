@@ -516,8 +516,8 @@ class KnitPipeline:
         self.out_alloc = None  # how the last output buffer was allocated (new_out)
         # slice mode: how a rank gets the operands of its slice (_choose_slice_prep, QKNIT_SLICE_PREP):
         # "replicated" — every rank sweeps every swept row and runs the whole preparation chain itself
-        # (deterministic kernels on identical inputs: identical operands and verdicts on every rank), then
-        # writes its slice; no collective in the step. "sharded" — rows dealt over the ranks, one
+        # (deterministic kernels on identical inputs: identical operands on every rank), checks its own
+        # slice's rows and writes its slice; no collective in the step. "sharded" — rows dealt over the ranks, one
         # all_to_all / all_reduce / all_gather / MIN all_reduce per step (round 2-4's slice mode).
         self.slice_prep = None
         self.slice_costs = None  # the cost model's per-step estimates (ms) of both, when it chose
@@ -1260,8 +1260,8 @@ class KnitPipeline:
             self.events.append((start, end))
         if not self.sharded:
             # replicated preparation: every rank holds the whole transformed operands, so the exact
-            # slice (predicated on the same device verdict, identical on every rank) reads its columns
-            # in place — no collective. Pipelined steps queue it before the write (_step_overlapped)
+            # slice (predicated on this rank's own verdict over its slice's rows) reads its columns in
+            # place — no collective. Pipelined steps queue it before the write (_step_overlapped)
             if p.get("exact_queued"):
                 return self.out
             A, kA, B, kB = self._slice_exact_operands(*self._exact_mats(p))
