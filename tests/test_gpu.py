@@ -1110,6 +1110,18 @@ def test_prep_operands_matches_torch(T, K, RA, RB, NA, NB):
     XA2, XB2, G2, U2 = engine.prep_operands(ctx, WtA, qA, WtB, qB, P)
     T.cuda.synchronize()
     assert T.equal(G, G2) and T.equal(U, U2) and T.equal(XB, XB2)  # deterministic
+    # the partials hold the upper 16 x 16 blocks only: the lower ones are their mirror, bit for bit
+    assert T.equal(G[0], G[0].T) and T.equal(G[1], G[1].T)
+    if NA >= 256:
+        # q as a 128-aligned column window of wider rows (row stride > width): the window's X, Gram
+        # and (B side) probe products, bit for bit those of the same columns copied out
+        h = NA // 2
+        qw = qA[:, h:]
+        assert not qw.is_contiguous()
+        XAw, _, Gw, _ = engine.prep_operands(ctx, WtA, qw, WtB, qB, P)
+        XAc, _, Gc, _ = engine.prep_operands(ctx, WtA, qw.contiguous(), WtB, qB, P)
+        T.cuda.synchronize()
+        assert T.equal(XAw, XAc) and T.equal(Gw, Gc)
     if K == 6:
         assert not engine.prep_ok(5, NA, NB)
         with pytest.raises(engine._lib.QknitError):
@@ -1168,6 +1180,13 @@ def test_compress_operands_matches_torch(T, K, NA, NB, rmax):
     T.cuda.synchronize()
     for got, ref in ((A2, TA @ XA), (B2, TB @ XB)):
         assert float((got - ref).abs().max()) <= 1e-13 * float(ref.abs().max())
+    if NA % 4 == 0:
+        # qk_compress_operands_ld, a replicated rank's form: A2's columns [base, base + n) only, from X_A's
+        # same columns — bit for bit the full compression's there (same kernel per column), B2 unchanged
+        base, n = NA // 4, NA // 2
+        A2c, B2c = engine.compress_operands(ctx, TA, XA, TB, XB, a_cols=(base, n))
+        T.cuda.synchronize()
+        assert A2c.shape == A2.shape and T.equal(A2c[:, base:base + n], A2[:, base:base + n]) and T.equal(B2c, B2)
 
 
 @pytest.mark.parametrize("K,ra,rb,r,noise", [(64, 8, 8, 2, 0.0), (64, 5, 12, 4, 0.0), (64, 20, 20, 8, 0.0),
