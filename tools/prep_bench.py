@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Time qk_prep_operands alone on syc 32 5's shapes (random operands): K = 64, 256 + 64 instance rows,
-2 x 65536 columns. Select a tuning build with QKNIT_LIB. Prints mean us per call and MFMA TF/s."""
+"""Time qk_prep_operands alone on syc 32 5's shapes (random operands): K = 64, RA + RB instance rows
+(argv: RA RB, default 65 65 — the swept rows after pruning; round 3 used 256 64), 2 x 65536 columns.
+Select a tuning build with QKNIT_LIB. Prints mean us per call and MFMA TF/s."""
 import json
 import os
 import sys
@@ -15,7 +16,8 @@ def main():
 
     ctx = engine.get_context(0)
     g = torch.Generator(device="cuda").manual_seed(0)
-    K, RA, RB, N = 64, 256, 64, 65536
+    RA, RB = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (65, 65)
+    K, N = 64, 65536
     WtA, WtB = (torch.randn(R, K, dtype=torch.float64, device="cuda", generator=g) for R in (RA, RB))
     qA, qB = (torch.randn(R, N, dtype=torch.float64, device="cuda", generator=g) for R in (RA, RB))
     P = torch.randn(16, N, dtype=torch.float64, device="cuda", generator=g)
@@ -30,7 +32,7 @@ def main():
     torch.cuda.synchronize()
     us = s.elapsed_time(e) / reps * 1e3
     flops = 2.0 * K * N * (RA + RB) + 2 * 2.0 * K * K * N + 2.0 * K * 16 * N
-    print(json.dumps({"lib": os.environ.get("QKNIT_LIB", "default"), "us": us, "TFs": flops / (us * 1e-6) / 1e12}),
+    print(json.dumps({"lib": os.environ.get("QKNIT_LIB", "default"), "rows": [RA, RB], "us": us, "TFs": flops / (us * 1e-6) / 1e12}),
           flush=True)
 
 
