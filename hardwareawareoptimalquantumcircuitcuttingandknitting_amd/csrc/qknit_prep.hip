@@ -128,7 +128,21 @@ __global__ __launch_bounds__(PTH, 2 * QK_PREP_WG_PER_CU) void qk_prep_operands_k
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, l4 = lane >> 4;
     const int K = a.K;
-    const int bi = wave & 3, bj0 = (wave >> 2) * 2;  // Gram blocks of this wave: (bi, bj0), (bi, bj0 + 1)
+    // Gram blocks of this wave: the 10 upper 16 x 16 blocks (the partials keep no others) dealt so each
+    // SIMD (waves s and s + 4) issues at most 3 Gram MFMAs per k-step plus, on the B side, wave s's probe
+    // block U(s) — round 4 gave every wave 2 of all 16 blocks: 4-5 MFMAs per SIMD and k-step. Waves 0-3
+    // take the diagonal block (s, s), whose row block is also U's operand; waves 4-7 the off-diagonal ones.
+    //   SIMD 0: (0,0) | (0,1) (0,2)    SIMD 1: (1,1) | (0,3) (1,2)    SIMD 2: (2,2) | (1,3)    SIMD 3: (3,3) | (2,3)
+    int gi0, gj0, gi1 = -1, gj1 = -1;
+    switch (wave) {
+        case 4: gi0 = 0, gj0 = 1, gi1 = 0, gj1 = 2; break;
+        case 5: gi0 = 0, gj0 = 3, gi1 = 1, gj1 = 2; break;
+        case 6: gi0 = 1, gj0 = 3; break;
+        case 7: gi0 = 2, gj0 = 3; break;
+        default: gi0 = gj0 = wave; break;
+    }
+    gi0 = __builtin_amdgcn_readfirstlane(gi0), gj0 = __builtin_amdgcn_readfirstlane(gj0);
+    gi1 = __builtin_amdgcn_readfirstlane(gi1), gj1 = __builtin_amdgcn_readfirstlane(gj1);
     const int wave_s = __builtin_amdgcn_readfirstlane(wave);
     for (int sd = 0; sd < 2; ++sd) {
         const PrepSide& S = a.s[sd];
@@ -228,15 +242,26 @@ __global__ __launch_bounds__(PTH, 2 * QK_PREP_WG_PER_CU) void qk_prep_operands_k
 #pragma unroll
                     for (int j = 0; j < PPB; ++j) pxn[j] = pp[4 * (s8 + PPB + j)];
                 }
+                if (wave < 4) {  // (s, s) and, on the B side, U(s): one operand read serves all three
 #pragma unroll
-                for (int j = 0; j < PPB; ++j) {
-                    const int c = 4 * (s8 + j) + l4;
-                    const double av = L.x[16 * bi + l16][c];
-                    const double b0 = L.x[16 * bj0 + l16][c];
-                    const double b1 = L.x[16 * (bj0 + 1) + l16][c];
-                    g0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0, g0, 0, 0, 0);
-                    g1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b1, g1, 0, 0, 0);
-                    if (probes) u = __builtin_amdgcn_mfma_f64_16x16x4f64(av, px[j], u, 0, 0, 0);  // waves 0-3: bi == wave
+                    for (int j = 0; j < PPB; ++j) {
+                        const double av = L.x[16 * gi0 + l16][4 * (s8 + j) + l4];
+                        g0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, av, g0, 0, 0, 0);
+                        if (probes) u = __builtin_amdgcn_mfma_f64_16x16x4f64(av, px[j], u, 0, 0, 0);
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < PPB; ++j) {
+                        const int c = 4 * (s8 + j) + l4;
+                        const double a0 = L.x[16 * gi0 + l16][c];
+                        const double b0 = L.x[16 * gj0 + l16][c];
+                        g0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, g0, 0, 0, 0);
+                        if (gi1 >= 0) {
+                            const double a1 = gi1 == gi0 ? a0 : L.x[16 * gi1 + l16][c];
+                            const double b1 = L.x[16 * gj1 + l16][c];
+                            g1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, g1, 0, 0, 0);
+                        }
+                    }
                 }
             }
             // ---- X tile to HBM: wave w stores rows 8w .. 8w+7, one contiguous 1-KiB row per
@@ -260,8 +285,8 @@ __global__ __launch_bounds__(PTH, 2 * QK_PREP_WG_PER_CU) void qk_prep_operands_k
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
             const int e = (l4 + 4 * rr) * 16 + l16;  // (row, column) inside the 16 x 16 block
-            if (bi <= bj0) p[prep_tri(bi, bj0) * 256 + e] = g0[rr];
-            if (bi <= bj0 + 1) p[prep_tri(bi, bj0 + 1) * 256 + e] = g1[rr];
+            p[prep_tri(gi0, gj0) * 256 + e] = g0[rr];
+            if (gi1 >= 0) p[prep_tri(gi1, gj1) * 256 + e] = g1[rr];
             if (sd == 1 && wave < 4) p[PPG + (16 * wave + l4 + 4 * rr) * PNP + l16] = u[rr];
         }
     }
