@@ -12,7 +12,8 @@
 // the instance rows), the tile goes to LDS once, and the same workgroup adds the tile's Gram block
 // (and, on the B side, its probe products) into register accumulators. Per-workgroup partial sums
 // go to a workspace that qk_prep_reduce_kernel sums in workgroup order (deterministic, no atomics).
-// Bound: fp64 MFMA (syc 32 5: 2.7 GFLOP of transforms + 1.2 of Grams / probes, 0.23 GB of HBM).
+// Bound: fp64 MFMA and the stage loads' latency (syc 32 5 after row pruning, 65 swept rows per side: 1.1
+// GFLOP of transforms + 0.8 of Grams (the 10 upper 16 x 16 blocks) and probe products, ~0.2 GB of HBM).
 // qk_compress_kernel forms A'' / B'' (one column per thread, T in LDS): HBM-bound on reading X.
 //
 // The acceptance check (qk_probe_errors / qk_probe_accept) runs on the real operands, as the probe
