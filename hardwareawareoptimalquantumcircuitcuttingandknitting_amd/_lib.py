@@ -98,6 +98,11 @@ SIGNATURES = {
                                      c_vp]),
     "qk_compress_operands_ld": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,
                                         c_vp, c_i64, c_i64, c_vp, c_i64]),
+    "qk_compress_probe_v": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp,
+                                    c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64]),
+    "qk_probe_errors_vpart": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp,
+                                      c_i64, c_vp, c_vp, ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp, c_i64,
+                                      c_vp]),
     "qk_probe_workspace_bytes": (c_i32, [c_vp, c_i64, ctypes.POINTER(c_i64)]),
     "qk_probe_errors": (c_i32, [c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64,
                                 c_i64, c_vp, c_i64, c_vp, c_vp, ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp,

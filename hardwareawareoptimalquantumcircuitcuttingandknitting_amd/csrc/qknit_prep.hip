@@ -502,6 +502,128 @@ __global__ __launch_bounds__(64) void qk_compress_cols_kernel(int K, int rmax, c
 constexpr int PV_GRID = 128;  // workgroups of the V = B'' P^T partial sums (probe_d sums their partials)
 constexpr int PV_PART = 8 * 16;  // doubles per V partial: rows j < 8 (rmax <= 8), 16 probes
 
+// Compression with the probe check's V pass fused in (round 5): the column kernel's arithmetic (a lane: two
+// adjacent columns over all K rows, T from LDS) in 4-wave workgroups of 512 columns; the first nA_wg
+// workgroups take A's columns, the rest B's, and a B workgroup also forms its V partial
+// vpart[b][j][p] = sum over its columns of B2[j][c] P[p][c] from the B2 values still in registers: each
+// wave's 8 x 128 block goes through LDS into 16x16x4 f64 MFMAs against its 128 probe columns, and the
+// four waves' sums are added in a fixed order. Replaces qk_probe_v_kernel's second read of B2 and its
+// launch.
+constexpr int CV_COLS = 512;  // columns per workgroup (4 waves x 128)
+__global__ __launch_bounds__(256) void qk_compress_v_kernel(int K, int rmax, const double* __restrict__ TA,
+                                                            const double* __restrict__ XA, int64_t NA, int64_t ldxa,
+                                                            double* __restrict__ A2, int64_t lda2,
+                                                            const double* __restrict__ TB,
+                                                            const double* __restrict__ XB, int64_t NB, int64_t ldxb,
+                                                            double* __restrict__ B2, int64_t ldb2,
+                                                            const double* __restrict__ P, int64_t ldp,
+                                                            double* __restrict__ vpart, int nA_wg) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool bs = (int)blockIdx.x >= nA_wg;  // uniform per workgroup
+    const int64_t wg = bs ? (int64_t)blockIdx.x - nA_wg : (int64_t)blockIdx.x;
+    const double* Tg = bs ? TB : TA;
+    const double* X = bs ? XB : XA;
+    double* out = bs ? B2 : A2;
+    const int64_t N = bs ? NB : NA, ld = bs ? ldxb : ldxa, ldo = bs ? ldb2 : lda2;
+    const int64_t base = wg * CV_COLS + wave * 128;
+    const int64_t c = base + 2 * lane;
+    const bool valid = c < N;
+    const int64_t cl = valid ? c : N - 2;  // loads of lanes past the end: the last column pair
+    __shared__ __attribute__((aligned(16))) double Tt[PK][8];
+    __shared__ __attribute__((aligned(16))) double Bt[4][8][128 + 2];  // each wave's B2 block (B side)
+    __shared__ double Vw[4][PV_PART];
+    d2_t acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = (d2_t){0.0, 0.0};
+    d2_t buf[2][PCW];
+    auto load = [&](int ch, d2_t (&b)[PCW]) {
+#pragma unroll
+        for (int u = 0; u < PCW; ++u) {
+            const int k = min(ch * PCW + u, K - 1);
+            b[u] = *reinterpret_cast<const d2_t*>(X + (int64_t)k * ld + cl);
+        }
+    };
+    const int nch = (K + PCW - 1) / PCW;
+    {
+        double tv[2];  // T^T [PK][8]: 512 entries, two per thread
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int e = tid + 256 * i, k = e >> 3, j = e & 7;
+            tv[i] = Tg[min(j, rmax - 1) * K + min(k, K - 1)];
+        }
+        if (base < N) load(0, buf[0]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int e = tid + 256 * i, k = e >> 3, j = e & 7;
+            Tt[k][j] = (k < K && j < rmax) ? tv[i] : 0.0;
+        }
+    }
+    __syncthreads();
+    if (base < N) {  // wave-uniform: the wave has columns
+#pragma unroll
+        for (int ch = 0; ch < PK / PCW; ++ch) {
+            if (ch >= nch) break;
+            if (ch + 1 < nch) load(ch + 1, buf[(ch + 1) & 1]);
+#pragma unroll
+            for (int u = 0; u < PCW; ++u) {
+                const int k = ch * PCW + u;
+                double t[8];
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    const d2_t tv = *reinterpret_cast<const d2_t*>(&Tt[k][2 * h]);
+                    t[2 * h] = tv.x;
+                    t[2 * h + 1] = tv.y;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    acc[j].x = fma(t[j], buf[ch & 1][u].x, acc[j].x);
+                    acc[j].y = fma(t[j], buf[ch & 1][u].y, acc[j].y);
+                }
+            }
+        }
+        if (valid) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < rmax) *reinterpret_cast<d2_t*>(out + (int64_t)j * ldo + c) = acc[j];
+        }
+    }
+    if (!bs) return;  // uniform per workgroup: no barrier below is split
+    // ---- V partial of this workgroup's columns
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const d2_t v = (valid && j < rmax) ? acc[j] : (d2_t){0.0, 0.0};
+        *reinterpret_cast<d2_t*>(&Bt[wave][j][2 * lane]) = v;
+    }
+    __syncthreads();
+    const int i16 = lane & 15, k4 = lane >> 4;
+    d4_t va = {0.0, 0.0, 0.0, 0.0};
+    if (base < N) {
+        // B operand: P[p = i16][base + 4 s + k4]; 8 steps of loads in flight per batch
+        constexpr int VB = 8;
+        const double* pr = P + (int64_t)i16 * ldp;
+#pragma unroll
+        for (int s0 = 0; s0 < 32; s0 += VB) {
+            double pb[VB];
+#pragma unroll
+            for (int s = 0; s < VB; ++s) {
+                const int64_t col = base + 4 * (s0 + s) + k4;
+                pb[s] = col < N ? pr[col] : 0.0;
+            }
+#pragma unroll
+            for (int s = 0; s < VB; ++s) {
+                const double a = i16 < 8 ? Bt[wave][i16][4 * (s0 + s) + k4] : 0.0;
+                va = __builtin_amdgcn_mfma_f64_16x16x4f64(a, pb[s], va, 0, 0, 0);
+            }
+        }
+    }
+    // C layout: row j = k4 + 4 r, column p = i16; rows j < 8 are r = 0, 1
+#pragma unroll
+    for (int r = 0; r < 2; ++r) Vw[wave][(k4 + 4 * r) * 16 + i16] = va[r];
+    __syncthreads();
+    if (tid < PV_PART)
+        vpart[wg * PV_PART + tid] = (Vw[0][tid] + Vw[1][tid]) + (Vw[2][tid] + Vw[3][tid]);
+}
+
 // V partials: vpart[b][j][p] = sum over this workgroup's columns c of B2[j][c] P[p][c] (j < rmax), on the
 // VALU: a lane takes one column per iteration (every load a coalesced 512-B row segment), wave w the
 // probes 4w..4w+3, acc[j][q] in registers; then a wave reduction and one store per (j, p). The MFMA form
@@ -1368,6 +1490,56 @@ int qk_compress_operands_ld(qk_ctx* ctx, int K, int rmax, const double* TA, cons
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return fail(ctx, QK_EHIP, (std::string("qk_compress_operands: ") + hipGetErrorString(e)).c_str());
+    return QK_OK;
+}
+
+int qk_compress_probe_v(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, int64_t ldxa,
+                        double* A2, int64_t lda2, const double* TB, const double* XB, int64_t NB, int64_t ldxb,
+                        double* B2, int64_t ldb2, const double* probes, int64_t ldp, double* vpart,
+                        int64_t vpart_doubles) {
+    if (!ctx) return QK_EARG;
+    if (K < 1 || K > PK || rmax < 1 || rmax > 8 || NA < 2 || NB < 2 || (NA | NB | ldxa | lda2 | ldxb | ldb2) & 1)
+        return fail(ctx, QK_EARG, "qk_compress_probe_v: need 1 <= K <= 64, 1 <= rmax <= 8, even widths and strides");
+    if (ldxa < NA || lda2 < NA || ldxb < NB || ldb2 < NB || ldp < NB)
+        return fail(ctx, QK_EARG, "qk_compress_probe_v: leading dimension below the width");
+    if (!TA || !XA || !A2 || !TB || !XB || !B2 || !probes || !vpart)
+        return fail(ctx, QK_EARG, "qk_compress_probe_v: null buffer");
+    if ((reinterpret_cast<uintptr_t>(XA) | reinterpret_cast<uintptr_t>(XB) | reinterpret_cast<uintptr_t>(A2) |
+         reinterpret_cast<uintptr_t>(B2)) & 15)
+        return fail(ctx, QK_EARG, "qk_compress_probe_v: operands must be 16-B aligned");
+    const int64_t ga = (NA + CV_COLS - 1) / CV_COLS, gb = (NB + CV_COLS - 1) / CV_COLS;
+    if (vpart_doubles < gb * PV_PART) return fail(ctx, QK_EARG, "qk_compress_probe_v: vpart too small");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_compress_probe_v: hipSetDevice");
+    hipLaunchKernelGGL(qk_compress_v_kernel, dim3((unsigned)(ga + gb)), dim3(256), 0, ctx->stream, K, rmax, TA, XA, NA,
+                       ldxa, A2, lda2, TB, XB, NB, ldxb, B2, ldb2, probes, ldp, vpart, (int)ga);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(ctx, QK_EHIP, (std::string("qk_compress_probe_v: ") + hipGetErrorString(e)).c_str());
+    return QK_OK;
+}
+
+int qk_probe_errors_vpart(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx, int64_t NA, const double* A2,
+                          int64_t lda2, const double* U, const double* vpart, int64_t gv, double* e2,
+                          const int32_t* r_dev, double tol, double rel_tol, int32_t* k_out, double* err_out,
+                          double* work, int64_t work_bytes, int64_t* tally) {
+    if (!ctx) return QK_EARG;
+    if (K < 1 || K > PK || rmax < 1 || rmax > 8 || NA < 16 || NA % 16 || gv < 1)
+        return fail(ctx, QK_EARG, "qk_probe_errors_vpart: need 1 <= K <= 64, 1 <= rmax <= 8, NA % 16 == 0, gv >= 1");
+    if (!XA || !A2 || !U || !vpart || !work || (k_out && !r_dev) || (tally && !k_out))
+        return fail(ctx, QK_EARG, "qk_probe_errors_vpart: null buffer");
+    if (ldx < NA) return fail(ctx, QK_EARG, "qk_probe_errors_vpart: leading dimension");
+    const int gd = probe_grid_d(ctx, NA);
+    if (work_bytes < (int64_t)(PV_GRID * PV_PART + gd * PE) * (int64_t)sizeof(double))
+        return fail(ctx, QK_EARG, "qk_probe_errors_vpart: workspace too small (qk_probe_workspace_bytes)");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, QK_EHIP, "qk_probe_errors_vpart: hipSetDevice");
+    double* epart = work + PV_GRID * PV_PART;
+    hipLaunchKernelGGL(qk_probe_d_kernel, dim3(gd), dim3(256), 0, ctx->stream, K, rmax, XA, ldx, NA, A2, lda2, U, vpart,
+                       (int)gv, epart);
+    hipLaunchKernelGGL(qk_probe_accept_kernel, dim3(1), dim3(256), 0, ctx->stream, epart, gd, r_dev, tol, rel_tol, e2,
+                       k_out, err_out, tally);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(ctx, QK_EHIP, (std::string("qk_probe_errors_vpart: ") + hipGetErrorString(e)).c_str());
     return QK_OK;
 }
 

@@ -1212,9 +1212,48 @@ def compress_operands(ctx: Context, TA, XA, TB, XB, a_cols: tuple | None = None,
     return A2, B2
 
 
+CV_COLS = 512  # qk_compress_probe_v: columns of B per V partial
+
+
+def compress_probe_v(ctx: Context, TA, XA, TB, XB, probes, a_cols: tuple | None = None, a_width: int | None = None):
+    """``qk_compress_probe_v``: ``(A2, B2, vpart)`` — :func:`compress_operands` (same arithmetic per column,
+    ``a_cols`` / ``a_width`` alike) with the probe check's V partials of B2 against ``probes`` formed in
+    the same launch ([ceil(NB / 512), 8, 16]); :func:`probe_errors` takes them as ``vpart``."""
+    T = torch()
+    rmax, K = TA.shape
+    assert TB.shape == (rmax, K) and XA.shape[0] == K and XB.shape[0] == K
+    assert XA.stride(1) == 1 and XB.is_contiguous() and TA.is_contiguous() and TB.is_contiguous()
+    NA = XA.shape[1] if a_width is None else a_width
+    NB = XB.shape[1]
+    assert probes.is_contiguous() and probes.shape == (N_PROBES, NB)
+    ab = T.empty(rmax * (NA + NB), dtype=T.float64, device=XA.device)
+    A2 = ab[:rmax * NA].view(rmax, NA)
+    B2 = ab[rmax * NA:].view(rmax, NB)
+    base, n = (0, NA) if a_cols is None else a_cols
+    assert 0 <= base and n >= 1 and base + n <= NA and XA.shape[1] in (n, NA)
+    src = XA.data_ptr() if XA.shape[1] == n else XA.data_ptr() + 8 * base
+    if a_cols is not None and POISON_UNUSED:
+        A2.fill_(float("nan"))
+    gv = -(-NB // CV_COLS)
+    vpart = T.empty((gv, 8, N_PROBES), dtype=T.float64, device=XA.device)
+    ctx.check(ctx.lib.qk_compress_probe_v(ctx.handle, K, rmax, TA.data_ptr(), src, n, XA.stride(0),
+                                          A2.data_ptr() + 8 * base, NA, TB.data_ptr(), XB.data_ptr(), NB, NB,
+                                          B2.data_ptr(), NB, probes.data_ptr(), NB, vpart.data_ptr(), vpart.numel()),
+              "qk_compress_probe_v")
+    return A2, B2, vpart
+
+
+def compress_probe_v_ok(XA, XB, a_cols=None) -> bool:
+    """Whether qk_compress_probe_v takes these operands (even widths and strides, 16-B aligned)."""
+    n = XA.shape[1] if a_cols is None else a_cols[1]
+    base = 0 if a_cols is None or XA.shape[1] == n else a_cols[0]
+    return (n % 2 == 0 and XB.shape[1] % 2 == 0 and XA.stride(0) % 2 == 0 and base % 2 == 0
+            and (XA.data_ptr() + 8 * base) % 16 == 0 and XB.data_ptr() % 16 == 0)
+
+
 _PROBE_WORK: dict = {}
 def probe_errors(ctx: Context, XA, A2, U, B2, probes, r=None, tol: float = 0.0, a2_cols: tuple | None = None,
-                 rel_tol: float = 0.0, tally=None):
+                 rel_tol: float = 0.0, tally=None, vpart=None):
     """``qk_probe_errors``: ``e2`` ([32]) = the squared probe errors of the compressed knit ([:16]) and the
     squared reference products ``||R p||^2`` ([16:]) over the columns of ``XA`` ([K, NA]); ``A2`` ([rmax, *])
     holds those columns at ``a2_cols = (offset, count)`` of its rows (default: all). ``U = XB probes^T`` and
@@ -1241,6 +1280,13 @@ def probe_errors(ctx: Context, XA, A2, U, B2, probes, r=None, tol: float = 0.0, 
     err = T.empty(1, dtype=T.float64, device=dev) if r is not None else None
     # tally (device int64[4], with r): the step's data-rank statistics updated by the accept kernel itself
     assert tally is None or (r is not None and tally.dtype == T.int64 and tally.numel() == 4)
+    if vpart is not None:  # V partials from qk_compress_probe_v: no pass over B2 and the probes here
+        assert vpart.is_contiguous() and vpart.shape[1:] == (8, N_PROBES)
+        ctx.check(ctx.lib.qk_probe_errors_vpart(ctx.handle, K, rmax, XA.data_ptr(), XA.stride(0), NA,
+                                                A2.data_ptr() + 8 * off, A2.shape[1], U.data_ptr(), vpart.data_ptr(),
+                                                vpart.shape[0], e2.data_ptr(), _ptr(r), tol, rel_tol, _ptr(k), _ptr(err),
+                                                work.data_ptr(), work.numel() * 8, _ptr(tally)), "qk_probe_errors_vpart")
+        return e2, k, err
     ctx.check(ctx.lib.qk_probe_errors_tally(ctx.handle, K, rmax, XA.data_ptr(), XA.stride(0), NA, A2.data_ptr() + 8 * off,
                                             A2.shape[1], U.data_ptr(), B2.data_ptr(), NB, NB, probes.data_ptr(), NB,
                                             e2.data_ptr(), _ptr(r), tol, rel_tol, _ptr(k), _ptr(err), work.data_ptr(),

@@ -349,9 +349,16 @@ class HipBackend:
 
     fuses_tally = True  # probe_errors(..., tally=) updates the data-rank statistics in its accept kernel
 
-    def probe_errors(self, XA, A2, U, B2, probes, r=None, tol=0.0, a2_cols=None, rel_tol=0.0, tally=None):
+    def probe_errors(self, XA, A2, U, B2, probes, r=None, tol=0.0, a2_cols=None, rel_tol=0.0, tally=None, vpart=None):
         return engine.probe_errors(self.ctx, XA, A2, U, B2, probes, r=r, tol=tol, a2_cols=a2_cols, rel_tol=rel_tol,
-                                   tally=tally)
+                                   tally=tally, vpart=vpart)
+
+    def compress_v(self, TA, XA, TB, XB, probes, a_cols=None, a_width=None):
+        """(A2, B2, vpart): the compression with the probe check's V pass fused in, or None where
+        qk_compress_probe_v does not take the operands."""
+        if os.environ.get("QKNIT_COMPRESS_V", "1") == "0" or not engine.compress_probe_v_ok(XA, XB, a_cols):
+            return None
+        return engine.compress_probe_v(self.ctx, TA, XA, TB, XB, probes, a_cols=a_cols, a_width=a_width)
 
     def probe_accept(self, e2, r, tol, rel_tol=0.0):
         return engine.probe_accept(self.ctx, e2, r, tol, rel_tol)
@@ -1083,12 +1090,32 @@ class KnitPipeline:
                 # verdict, as each rank's rows in the sharded check. The Grams and factors stay whole, so
                 # every rank's compressed values are the single-GPU ones bit for bit
                 base, n = a_cols
-                A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib], a_cols=a_cols)
-                XAc = mats[ia][:, base:base + n]
                 kw = {"tally": self._tally_for(r.device)} if getattr(self.be, "fuses_tally", False) else {}
+                cv = self.be.compress_v(TA, mats[ia], TB, mats[ib], x, a_cols=a_cols) \
+                    if hasattr(self.be, "compress_v") else None
+                if cv is not None:  # the V pass of the check inside the compression
+                    A2, B2, kw["vpart"] = cv
+                else:
+                    A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib], a_cols=a_cols)
+                XAc = mats[ia][:, base:base + n]
                 _, k_eff, _ = self.be.probe_errors(XAc, A2, U, B2, x, r=r, tol=self.rank_tol, a2_cols=a_cols,
                                                    rel_tol=self.rank_tol_rel, **kw)
                 if kw:
+                    self._pending += 1
+                else:
+                    self._note_rank(r, k_eff)
+                return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
+            cv = None
+            if not self.spec_write and hasattr(self.be, "compress_v"):
+                cv = self.be.compress_v(TA, mats[ia], TB, mats[ib], x)  # the check's V pass fused in
+            if cv is not None:
+                A2, B2, vp = cv
+                kw = {"vpart": vp}
+                if getattr(self.be, "fuses_tally", False):
+                    kw["tally"] = self._tally_for(r.device)
+                _, k_eff, _ = self.be.probe_errors(mats[ia], A2, U, B2, x, r=r, tol=self.rank_tol,
+                                                   rel_tol=self.rank_tol_rel, **kw)
+                if "tally" in kw:
                     self._pending += 1
                 else:
                     self._note_rank(r, k_eff)

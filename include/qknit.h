@@ -367,6 +367,21 @@ int qk_compress_operands_ld(qk_ctx* ctx, int K, int rmax, const double* TA, cons
                             double* A2, int64_t lda2, const double* TB, const double* XB, int64_t NB, int64_t ldxb,
                             double* B2, int64_t ldb2);
 
+/* qk_compress_operands_ld with the probe check's V pass fused in: also vpart[b][j][p] = sum over the b-th
+ * 512-column block of B of B2[j][c] probes[p][c] (j < 8, rows >= rmax zero; ceil(NB / 512) blocks of 128
+ * doubles), which qk_probe_errors_vpart takes instead of reading B2 and the probes again. Even widths and
+ * leading dimensions, 16-B aligned operands. */
+int qk_compress_probe_v(qk_ctx* ctx, int K, int rmax, const double* TA, const double* XA, int64_t NA, int64_t ldxa,
+                        double* A2, int64_t lda2, const double* TB, const double* XB, int64_t NB, int64_t ldxb,
+                        double* B2, int64_t ldb2, const double* probes, int64_t ldp, double* vpart,
+                        int64_t vpart_doubles);
+
+/* qk_probe_errors_tally from qk_compress_probe_v's gv V partials (no B2 / probes pass of its own). */
+int qk_probe_errors_vpart(qk_ctx* ctx, int K, int rmax, const double* XA, int64_t ldx, int64_t NA, const double* A2,
+                          int64_t lda2, const double* U, const double* vpart, int64_t gv, double* e2,
+                          const int32_t* r_dev, double tol, double rel_tol, int32_t* k_out, double* err_out,
+                          double* work, int64_t work_bytes, int64_t* tally);
+
 /* Acceptance check of a compressed knit on the real operands (the probe products of the torch form,
  * not materialised): e2[p] = ||(X_A^T X_B - A2^T B2) P_p||^2 and e2[16 + p] = ||X_A^T X_B P_p||^2
  * (the reference product, ~||R||_F^2), summed over the NA columns of X_A given (X_A: [K][ldx], A2:

@@ -1189,6 +1189,46 @@ def test_compress_operands_matches_torch(T, K, NA, NB, rmax):
         assert A2c.shape == A2.shape and T.equal(A2c[:, base:base + n], A2[:, base:base + n]) and T.equal(B2c, B2)
 
 
+@pytest.mark.parametrize("K,NA,NB,rmax,a_cols", [(64, 65536, 65536, 8, None), (64, 65536, 65536, 8, (8192, 8192)),
+                                                  (24, 4096, 2052, 3, None), (17, 2048, 132, 8, (512, 1024)),
+                                                  (64, 1024, 8192, 1, None), (6, 128, 512, 2, (0, 64))])
+def test_compress_probe_v_matches_separate_passes(T, K, NA, NB, rmax, a_cols):
+    """qk_compress_probe_v (the compression with the probe check's V pass fused in) against the separate
+    passes: A2 / B2 bit for bit those of qk_compress_operands(_ld) (same arithmetic per column), and the
+    probe check from its V partials (qk_probe_errors_vpart) equal to qk_probe_errors' within 1e-12 —
+    ragged widths (not multiples of the 512-column blocks), K below 64, rmax below 8, a column range
+    of A given as a window of X_A and as its own [K, n] block."""
+    ctx = engine.get_context(0)
+    g = T.Generator(device="cuda").manual_seed(K + NA + NB + rmax)
+    TA, TB = (T.randn(rmax, K, dtype=T.float64, device="cuda", generator=g) for _ in range(2))
+    XA = T.randn(K, NA, dtype=T.float64, device="cuda", generator=g)
+    XB = T.randn(K, NB, dtype=T.float64, device="cuda", generator=g)
+    P = T.randn(16, NB, dtype=T.float64, device="cuda", generator=g)
+    U = XB @ P.T
+    r = T.tensor([rmax], dtype=T.int32, device="cuda")
+    A2, B2 = engine.compress_operands(ctx, TA, XA, TB, XB, a_cols=a_cols)
+    A2v, B2v, vp = engine.compress_probe_v(ctx, TA, XA, TB, XB, P, a_cols=a_cols)
+    base, n = (0, NA) if a_cols is None else a_cols
+    T.cuda.synchronize()
+    assert T.equal(A2v[:, base:base + n], A2[:, base:base + n]) and T.equal(B2v, B2)
+    assert vp.shape == (-(-NB // 512), 8, 16)
+    ref = (B2 @ P.T).cpu()
+    assert float((vp.sum(dim=0)[:rmax].cpu() - ref).abs().max()) <= 1e-12 * float(ref.abs().max())
+    if rmax < 8:  # rows past the rank are zero
+        assert float(vp[:, rmax:].abs().max()) == 0.0
+    XAc = XA[:, base:base + n]
+    e2, k, err = engine.probe_errors(ctx, XAc, A2, U, B2, P, r=r, tol=1e300, a2_cols=None if a_cols is None else a_cols)
+    e2v, kv, errv = engine.probe_errors(ctx, XAc, A2v, U, B2v, P, r=r, tol=1e300,
+                                        a2_cols=None if a_cols is None else a_cols, vpart=vp)
+    T.cuda.synchronize()
+    assert int(k) == int(kv) == rmax
+    assert float((e2v - e2).abs().max()) <= 1e-12 * float(e2.abs().max())
+    if a_cols is not None and n % 2 == 0:  # X_A's columns as their own [K, n] block
+        A2w, _, vpw = engine.compress_probe_v(ctx, TA, XAc.contiguous(), TB, XB, P, a_cols=a_cols, a_width=NA)
+        T.cuda.synchronize()
+        assert T.equal(A2w[:, base:base + n], A2[:, base:base + n]) and T.equal(vpw, vp)
+
+
 @pytest.mark.parametrize("K,ra,rb,r,noise", [(64, 8, 8, 2, 0.0), (64, 5, 12, 4, 0.0), (64, 20, 20, 8, 0.0),
                                              (64, 8, 8, 2, 1e-9), (24, 3, 3, 3, 0.0)])
 def test_probe_check_and_compress(T, K, ra, rb, r, noise):
