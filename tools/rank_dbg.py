@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase clocks of qk_rank_factors on the syc 32 5 Grams (QK_RANK_DEBUG variant build:
-QKNIT_LIB=tools/variants/lib_rankdbg.so). Prints cholesky / core+Jacobi / rank+factors microseconds
-(wall_clock64 at 100 MHz), the Jacobi sweep count and the pivot counts."""
+QKNIT_LIB=tools/variants/lib_rankdbg.so). Prints the phase times in microseconds
+(wall_clock64 at 100 MHz: Gram load, pivoted Cholesky, core, LU, factors) and the pivot counts."""
 import ctypes
 import os
 import sys
@@ -26,10 +26,11 @@ def main():
         pipe.be.rank_factors(G[0], G[1])
         torch.cuda.synchronize()
         lib.qk_rank_debug(out)
-        t = [out[i] for i in range(4)]
-        print({"gram_load_us": (out[4] - t[0]) / 100, "cholesky_us": (t[1] - t[0]) / 100, "jacobi_us": (t[2] - t[1]) / 100, "factors_us": (t[3] - t[2]) / 100,
-               "sweeps": out[5], "ra": out[6], "rb": out[7]}, flush=True)
-
+        s0, s1, s2, s3, s4, s5 = (out[i] for i in range(6))  # RK_STAMP(i): 0 start, 4 Grams loaded,
+        # 1 Cholesky done, 2 core done, 5 LU done, 3 end (wall_clock64 at 100 MHz)
+        print({"gram_load_us": (s4 - s0) / 100, "cholesky_us": (s1 - s4) / 100, "core_us": (s2 - s1) / 100,
+               "lu_us": (s5 - s2) / 100, "factors_us": (s3 - s5) / 100, "total_us": (s3 - s0) / 100,
+               "ra": out[6], "rb": out[7]}, flush=True)
 
 if __name__ == "__main__":
     main()
