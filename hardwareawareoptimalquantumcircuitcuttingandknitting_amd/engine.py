@@ -229,9 +229,12 @@ OUT_MAPPED_MIN_BYTES = int(os.environ.get("QKNIT_OUT_MAPPED_MIN_BYTES", str(1 <<
 # (so its memory cannot come straight back), up to OUT_TRIES, the fastest kept and the others freed.
 # Extra tries only with free memory for them (2 GiB spare): a 2^32 output holds at most OUT_TRIES x
 # 34 GB for the few milliseconds of the selection.
-# (only full 2^32 outputs: a rank's slice of it writes at 5.7-6.9 TB/s into every buffer, by its size,
-# tools/slice_write_bench.py, so the threshold would reject good buffers there)
-OUT_SELECT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_SELECT_MIN_BYTES", str(24 << 30)))
+# From 4 GiB on (round 5; before: full 2^32 outputs only): a rank's slice writes at 5.6-6.3 TB/s by the
+# same check, below the threshold, so each slice buffer is the fastest of OUT_TRIES mappings — and the
+# pipelined multi-GPU step gains from it on every box measured: 8 ranks 0.776-0.816 vs 0.839-0.870 ms,
+# 4 ranks 1.39-1.41 vs 1.64, 2 ranks 2.52-2.53 vs 2.62 (profiles/r05ar_*, r05as_*). A slice buffer is
+# held by a pipelined step for the run, so the milliseconds of the selection are a plan-time cost.
+OUT_SELECT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_SELECT_MIN_BYTES", str(4 << 30)))
 OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "6850"))
 OUT_TRIES = int(os.environ.get("QKNIT_OUT_TRIES", "3"))
 out_selections: list = []  # per selected output: the candidates' write rates (GB/s), the kept one first

@@ -56,7 +56,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting, engine
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
 
     name, n, d, p, variant = cutting.BASELINE_CONFIGS[args.workload]
@@ -204,6 +204,7 @@ def main():
         M, N, K = pipe.gemm_shape()
         print(json.dumps({"workload": args.workload, "mode": pipe.mode, "prep": pipe.slice_prep,
                           "cost_model_ms": pipe.slice_costs, "out_buffers": pipe.out_buffers,
+                          "out_selections": list(engine.out_selections),
                           "world": world, "rank": args.rank,
                           "slice": list(pipe.slice), "ms_per_step_no_xgmi": round(ms, 3), "host_ms_per_step": round(host / args.steps * 1e3, 3), "drain_ms": round(drain * 1e3, 3),
                           "sweep_ms": round(sweep, 3), "prep_ms": round(prep, 3), "knit_ms": round(knit, 3),
