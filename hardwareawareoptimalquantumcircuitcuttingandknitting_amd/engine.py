@@ -225,8 +225,8 @@ OUT_MAPPED_MIN_BYTES = int(os.environ.get("QKNIT_OUT_MAPPED_MIN_BYTES", str(1 <<
 # for every store order tried (task widths 2^12-2^16, compact or spread windows, other grids), for
 # 1-GiB-aligned and unaligned addresses, chunks created per buffer or all first (tools/write_probe11-13,
 # out_mapping_tb.py). qk_out_write_rate times the knit's store order into a new mapping
-# (one 5-ms launch for 34 GB); below OUT_FAST_GBS another mapping is made while the slow one is held
-# (so its memory cannot come straight back), up to OUT_TRIES, the fastest kept and the others freed.
+# (one 5-ms launch for 34 GB); below OUT_FAST_GBS another mapping is made while the earlier ones are held
+# (so their memory cannot come straight back), up to OUT_TRIES, the fastest kept and the others freed.
 # Extra tries only with free memory for them (2 GiB spare): a 2^32 output holds at most OUT_TRIES x
 # 34 GB for the few milliseconds of the selection.
 # From 4 GiB on (round 5; before: full 2^32 outputs only): a rank's slice writes at 5.6-6.3 TB/s by the
@@ -235,7 +235,11 @@ OUT_MAPPED_MIN_BYTES = int(os.environ.get("QKNIT_OUT_MAPPED_MIN_BYTES", str(1 <<
 # 4 ranks 1.39-1.41 vs 1.64, 2 ranks 2.52-2.53 vs 2.62 (profiles/r05ar_*, r05as_*). A slice buffer is
 # held by a pipelined step for the run, so the milliseconds of the selection are a plan-time cost.
 OUT_SELECT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_SELECT_MIN_BYTES", str(4 << 30)))
-OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "6850"))
+# Early-stop rate: a candidate at least this fast is kept at once. Default: none (every one of OUT_TRIES
+# candidates is made and the fastest kept) — one GPU, same box, three alternating rounds: 4.948-4.967 vs
+# 4.964-4.982 ms per step with a 6850 GB/s stop (profiles/r05av_*); the extra candidates cost ~20 ms
+# at plan time and, for the milliseconds of the selection, their memory (2 GiB spare required)
+OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "inf"))
 OUT_TRIES = int(os.environ.get("QKNIT_OUT_TRIES", "3"))
 out_selections: list = []  # per selected output: the candidates' write rates (GB/s), the kept one first
 _out_select_lock = threading.Lock()  # one selection at a time per process: two threads' candidates never stack
