@@ -1083,43 +1083,8 @@ class KnitPipeline:
             x = self._probes(qs[ib].shape[1], qs[ib].device)
             mats, G, U = self._prep_fused(qs, x)
             TA, TB, r = self.be.rank_factors(G[0], G[1])
-            a_cols = self._replicated_a_cols()
-            if a_cols is not None:
-                # replicated slice: this rank's output slice reads only A columns [base, base + n) (rows
-                # of R): it compresses those and checks those rows against every probe — its own slice's
-                # verdict, as each rank's rows in the sharded check. The Grams and factors stay whole, so
-                # every rank's compressed values are the single-GPU ones bit for bit
-                base, n = a_cols
-                kw = {"tally": self._tally_for(r.device)} if getattr(self.be, "fuses_tally", False) else {}
-                cv = self.be.compress_v(TA, mats[ia], TB, mats[ib], x, a_cols=a_cols) \
-                    if hasattr(self.be, "compress_v") else None
-                if cv is not None:  # the V pass of the check inside the compression
-                    A2, B2, kw["vpart"] = cv
-                else:
-                    A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib], a_cols=a_cols)
-                XAc = mats[ia][:, base:base + n]
-                _, k_eff, _ = self.be.probe_errors(XAc, A2, U, B2, x, r=r, tol=self.rank_tol, a2_cols=a_cols,
-                                                   rel_tol=self.rank_tol_rel, **kw)
-                if kw:
-                    self._pending += 1
-                else:
-                    self._note_rank(r, k_eff)
-                return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
-            cv = None
-            if not self.spec_write and hasattr(self.be, "compress_v"):
-                cv = self.be.compress_v(TA, mats[ia], TB, mats[ib], x)  # the check's V pass fused in
-            if cv is not None:
-                A2, B2, vp = cv
-                kw = {"vpart": vp}
-                if getattr(self.be, "fuses_tally", False):
-                    kw["tally"] = self._tally_for(r.device)
-                _, k_eff, _ = self.be.probe_errors(mats[ia], A2, U, B2, x, r=r, tol=self.rank_tol,
-                                                   rel_tol=self.rank_tol_rel, **kw)
-                if "tally" in kw:
-                    self._pending += 1
-                else:
-                    self._note_rank(r, k_eff)
-                return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
+            if not self.spec_write:
+                return self._compress_and_check(TA, TB, r, mats, U, x)
             A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib])
             if self.spec_write and getattr(self.be, "dev", None) is not None and self.be.dev.type == "cuda":
                 # speculative write: the write runs at the factored rank r while the probe check runs
@@ -1156,6 +1121,37 @@ class KnitPipeline:
         TA, TB, r = self.be.rank_factors(G[0].contiguous(), G[1].contiguous())
         A2, B2 = (TA @ A).contiguous(), (TB @ B).contiguous()
         k_eff, _ = self._accept(A, B, A2, B2, self._probes(B.shape[1], B.device), r)
+        return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
+
+    def _compress_and_check(self, TA, TB, r, mats, U, x) -> dict:
+        """The fused chain's compression and probe check (no speculative write): the compressed operands
+        and the accepted rank of a prepared step. With the backend's fused form (compress_v) the check's V
+        pass runs inside the compression. A replicated slice rank reads only A columns [base, base + n)
+        (rows of R): it compresses those and checks those rows against every probe — its own slice's
+        verdict, as each rank's rows in the sharded check; the Grams and factors stay whole, so its
+        compressed values are the single-GPU ones bit for bit."""
+        ia, ib = self.order[0], self.order[-1]
+        a_cols = self._replicated_a_cols()
+        kw = {"a_cols": a_cols} if a_cols is not None else {}
+        cv = self.be.compress_v(TA, mats[ia], TB, mats[ib], x, **kw) if hasattr(self.be, "compress_v") else None
+        check = {}
+        if cv is not None:
+            A2, B2, check["vpart"] = cv
+        else:
+            A2, B2 = self.be.compress(TA, mats[ia], TB, mats[ib], **kw)
+        XA = mats[ia]
+        if a_cols is not None:
+            XA = XA[:, a_cols[0]:a_cols[0] + a_cols[1]]
+            check["a2_cols"] = a_cols
+        tally = getattr(self.be, "fuses_tally", False)  # the statistics in the accept kernel: one launch fewer
+        if tally:
+            check["tally"] = self._tally_for(r.device)
+        _, k_eff, _ = self.be.probe_errors(XA, A2, U, B2, x, r=r, tol=self.rank_tol, rel_tol=self.rank_tol_rel,
+                                           **check)
+        if tally:
+            self._pending += 1
+        else:
+            self._note_rank(r, k_eff)
         return {"A2": A2, "B2": B2, "k_eff": k_eff, "mats": mats}
 
     def _kernel_name(self, K, cA, cB, o_begin=0, o_count=None):
