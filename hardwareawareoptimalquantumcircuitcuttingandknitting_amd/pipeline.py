@@ -1322,9 +1322,11 @@ class KnitPipeline:
         if self._prep_stream is None:
             T = self.T
             dev = self.be.dev.index or 0
-            # 8+ ranks: 128 preparation CUs (the replicated sweep + chain on 96 left the write waiting:
-            # 0.82-0.86 vs 0.82-0.85 ms per step with three buffers, profiles/r05j_*), else PREP_CUS
-            env = os.environ.get("QKNIT_PREP_CUS", str(128 if self.world >= 8 else self.PREP_CUS))
+            # 4+ ranks: 128 preparation CUs (the replicated sweep + chain on 96 left the write waiting: 8
+            # ranks 0.82-0.86 vs 0.82-0.85 ms per step with three buffers, profiles/r05j_*; 4 ranks
+            # 1.319-1.322 vs 1.349-1.378 ms, r05az_*), 2 ranks PREP_CUS (2.533-2.546 vs 2.545-2.561 at 128,
+            # r05ba_*)
+            env = os.environ.get("QKNIT_PREP_CUS", str(128 if self.world >= 4 else self.PREP_CUS))
             total = engine.device_cu_count(dev)
             if env == "all":
                 # no CU split: both streams may use every CU (their own hardware queues); the write's
