@@ -235,11 +235,12 @@ OUT_MAPPED_MIN_BYTES = int(os.environ.get("QKNIT_OUT_MAPPED_MIN_BYTES", str(1 <<
 # 4 ranks 1.39-1.41 vs 1.64, 2 ranks 2.52-2.53 vs 2.62 (profiles/r05ar_*, r05as_*). A slice buffer is
 # held by a pipelined step for the run, so the milliseconds of the selection are a plan-time cost.
 OUT_SELECT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_SELECT_MIN_BYTES", str(4 << 30)))
-# Early-stop rate: a candidate at least this fast is kept at once. Default: none (every one of OUT_TRIES
-# candidates is made and the fastest kept) — one GPU, same box, three alternating rounds: 4.948-4.967 vs
-# 4.964-4.982 ms per step with a 6850 GB/s stop (profiles/r05av_*); the extra candidates cost ~20 ms
-# at plan time and, for the milliseconds of the selection, their memory (2 GiB spare required)
-OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "inf"))
+# Early-stop rate: a candidate at least this fast is kept at once. QKNIT_OUT_FAST_GBS=inf makes every one
+# of OUT_TRIES candidates and keeps the fastest — one GPU, same box, three alternating rounds: 4.948-4.967
+# vs 4.964-4.982 ms per step (profiles/r05av_*). Not the default: the first run that did so in a process
+# stepping 2- then 4-rank slice pipelines (tools/rank_sim.py --world 2 4 8) ended in a memory-access fault
+# reported at a write-rate check, cause not found (r05bb); the 6850 stop ran that sequence clean (r05at)
+OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "6850"))
 OUT_TRIES = int(os.environ.get("QKNIT_OUT_TRIES", "3"))
 out_selections: list = []  # per selected output: the candidates' write rates (GB/s), the kept one first
 _out_select_lock = threading.Lock()  # one selection at a time per process: two threads' candidates never stack

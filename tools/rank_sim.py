@@ -217,6 +217,10 @@ def main():
                           "host_phase_ms": {k: round(v / args.steps * 1e3, 3) for k, v in host_phase.items()}}),
               flush=True)
         del pipe
+        import gc
+
+        gc.collect()  # this world's output mappings go now (synchronised), not at a later collection
+        torch.cuda.synchronize()
         torch.cuda.empty_cache()
 
 
