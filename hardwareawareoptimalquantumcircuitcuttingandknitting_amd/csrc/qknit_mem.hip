@@ -77,17 +77,6 @@ void unmap_retire(void* va, OutMapping& m) {
     g_retired.emplace_back(va, m.bytes);
 }
 
-// give the retired ranges back (only when a reservation fails: the address space is exhausted)
-size_t free_retired() {
-    std::vector<std::pair<void*, size_t>> r;
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        r.swap(g_retired);
-    }
-    for (auto& x : r) (void)hipMemAddressFree(x.first, x.second);
-    return r.size();
-}
-
 }  // namespace
 
 extern "C" {
@@ -118,8 +107,11 @@ int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr) {
     // the last chunk holds only the rest (a multiple of the granularity): 1.1 GiB maps 1.1, not 2 GiB
     OutMapping m{want, ctx->device, {}};
     void* va = nullptr;
+    // A failed reservation is an error (the caller falls back to an ordinary allocation): retired ranges
+    // are never handed back, since translations of an unmapped range outlive it — round 4 kept them
+    // and released them all when a reservation failed, and a new mapping that landed on one could
+    // fault on its first write (a 2 -> 4-rank process, profiles/r05bb_*)
     e = hipMemAddressReserve(&va, m.bytes, align, nullptr, 0);
-    if (e != hipSuccess && free_retired() > 0) e = hipMemAddressReserve(&va, m.bytes, align, nullptr, 0);
     if (e != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_alloc: hipMemAddressReserve", e);
     size_t mapped = 0;
     for (size_t i = 0; i < n_chunks; ++i) {

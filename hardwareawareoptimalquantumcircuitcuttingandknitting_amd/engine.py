@@ -260,11 +260,18 @@ def out_buffer(ctx: Context, n: int):
     T = torch()
     if 8 * n < OUT_MAPPED_MIN_BYTES:
         return T.empty(n, dtype=T.float64, device=T.device("cuda", ctx.device)), None
+    try:
+        first = MappedOut(ctx, n)
+    except _lib.QknitError:
+        # no mapping (the address space of never-reused retired ranges is full, or no physical chunk):
+        # an ordinary allocation, recorded
+        out_selections.append(["torch allocation: qk_out_alloc failed"])
+        return T.empty(n, dtype=T.float64, device=T.device("cuda", ctx.device)), None
     if 8 * n < OUT_SELECT_MIN_BYTES or OUT_TRIES <= 1:
-        owner = MappedOut(ctx, n)
-        return owner.tensor(), owner
+        return first.tensor(), first
     with _out_select_lock:
-        owner = MappedOut(ctx, n)
+        owner = first
+        first = None
         tried = [(_out_rate(ctx, owner), owner)]
         while tried[-1][0] < OUT_FAST_GBS and len(tried) < OUT_TRIES:
             free, _ = T.cuda.mem_get_info(ctx.device)

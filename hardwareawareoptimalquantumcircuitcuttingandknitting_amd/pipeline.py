@@ -1714,7 +1714,8 @@ class KnitPipeline:
         out, owner = alloc(n)
         self.out_alloc = "qk_out_alloc (1-GiB mapped chunks)" if owner is not None else "torch"
         if len(engine.out_selections) > n_sel:  # candidates' write rates, the kept one first
-            self.out_alloc += f", write-rate selected: {engine.out_selections[-1]} GB/s"
+            last = engine.out_selections[-1]
+            self.out_alloc += f" ({last[0]})" if owner is None else f", write-rate selected: {last} GB/s"
         self._last_owner = owner
         if zero:
             out.zero_()

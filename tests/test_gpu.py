@@ -845,6 +845,26 @@ def test_mapped_output_buffer_steps_match_oracle(T, case, monkeypatch):
     assert pipe.take_out().data_ptr() == owner.ptr  # nothing holds it: handed out again
 
 
+def test_output_falls_back_to_an_ordinary_allocation(T, monkeypatch):
+    """A failed qk_out_alloc (address space of retired ranges full, no physical chunk): engine.out_buffer
+    hands out an ordinary torch allocation, records it, and the knit into it equals the oracle."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import _lib
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    monkeypatch.setattr(engine, "OUT_MAPPED_MIN_BYTES", 0)
+
+    class Failing(engine.MappedOut):
+        def __init__(self, ctx, n):
+            raise _lib.QknitError("qk_out_alloc failed (test)")
+
+    monkeypatch.setattr(engine, "MappedOut", Failing)
+    cut = circuits.two_fragment("cx", 8, 8, n_cuts=4)[1]
+    pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
+    got = pipe.step().cpu().numpy()
+    np.testing.assert_allclose(got, dense.run_dense(cut), atol=1e-12, rtol=0)
+    assert pipe.out_alloc.startswith("torch (torch allocation")
+
+
 def test_output_selection_keeps_fastest_and_frees_the_others(T, monkeypatch):
     """engine.out_buffer's write-rate selection (forced here on a 512-KiB output: every candidate
     tried): OUT_TRIES mappings are made and timed, the fastest is kept (its rate first in
