@@ -8,6 +8,8 @@ every cut instance of every fragment + the dense fp64 knit of the complete
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload syc_32_5_p2] [--direct]
   N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+       or plain `python bench.py --gpus N`, which starts that launcher itself as a child process
+       (WORLD_SIZE set and different from N is an error)
 
 value = reference-counted instances (sum over fragments of their label lists, run.py:37-39)
 processed per second by the whole job, timed between barriers, max over ranks.
@@ -361,7 +363,9 @@ def drop_in_timing(cut, ref_out, steps: int, device: int) -> dict:
     first = time.perf_counter() - t0
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.run import cached_plan
 
-    placement = getattr(cached_plan(virt0, device), "out_alloc", None)
+    plan0 = cached_plan(virt0, device)
+    placement = getattr(plan0, "out_alloc", None)
+    breakdown = {k: round(v, 2) for k, v in getattr(plan0, "first_call_ms", {}).items()}
     diff = 0.0
     chunk = 1 << 28
     for i in range(0, out.numel(), chunk):
@@ -395,6 +399,7 @@ def drop_in_timing(cut, ref_out, steps: int, device: int) -> dict:
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import quasi_distr
 
     return {"api": "run_virtual_circuit(virt, dense=True)", "first_call_ms": first * 1e3,
+            "first_call_breakdown_ms": breakdown,
             "dict_api": "run_virtual_circuit(virt): qk_knit_select (entries above ACCURACY only) + qk_npd_pairs",
             "dict_first_ms": dict_first * 1e3,
             "dict_steady_ms": float(sum(dict_times) / len(dict_times)) * 1e3, "dict_min_ms": min(dict_times) * 1e3,
@@ -524,8 +529,59 @@ def sweep_counters(workload: str):
     return best
 
 
+def launch_plan(gpus: int, env) -> tuple:
+    """What ``bench.py --gpus N`` does in this environment (checked before anything touches a GPU):
+    ("run", world) — this process is one rank (WORLD_SIZE set by a launcher, equal to N; or N = 1);
+    ("spawn", N) — no launcher: start N ranks as a child ``torch.distributed.run`` and relay its line
+    (the reference spreads its knit over ``Pool(processes=8)`` itself, run.py:64-67);
+    ("error", message) — a launcher's WORLD_SIZE that contradicts --gpus."""
+    if gpus < 1:
+        return ("error", f"--gpus must be >= 1, got {gpus}")
+    ws = env.get("WORLD_SIZE")
+    if ws is None or ws == "":
+        return ("spawn", gpus) if gpus > 1 else ("run", 1)
+    try:
+        world = int(ws)
+    except ValueError:
+        return ("error", f"WORLD_SIZE={ws!r} is not an integer")
+    if world != gpus:
+        return ("error", f"--gpus {gpus} but WORLD_SIZE={world}: the launcher started a different number of "
+                         f"ranks than the job asks for")
+    return ("run", world)
+
+
+def spawn_command(gpus: int, argv: list, port: int) -> list:
+    """The child launcher's command line: one process per GPU of this node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def spawn_ranks(gpus: int, argv: list) -> int:
+    """Run the N-rank bench as a child process (nothing here has touched the GPU) and relay its output;
+    returns the child's exit code. The JSON line is rank 0's (the ranks' max-over-ranks timing)."""
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = spawn_command(gpus, argv, port)
+    print(f"bench.py: no launcher, starting {gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    for line in proc.stdout:  # relay as it comes (the JSON line included)
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return proc.wait()
+
+
 def main():
     args = parse()
+    plan = launch_plan(args.gpus, os.environ)
+    if plan[0] == "error":
+        print(f"bench.py: {plan[1]}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if plan[0] == "spawn":
+        sys.exit(spawn_ranks(plan[1], sys.argv[1:]))
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -55,6 +55,7 @@ SIGNATURES = {
     "qk_out_free": (c_i32, [c_vp, c_vp]),
     "qk_out_mapped_bytes": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),
     "qk_out_write_rate": (c_i32, [c_vp, c_vp, c_i64, ctypes.POINTER(ctypes.c_double)]),
+    "qk_out_stats": (c_i32, [ctypes.POINTER(c_i64), c_i32]),
     "qk_sweep_workspace_bytes": (c_i32, [ctypes.POINTER(QkProgram), c_i64, ctypes.POINTER(c_i64)]),
     "qk_sweep": (c_i32, [c_vp, ctypes.POINTER(QkProgram), c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "qk_module_compile": (c_i32, [c_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,

@@ -2,33 +2,34 @@
 //
 // The knit's dominant kernel streams the 2^N output (syc 32: 2^32 fp64 = 34.4 GB per step) from
 // persistent workgroups, each writing its own 512-KiB task. Into a plain hipMalloc buffer that write
-// is bimodal: 4.83-4.87 ms into some allocations, 5.8-6.0 ms into others on the same box, while a
-// store order with one short-lived workgroup per 4 KiB is ~4.9 ms into every one of them
-// (tools/write_probe2..8). Composing the same 34 GB from 1-GiB physical allocations (hipMemCreate)
-// mapped at 1-GiB-aligned virtual addresses makes every buffer fast — 4.83-4.86 ms for 24 buffers
-// covering all 280 GB of the device in order, interleaved and permuted (tools/write_probe10) — so the
-// slow mode follows the virtual-to-physical mapping (the translation granularity a hipMalloc block
-// happens to get), not the physical memory. qk_out_alloc maps every large output this way. Later
-// probes (round 4) found the slow mode in such mappings too once several are made, so
-// for full 2^32 outputs engine.out_buffer still times a new mapping's write rate (qk_out_write_rate)
-// and keeps the fastest of at most three.
+// is bimodal: 4.83-4.87 ms into some allocations, 5.8-6.0 ms into others on the same box
+// (tools/write_probe2..8). Composing the output from 1-GiB physical allocations (hipMemCreate) mapped
+// into a reserved range made every buffer fast in one probe (tools/write_probe10), but later probes
+// found the slow mode in such mappings too once several are made in a process, so
+// engine.out_buffer times every new mapping of 4 GiB or more (a full 2^32 output or a multi-GPU
+// rank's slice) with qk_out_write_rate and keeps the fastest of at most three.
 //
 //   qk_out_alloc(ctx, bytes, &ptr)  device memory of at least `bytes`, 1-GiB physical chunks (the
-//                                   last rounded up to the allocation granularity) mapped
-//                                   read-write for ctx's device at a 1-GiB-aligned address;
-//                                   below 1 GiB one chunk at an alignment of its power-of-two size
+//                                   last holds only the rest, a multiple of the granularity) mapped
+//                                   read-write for ctx's device; below 1 GiB one chunk at an
+//                                   alignment of its power-of-two size
 //   qk_out_write_rate(ctx, p, n, &gbs)  GB/s of the knit's static store order over [p, p + n) (one
-//                                   timed launch after a warm one; the contents are overwritten)
+//                                   timed launch after a warm one; the contents are overwritten).
+//                                   It first drains the device: an error left by earlier work is
+//                                   reported as "pre-existing", not as the probe's own
 //   qk_out_free(ctx, ptr)           synchronizes the device, unmaps, releases the physical chunks;
 //                                   the virtual range stays reserved (retired, never mapped again)
+//   qk_out_stats(out, n)            process counters: reservations made / failed, live and retired
+//                                   ranges and bytes, the largest reservation
 //
 // Retired ranges: a freed range whose addresses were reserved again for the next mapping read back
 // wrong — 32-KiB runs of a live small mapping came back as zeros after other mappings had been freed
 // and re-reserved (tools/diag/mapped_loop.py: 44 of 60 drop-in calls on cx_8x8 with 512-KiB outputs;
 // none while no mapping was ever freed, tools/diag/mapped_read.py), i.e. translations of the old
 // mapping outlived it. So a freed range's addresses are never handed out again: the physical memory
-// goes back at once, the address range (not memory) only when a reservation fails (the 47-bit
-// device address space holds thousands of 34-GB outputs).
+// goes back at once, the address range never. A reservation that fails is an error, and the caller
+// (engine.out_buffer) falls back to an ordinary allocation with a warning. The device's reservable
+// address space was measured with tools/va_probe.py (profiles/r06*_va_probe.json): see DESIGN.md §4.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -51,6 +52,14 @@ struct OutMapping {
 std::mutex g_mu;
 std::map<uintptr_t, OutMapping> g_maps;
 std::vector<std::pair<void*, size_t>> g_retired;  // unmapped ranges kept reserved (see above)
+
+// process counters (qk_out_stats), under g_mu
+struct OutStats {
+    int64_t reserved = 0, reserve_failed = 0, map_failed = 0;  // hipMemAddressReserve calls ok / failed; chunk map failures
+    int64_t live = 0, live_bytes = 0, retired = 0, retired_bytes = 0, max_bytes = 0;
+    int64_t probe_pre_errors = 0;  // qk_out_write_rate calls that found an error left by earlier work
+};
+OutStats g_stats;
 
 constexpr size_t OUT_CHUNK = size_t(1) << 30;
 
@@ -75,6 +84,10 @@ void unmap_retire(void* va, OutMapping& m) {
     for (auto h : m.chunks) (void)hipMemRelease(h);
     std::lock_guard<std::mutex> lk(g_mu);
     g_retired.emplace_back(va, m.bytes);
+    g_stats.live -= 1;
+    g_stats.live_bytes -= (int64_t)m.bytes;
+    g_stats.retired += 1;
+    g_stats.retired_bytes += (int64_t)m.bytes;
 }
 
 }  // namespace
@@ -112,6 +125,11 @@ int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr) {
     // and released them all when a reservation failed, and a new mapping that landed on one could
     // fault on its first write (a 2 -> 4-rank process, profiles/r05bb_*)
     e = hipMemAddressReserve(&va, m.bytes, align, nullptr, 0);
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (e != hipSuccess) g_stats.reserve_failed += 1;
+        else g_stats.reserved += 1;
+    }
     if (e != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_alloc: hipMemAddressReserve", e);
     size_t mapped = 0;
     for (size_t i = 0; i < n_chunks; ++i) {
@@ -125,7 +143,11 @@ int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr) {
         if (e != hipSuccess) {
             (void)hipMemUnmap(va, mapped);
             for (auto hh : m.chunks) (void)hipMemRelease(hh);
-            (void)hipMemAddressFree(va, m.bytes);
+            (void)hipMemAddressFree(va, m.bytes);  // never mapped whole: nothing to outlive
+            {
+                std::lock_guard<std::mutex> lk(g_mu);
+                g_stats.map_failed += 1;
+            }
             return mem_fail(ctx, QK_EHIP, "qk_out_alloc: hipMemCreate / hipMemMap", e);
         }
         m.chunks.push_back(h);
@@ -141,6 +163,9 @@ int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr) {
     }
     {
         std::lock_guard<std::mutex> lk(g_mu);
+        g_stats.live += 1;
+        g_stats.live_bytes += (int64_t)m.bytes;
+        if ((int64_t)m.bytes > g_stats.max_bytes) g_stats.max_bytes = (int64_t)m.bytes;
         g_maps[(uintptr_t)va] = std::move(m);
     }
     *ptr = va;
@@ -181,6 +206,27 @@ int qk_out_write_rate(qk_ctx* ctx, void* ptr, int64_t bytes, double* gbs) {
         return mem_fail(ctx, QK_EARG, "qk_out_write_rate: need a context, a buffer of >= 512 KiB, an out pointer", hipSuccess);
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_write_rate: hipSetDevice", e);
+    // Drain the device first: an error that earlier asynchronous work left (a fault in another stream's
+    // kernel) would otherwise surface at this call's event wait and read as the probe's own
+    e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess) {
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            g_stats.probe_pre_errors += 1;
+        }
+        return mem_fail(ctx, QK_EHIP, "qk_out_write_rate: pre-existing error (earlier work, before the probe)", e);
+    }
+    {  // the probe's grid covers exactly [ptr, ptr + 512 KiB * nblocks): the range must be one live mapping
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_maps.upper_bound((uintptr_t)ptr);
+        bool inside = false;
+        if (it != g_maps.begin()) {
+            --it;
+            inside = (uintptr_t)ptr + (uintptr_t)bytes <= it->first + it->second.bytes;
+        }
+        if (!inside) return mem_fail(ctx, QK_EARG, "qk_out_write_rate: range is not inside a live qk_out_alloc mapping", hipSuccess);
+    }
     const int64_t nblocks = bytes >> 19;
     hipEvent_t t0, t1;
     if ((e = hipEventCreate(&t0)) != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_write_rate: event", e);
@@ -193,13 +239,25 @@ int qk_out_write_rate(qk_ctx* ctx, void* ptr, int64_t bytes, double* gbs) {
     (void)hipEventRecord(t0, ctx->stream);
     hipLaunchKernelGGL(qk_out_probe_kernel, grid, dim3(256), 0, ctx->stream, (double*)ptr, nblocks);
     (void)hipEventRecord(t1, ctx->stream);
-    e = hipEventSynchronize(t1);
+    e = hipGetLastError();  // launch errors
+    if (e == hipSuccess) e = hipEventSynchronize(t1);
     float ms = 0.0f;
     if (e == hipSuccess) e = hipEventElapsedTime(&ms, t0, t1);
     (void)hipEventDestroy(t0);
     (void)hipEventDestroy(t1);
     if (e != hipSuccess) return mem_fail(ctx, QK_EHIP, "qk_out_write_rate", e);
     *gbs = ms > 0 ? (double)(nblocks << 19) / (ms * 1e6) : 0.0;
+    return QK_OK;
+}
+
+int qk_out_stats(int64_t* out, int n) {
+    if (!out || n <= 0) return QK_EARG;
+    std::lock_guard<std::mutex> lk(g_mu);
+    const int64_t v[] = {g_stats.reserved, g_stats.reserve_failed, g_stats.map_failed, g_stats.live,
+                         g_stats.live_bytes, g_stats.retired, g_stats.retired_bytes, g_stats.max_bytes,
+                         g_stats.probe_pre_errors};
+    const int m = (int)(sizeof v / sizeof v[0]);
+    for (int i = 0; i < n; ++i) out[i] = i < m ? v[i] : 0;
     return QK_OK;
 }
 

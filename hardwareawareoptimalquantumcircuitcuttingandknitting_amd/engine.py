@@ -18,6 +18,7 @@ Pipeline of one virtual-circuit run (``run.py:23-71`` in the reference):
 from __future__ import annotations
 
 import atexit
+import contextlib
 import ctypes
 import dataclasses
 import hashlib
@@ -235,15 +236,35 @@ OUT_MAPPED_MIN_BYTES = int(os.environ.get("QKNIT_OUT_MAPPED_MIN_BYTES", str(1 <<
 # 4 ranks 1.39-1.41 vs 1.64, 2 ranks 2.52-2.53 vs 2.62 (profiles/r05ar_*, r05as_*). A slice buffer is
 # held by a pipelined step for the run, so the milliseconds of the selection are a plan-time cost.
 OUT_SELECT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_SELECT_MIN_BYTES", str(4 << 30)))
-# Early-stop rate: a candidate at least this fast is kept at once. QKNIT_OUT_FAST_GBS=inf makes every one
-# of OUT_TRIES candidates and keeps the fastest — one GPU, same box, three alternating rounds: 4.948-4.967
-# vs 4.964-4.982 ms per step (profiles/r05av_*). Not the default: the first run that did so in a process
-# stepping 2- then 4-rank slice pipelines (tools/rank_sim.py --world 2 4 8) ended in a memory-access fault
-# reported at a write-rate check, cause not found (r05bb); the 6850 stop ran that sequence clean (r05at)
+# Early-stop rate: a candidate at least this fast is kept at once (the others are made only while the
+# candidates so far are slower). Slice buffers of a 2-8-rank step write at 5.6-6.3 TB/s, below it, so
+# for them every one of OUT_TRIES candidates is made and the fastest kept (the early stop acts only on
+# full 2^32 outputs). QKNIT_OUT_FAST_GBS=inf does the same for every output: one GPU, same box, three
+# alternating rounds 4.948-4.967 vs 4.964-4.982 ms per step (profiles/r05av_*). Round 5 saw one
+# memory-access fault reported at a write-rate check with inf in a 2 -> 4-rank rank_sim process
+# (r05bb); qk_out_write_rate now drains the device first and says when an error predates its probe,
+# and qk_out_stats counts reservations (DESIGN.md §4 for what the reruns found)
 OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "6850"))
 OUT_TRIES = int(os.environ.get("QKNIT_OUT_TRIES", "3"))
 out_selections: list = []  # per selected output: the candidates' write rates (GB/s), the kept one first
 _out_select_lock = threading.Lock()  # one selection at a time per process: two threads' candidates never stack
+
+
+OUT_STATS_FIELDS = ("reserved", "reserve_failed", "map_failed", "live", "live_bytes", "retired", "retired_bytes",
+                    "max_bytes", "probe_pre_errors")
+
+
+def out_stats() -> dict:
+    """qk_out_alloc's process counters (``qk_out_stats``): reservations made / failed, live and retired
+    mappings and bytes, the largest mapping, write-rate checks that found an earlier error."""
+    L = _lib.lib()
+    v = (ctypes.c_int64 * len(OUT_STATS_FIELDS))()
+    if L.qk_out_stats(v, len(OUT_STATS_FIELDS)) != 0:
+        raise _lib.QknitError("qk_out_stats failed")
+    return dict(zip(OUT_STATS_FIELDS, (int(x) for x in v)))
+
+
+_out_fallback_warned = [False]
 
 
 def _out_rate(ctx: Context, owner) -> float:
@@ -262,10 +283,16 @@ def out_buffer(ctx: Context, n: int):
         return T.empty(n, dtype=T.float64, device=T.device("cuda", ctx.device)), None
     try:
         first = MappedOut(ctx, n)
-    except _lib.QknitError:
+    except _lib.QknitError as e:
         # no mapping (the address space of never-reused retired ranges is full, or no physical chunk):
-        # an ordinary allocation, recorded
+        # an ordinary allocation, recorded — and said once, since its write rate is the buffer lottery's
         out_selections.append(["torch allocation: qk_out_alloc failed"])
+        if not _out_fallback_warned[0]:
+            _out_fallback_warned[0] = True
+            import warnings
+
+            warnings.warn(f"qk_out_alloc failed ({e}); large outputs fall back to torch allocations "
+                          f"(out_stats: {out_stats()})", RuntimeWarning, stacklevel=2)
         return T.empty(n, dtype=T.float64, device=T.device("cuda", ctx.device)), None
     if 8 * n < OUT_SELECT_MIN_BYTES or OUT_TRIES <= 1:
         return first.tensor(), first
@@ -853,8 +880,33 @@ def fold_traced(ctx: Context, x, fold: int):
     return reduce_labels(ctx, x.contiguous().view(rows * fold, w // fold), off, rows)
 
 
+@contextlib.contextmanager
+def host_planning():
+    """Context of the host side of planning: endpoint side programs memoised for the plan
+    (``fragment_program.planning_memo``) and the BLAS pool held to one thread. The plan's matrices are
+    tiny (the two-fragment core is 64 x 256), and a multi-threaded OpenBLAS spends 0.25-0.55 s on that
+    one SVD spinning up its pool against 2.5 ms on one thread (measured in the build container)."""
+    from .fragment_program import planning_memo
+
+    with contextlib.ExitStack() as st:
+        st.enter_context(planning_memo())
+        try:
+            from threadpoolctl import threadpool_limits
+
+            st.enter_context(threadpool_limits(1, user_api="blas"))
+        except ImportError:  # threadpoolctl absent: planning still works, only slower
+            pass
+        yield
+
+
 def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = True,
                       basis: bool = False, jit: bool | None = None, relevance: bool = True) -> list[FragmentState]:
+    with host_planning():
+        return _prepare_fragments(virt, device, upload, dedup, basis, jit, relevance)
+
+
+def _prepare_fragments(virt, device: int, upload: bool, dedup: bool, basis: bool, jit: bool | None,
+                       relevance: bool) -> list[FragmentState]:
     """Compile every fragment, dedup its instances and expand them into branch jobs.
 
     ``basis=True`` (factored knit only) additionally sweeps a spanning set of instances
@@ -988,6 +1040,11 @@ def _affine_stride(clbits: list):
 
 
 def knit_operands(virt, frags: list[FragmentState], factored: bool = False, compress: bool = True) -> KnitOperands:
+    with host_planning():
+        return _knit_operands(virt, frags, factored, compress)
+
+
+def _knit_operands(virt, frags: list[FragmentState], factored: bool, compress: bool) -> KnitOperands:
     vg = [v.operation for v in virt.vgate_instructions]
     space = LabelSpace([g.num_instantiations for g in vg], [g.knit_coefficients() for g in vg])
     clbits = [[] if fs.dropped else list(fs.prog.clbits) for fs in frags]

@@ -30,7 +30,7 @@ import numpy as np
 
 from . import gates as _g
 from .circuit import CompositeInstruction
-from .virtual_gates import VirtualGateEndpoint
+from .virtual_gates import VirtualGateEndpoint, _memoised, planning_memo  # noqa: F401 (planning_memo re-exported)
 
 P0 = np.array([[1, 0], [0, 0]], dtype=np.complex128)
 P1 = np.array([[0, 0], [0, 1]], dtype=np.complex128)
@@ -264,11 +264,21 @@ class BranchMeasure:
         self.clbit = clbit
 
 
+def side_program(endpoint, inst_id: int):
+    """``endpoint.side_circuit(inst_id)``, memoised inside :func:`planning_memo`."""
+    return _memoised("side", endpoint, inst_id, lambda: endpoint.side_circuit(inst_id))
+
+
 def side_branches(endpoint, inst_id: int) -> list[tuple[np.ndarray, float]]:
     """Branches ``(matrix, sign)`` of one endpoint side for instantiation ``inst_id``."""
     if isinstance(endpoint, BranchMeasure):
         return [(P0.copy(), 1.0), (P1.copy(), 1.0)]
-    side = endpoint.side_circuit(inst_id)
+    got = _memoised("branches", endpoint, inst_id, lambda: _side_branches(endpoint, inst_id))
+    return [(m.copy(), sg) for m, sg in got]
+
+
+def _side_branches(endpoint, inst_id: int) -> list[tuple[np.ndarray, float]]:
+    side = side_program(endpoint, inst_id)
     pre, post, measured = I2.copy(), I2.copy(), False
     for instr in side.data:
         name = instr.operation.name
@@ -292,7 +302,7 @@ def side_branches(endpoint, inst_id: int) -> list[tuple[np.ndarray, float]]:
 def _side_signature(endpoint, inst_id: int) -> tuple:
     if isinstance(endpoint, BranchMeasure):
         return ("branch",)
-    side = endpoint.side_circuit(inst_id)
+    side = side_program(endpoint, inst_id)
     return tuple((ins.operation.name, tuple(round(float(p), 15) for p in getattr(ins.operation, "params", ())))
                  for ins in side.data)
 
@@ -456,13 +466,16 @@ def basis_reduce(prog: FragmentProgram, unique_labels: list, tol: float = 1e-12,
         labels.append(tuple(lab))
     if sum(_label_jobs(prog, lab, nb_cache) for lab in labels) >= jobs_now:
         return None
-    expand = np.zeros((len(unique_labels), n_basis))
-    for u, lab in enumerate(unique_labels):
-        row = np.ones(1)
-        for s, (_, coef) in zip(prog.slots, per_slot):
-            row = np.kron(row, coef[0 if isinstance(s.endpoint, BranchMeasure) else int(lab[s.vgate_idx])])
-        expand[u] = row
-    return BasisReduction(labels, expand)
+    # expand[u] = kron over slots of the label's coefficient rows, as a row-wise Khatri-Rao product
+    # (the same products in the same order as a per-label np.kron loop: bit-identical)
+    expand = np.ones((len(unique_labels), 1))
+    for s, (_, coef) in zip(prog.slots, per_slot):
+        if isinstance(s.endpoint, BranchMeasure):
+            C = np.broadcast_to(coef[0], (len(unique_labels), len(coef[0])))
+        else:
+            C = np.stack([coef[int(lab[s.vgate_idx])] for lab in unique_labels])
+        expand = (expand[:, :, None] * C[:, None, :]).reshape(len(unique_labels), -1)
+    return BasisReduction(labels, np.ascontiguousarray(expand))
 
 
 def _label_jobs(prog: FragmentProgram, label, cache: dict) -> int:

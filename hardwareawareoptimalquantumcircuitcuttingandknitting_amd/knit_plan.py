@@ -75,7 +75,9 @@ class LabelSpace:
 
 # ----------------------------------------------------------------------------- factored knit
 def _signature(endpoint, inst_id: int) -> tuple:
-    side = endpoint.side_circuit(inst_id)
+    from .fragment_program import side_program
+
+    side = side_program(endpoint, inst_id)
     sig = []
     for instr in side.data:
         op = instr.operation

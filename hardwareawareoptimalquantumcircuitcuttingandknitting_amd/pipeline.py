@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+from time import perf_counter
 
 import numpy as np
 
@@ -420,8 +421,15 @@ class KnitPipeline:
         kw = {} if light_cone else {"relevance": False}
         if jit is not None:
             kw["jit"] = jit
-        self.frags = self.be.prepare_fragments(virt, basis=factored, **kw)
-        self.ops = engine.knit_operands(virt, self.frags, factored, compress=light_cone)
+        # host time of each planning phase (ms; device work inside a phase is included only where
+        # the phase waits for it): the drop-in's first-call breakdown (bench.py drop_in)
+        self.plan_ms = {}
+        tick = perf_counter()
+        with engine.host_planning():
+            self.frags = self.be.prepare_fragments(virt, basis=factored, **kw)
+            tick = self._phase("prepare_fragments", tick)
+            self.ops = engine.knit_operands(virt, self.frags, factored, compress=light_cone)
+            tick = self._phase("knit_operands", tick)
         self.N = virt.circuit.num_clbits
         q_bytes = sum(len(fs.labels) << fs.prog.m for fs in self.frags) * 8
         out_bytes = (1 << self.N) * 8
@@ -530,6 +538,12 @@ class KnitPipeline:
         self.slice_costs = None  # the cost model's per-step estimates (ms) of both, when it chose
         self._plan()
 
+    def _phase(self, name: str, since: float) -> float:
+        """Record ``perf_counter() - since`` as planning phase ``name`` (ms); returns the new mark."""
+        now = perf_counter()
+        self.plan_ms[name] = self.plan_ms.get(name, 0.0) + (now - since) * 1e3
+        return now
+
     def _stream_bits(self):
         """(clbits of the row side, of the column side) when two live fragments partition the output
         bits with clbit 0 on the column side (the streaming knit applies), else (None, None)."""
@@ -560,7 +574,9 @@ class KnitPipeline:
         L = self.ops.num_terms
         self.term_range = _shard(L, self.rank, self.world) if self.mode == "reduce" else (0, L)
         self.place = {}  # gather mode: fragment -> position of each swept row in the gathered rows
+        tick = perf_counter()
         pruned = self._prune_rows()
+        tick = self._phase("row_pruning", tick)
         swept = [self._swept_rows(i, fs, pruned.get(i)) for i, fs in enumerate(self.frags)]
         if self.mode == "slice":
             self.slice_prep, self.slice_costs = self._choose_slice_prep(swept)
@@ -619,10 +635,13 @@ class KnitPipeline:
                                           else alloc((max(rows, 1), width), T.float64)),
                                     q=alloc((max(rows, 1), width), T.float64) if branching else None,
                                     ws=be.empty((max(need, 1),), T.uint8)))
+        tick = self._phase("job_tables", tick)
         self._plan_knit()
         if self.sharded:
             self._plan_exchange()
+        tick = self._phase("knit_tables", tick)
         self._plan_multi()
+        self._phase("sweep_launch_plan", tick)
 
     def _prune_rows(self) -> dict:
         """{fragment: kept swept rows} of the row pruning (ROW_PRUNE, PRUNE_TOL): two live fragments
@@ -1716,6 +1735,11 @@ class KnitPipeline:
         if len(engine.out_selections) > n_sel:  # candidates' write rates, the kept one first
             last = engine.out_selections[-1]
             self.out_alloc += f" ({last[0]})" if owner is None else f", write-rate selected: {last} GB/s"
+        if owner is not None:
+            st = engine.out_stats()
+            self.out_alloc += (f"; process: {st['reserved']} reservations ({st['reserve_failed']} failed), "
+                               f"{st['live']} live, {st['retired']} retired "
+                               f"({st['retired_bytes'] / 2**30:.0f} GiB of address space)")
         self._last_owner = owner
         if zero:
             out.zero_()

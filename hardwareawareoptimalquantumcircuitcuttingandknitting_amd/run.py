@@ -238,9 +238,11 @@ def _planned_dense(virt: VirtualCircuit, device: int, out):
     T = engine.torch()
     now = perf_counter()
     pipe = cached_plan(virt, device)
+    t_plan = perf_counter()
     pipe.be.bind()
     if out is None:  # 1-GiB-mapped when large; the previous call's mapping once the caller dropped it
         out = pipe.take_out()
+    t_out = perf_counter()
     e0, e1 = T.cuda.Event(enable_timing=True), T.cuda.Event(enable_timing=True)
     host = perf_counter() - now
     e0.record()
@@ -254,6 +256,12 @@ def _planned_dense(virt: VirtualCircuit, device: int, out):
         pipe.out = None
     _sync(device)
     wall = perf_counter() - now
+    if not pipe.plan_reused and not hasattr(pipe, "first_call_ms"):
+        # where the first call's time goes: the plan's phases (KnitPipeline.plan_ms), the output buffer
+        # (mapping + write-rate selection), the step itself (launches + device time to the sync)
+        pipe.first_call_ms = {"plan": (t_plan - now) * 1e3, **{f"plan.{k}": v for k, v in pipe.plan_ms.items()},
+                              "output_buffer": (t_out - t_plan) * 1e3, "step": (now + wall - t_out) * 1e3,
+                              "total": wall * 1e3}
     pipe.sync_stats()
     run_time = host + e0.elapsed_time(e1) * 1e-3
     return out, RunTimeInfo(run_time, max(wall - run_time, 0.0)), pipe

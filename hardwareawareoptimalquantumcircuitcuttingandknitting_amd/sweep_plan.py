@@ -48,21 +48,34 @@ PASS_INIT, PASS_FINAL = 1, 2
 
 
 # ----------------------------------------------------------------------------- analysis
-def _diag_qubits(op: HostOp) -> set:
-    """Qubits on which the op acts diagonally (it commutes with Z there)."""
+_Z0 = np.array([1, -1, 1, -1], dtype=np.float64)  # 4x4 little-endian on (q0, q1): index b0 + 2 b1
+_Z1 = np.array([1, 1, -1, -1], dtype=np.float64)
+_DIAG_MEMO: dict = {}
+
+
+def _diag_qubits(op: HostOp) -> frozenset:
+    """Qubits on which the op acts diagonally (it commutes with Z there). Memoised on the op's
+    kind, qubits and matrix bytes: the pass scheduler asks for every op of every candidate tile
+    width (syc 32 5: ~8000 queries for ~190 ops)."""
     if op.kind == "slot":
-        return set()
-    m = op.mat
+        return frozenset()
+    m = np.asarray(op.mat)
+    key = (op.kind, tuple(op.qubits), m.dtype.str, m.shape, m.tobytes())
+    hit = _DIAG_MEMO.get(key)
+    if hit is not None:
+        return hit
     if op.kind == "u1":
-        return {op.qubits[0]} if _is_diag(m) else set()
-    out = set()
-    # 4x4 little-endian on (q0, q1): index b0 + 2 b1
-    z0 = np.diag([1, -1, 1, -1]).astype(np.complex128)
-    z1 = np.diag([1, 1, -1, -1]).astype(np.complex128)
-    if np.allclose(m @ z0, z0 @ m, atol=1e-15, rtol=0):
-        out.add(op.qubits[0])
-    if np.allclose(m @ z1, z1 @ m, atol=1e-15, rtol=0):
-        out.add(op.qubits[1])
+        out = frozenset({op.qubits[0]}) if _is_diag(m) else frozenset()
+    else:
+        # [M, Z] = 0 for diagonal Z  <=>  M[i, j] (z_j - z_i) = 0 for every entry
+        q = []
+        for z, qb in ((_Z0, op.qubits[0]), (_Z1, op.qubits[1])):
+            if np.all(np.abs(m * (z[None, :] - z[:, None])) <= 1e-15):
+                q.append(qb)
+        out = frozenset(q)
+    if len(_DIAG_MEMO) > 65536:
+        _DIAG_MEMO.clear()
+    _DIAG_MEMO[key] = out
     return out
 
 

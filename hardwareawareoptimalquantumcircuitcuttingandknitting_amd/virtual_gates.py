@@ -22,6 +22,8 @@ VirtualRZZ ``230-260``, VirtualCPhase ``299-310``. Knit rules: ``105-124``,
 from __future__ import annotations
 
 import abc
+import threading
+from contextlib import contextmanager
 from math import cos, pi, sin
 
 from .circuit import Barrier, CompositeInstruction, Gate, QuantumCircuit, QuantumRegister
@@ -29,6 +31,38 @@ from .quasi_distr import QuasiDistr
 
 #: degenerate-angle threshold of VirtualRZZ, ``virtual_gates.py:223``
 RZZ_ACCURACY = 0.00001
+
+
+_memo = threading.local()
+
+
+@contextmanager
+def planning_memo():
+    """Memoise endpoint side programs for the duration of one plan (per thread). Every query of a
+    side (``side_circuit``, its branches, its signature) otherwise rebuilds the virtual gate's
+    whole instantiation list (``virtual_gates.py:62-103,154-177``: circuits composed per call), and a
+    plan asks hundreds of times (syc 32 5: ~580 instantiation lists). Scoped to the plan: the
+    reference's gates alias their original gate's parameter list (``virtual_gates.py:22``), so a
+    side may change between plans, never within one. Nested uses share the outer memo."""
+    outer = getattr(_memo, "d", None)
+    if outer is None:
+        _memo.d = {}
+    try:
+        yield
+    finally:
+        if outer is None:
+            _memo.d = None
+
+
+def _memoised(kind: str, endpoint, inst_id: int, make):
+    d = getattr(_memo, "d", None)
+    if d is None:
+        return make()
+    key = (kind, id(endpoint), inst_id)
+    hit = d.get(key)
+    if hit is None or hit[0] is not endpoint:  # (the endpoint is held: its id is not reused meanwhile)
+        hit = d[key] = (endpoint, make())
+    return hit[1]
 
 
 def _zero_like(r):
@@ -86,7 +120,11 @@ class VirtualBinaryGate(Barrier, abc.ABC):
 
     @property
     def num_instantiations(self) -> int:
-        return len(self._instantiations())
+        return len(self._instantiation_list())
+
+    def _instantiation_list(self) -> list:
+        """``_instantiations()``, built once per plan inside :func:`planning_memo` (read-only there)."""
+        return _memoised("insts", self, 0, self._instantiations)
 
     @abc.abstractmethod
     def _instantiations(self) -> list[QuantumCircuit]:
@@ -101,7 +139,7 @@ class VirtualBinaryGate(Barrier, abc.ABC):
         """Coefficient ``a_i`` per instantiation; config-bit outcomes fold as ``(-1)^m``."""
 
     def instantiate(self, inst_id: int) -> QuantumCircuit:
-        return self._instantiations()[inst_id]
+        return self._instantiation_list()[inst_id]
 
     @staticmethod
     def _check_instantiation(inst: QuantumCircuit) -> None:

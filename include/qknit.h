@@ -110,13 +110,18 @@ const char* qk_version(void);
  * caller owns the buffer; qk_out_free synchronizes the device, unmaps it and releases its memory (its
  * address range is never handed out again). qk_out_mapped_bytes: the mapped size of a qk_out_alloc
  * pointer (QK_EARG otherwise). qk_out_write_rate: GB/s of the knit's store order into [ptr, ptr +
- * bytes) (one timed launch; overwrites the contents) — the 2^32-entry knit writes at 4.8-5.0 ms into
- * most buffers and at 5.2-5.9 ms into others, fixed per buffer, whatever the store order (DESIGN.md
- * §4), so the engine keeps a large output only if it writes fast (engine.out_buffer). */
+ * bytes) (one timed launch; overwrites the contents; the range must lie in one live qk_out_alloc
+ * mapping; the device is drained first and an error left by earlier work is reported as
+ * "pre-existing") — the 2^32-entry knit writes at 4.8-5.0 ms into most buffers and at 5.2-5.9 ms into
+ * others, fixed per buffer, whatever the store order, so the engine keeps a large
+ * output only if it writes fast (engine.out_buffer). qk_out_stats: process counters into out[0, n):
+ * reservations made, reservations failed, chunk maps failed, live mappings, live bytes, retired
+ * ranges, retired bytes, largest mapping, write-rate calls that found a pre-existing error. */
 int qk_out_alloc(qk_ctx* ctx, int64_t bytes, void** ptr);
 int qk_out_free(qk_ctx* ctx, void* ptr);
 int qk_out_mapped_bytes(const void* ptr, int64_t* bytes);
 int qk_out_write_rate(qk_ctx* ctx, void* ptr, int64_t bytes, double* gbs);
+int qk_out_stats(int64_t* out, int n);
 
 /* Workspace (bytes) qk_sweep needs for n_jobs jobs of prog (0 in PACKED mode). */
 int qk_sweep_workspace_bytes(const qk_program* prog, int64_t n_jobs, int64_t* bytes);

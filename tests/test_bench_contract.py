@@ -35,3 +35,4 @@ def test_bench_json_line_contract(require_gpu):
     assert 0 < r["achieved"] <= r["peak"] and abs(r["frac"] - r["achieved"] / r["peak"]) <= 1e-9
     # the write kernel runs inside the step
     assert r["avg_launch_ms"] <= d["ms_per_step"]
+

@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--prep", default="auto", choices=["auto", "replicated", "sharded"],
                     help="slice-mode preparation (QKNIT_SLICE_PREP): replicated = no collective at all")
     ap.add_argument("--cprofile", action="store_true", help="cProfile the timed steps (top host functions to stderr)")
+    ap.add_argument("--no-world-sync", action="store_true",
+                    help="between worlds only `del pipe` (no gc.collect / synchronize / empty_cache): the "
+                         "sequence of round 5's faulting run (profiles/r05bb_*)")
     ap.add_argument("--host-profile", action="store_true",
                     help="host time per pipeline phase (sweep / preparation / launch), to find blocking calls")
     args = ap.parse_args()
@@ -205,6 +208,7 @@ def main():
         print(json.dumps({"workload": args.workload, "mode": pipe.mode, "prep": pipe.slice_prep,
                           "cost_model_ms": pipe.slice_costs, "out_buffers": pipe.out_buffers,
                           "out_selections": list(engine.out_selections),
+                          "out_stats": engine.out_stats(),
                           "world": world, "rank": args.rank,
                           "slice": list(pipe.slice), "ms_per_step_no_xgmi": round(ms, 3), "host_ms_per_step": round(host / args.steps * 1e3, 3), "drain_ms": round(drain * 1e3, 3),
                           "sweep_ms": round(sweep, 3), "prep_ms": round(prep, 3), "knit_ms": round(knit, 3),
@@ -217,6 +221,8 @@ def main():
                           "host_phase_ms": {k: round(v / args.steps * 1e3, 3) for k, v in host_phase.items()}}),
               flush=True)
         del pipe
+        if args.no_world_sync:
+            continue
         import gc
 
         gc.collect()  # this world's output mappings go now (synchronised), not at a later collection
