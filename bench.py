@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-north-star", action="store_true",
                     help="skip the syc 32 1 sweep-only measurement (north_star_sweep)")
+    ap.add_argument("--no-sweep-full", action="store_true",
+                    help="skip sweep_full (the direct plan's sweep of every unique instance, timed alone)")
     ap.add_argument("--cpu-sample-labels", type=int, default=12)
     ap.add_argument("--no-npd", action="store_true", help="skip the NPD timing on the 2^N output")
     ap.add_argument("--no-drop-in", action="store_true",
@@ -494,6 +496,61 @@ def north_star_sweep(steps: int) -> dict:
     return out
 
 
+def sweep_full(steps: int) -> dict:
+    """The sweep kernels at a size where HBM could matter (verdict r5, north_star "HBM GB/s on the
+    batched statevector sweep"): syc 32 5 with basis reduction, light cone and row pruning off —
+    the direct plan's sweep of every unique instance of both 16-qubit fragments with all their branch
+    jobs (2 x 625 instances of the reference's 2 x 1296, 2 x 1296 branch jobs), timed alone with HIP
+    events on the launch stream. ``algorithmic_bytes``: SURVEY.md §8d (one read + write of the
+    complex128 state per fused gate per branch job) — a model that counts every gate as a pass over
+    HBM, not a ceiling (a pass touches the state once for all of its gates). ``counters``: the
+    profiled HBM bytes (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) and fp64 VALU instructions of
+    the same sweep (profiles/*sweep_full_pmc.json, rocprofv3 --pmc passes over tools/sweep_run.py
+    --full), divided by THIS run's time: the fractions of 8 TB/s and of the 78.6 TF/s fp64 vector peak
+    that bound it."""
+    import torch
+
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    name, n, d, p, var = cutting.BASELINE_CONFIGS["syc_32_5_p2"]
+    cut = cutting.config_cut_circuit(name, n, d, p, var)[1]
+    pipe = KnitPipeline(VirtualCircuit(cut), factored=False)
+    for _ in range(2):
+        pipe.sweep()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(steps):
+        pipe.sweep()
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / steps
+    tr = pipe.sweep_traffic()
+    counts = pipe.instance_counts()
+    out = {"workload": "syc 32 5 p=2, direct plan (no basis reduction / light cone / row pruning)",
+           "instances_ref": counts["instances_ref"], "instances_swept": counts["instances_swept"],
+           "branch_jobs": counts["branch_jobs"], "ms_per_sweep": ms,
+           "hbm_bytes_model": tr["hbm"], "hbm_GBs_model": tr["hbm"] / (ms * 1e-3) / 1e9,
+           "algorithmic_bytes": tr["algorithmic"], "algorithmic_GBs": tr["algorithmic"] / (ms * 1e-3) / 1e9,
+           "fp64_flops_model": tr["flops"]}
+    cnt = sweep_counters("syc 32 5 p=2 (full sweep)", pattern="*sweep_full_pmc.json")
+    if cnt is not None:
+        src, c = cnt
+        out.update({"counters": src, "hbm_bytes": c["hbm_bytes"],
+                    "hbm_GBs": c["hbm_bytes"] / (ms * 1e-3) / 1e9,
+                    "hbm_frac": c["hbm_bytes"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "fp64_flops": c["fp64_flops"], "fp64_TFs": c["fp64_flops"] / (ms * 1e-3) / 1e12,
+                    "fp64_valu_frac": c["fp64_flops"] / (ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS})
+        for k in ("f64_issue_frac", "valu_busy_frac", "lds_bank_conflict_frac", "per_kernel"):
+            if k in c:
+                out[k] = c[k]
+        out["bound"] = ("fp64 VALU issue" if c.get("valu_busy_frac", 0) > out["hbm_frac"] else "HBM")
+    del pipe
+    torch.cuda.empty_cache()
+    return out
+
+
 def traffic_per_launch(M, N, K):
     """HBM bytes per knit-GEMM launch from the committed PMC summary (profiles/*traffic*.json,
     written by tools/pmc_traffic.py from a rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE pass of this
@@ -511,7 +568,7 @@ def traffic_per_launch(M, N, K):
     return None if best is None else best["hbm_bytes_per_launch"]
 
 
-def sweep_counters(workload: str):
+def sweep_counters(workload: str, pattern: str = "*sweep_pmc.json"):
     """Counter-measured sweep bytes / flops per step (profiles/*sweep_pmc.json, written from
     rocprofv3 --pmc passes over tools/sweep_bench.py): the HBM bytes the sweep kernels really moved
     (2 x FETCH_SIZE + WRITE_SIZE) and the fp64 flops they executed (SQ_INSTS_VALU_{ADD,MUL,FMA}_F64),
@@ -519,12 +576,12 @@ def sweep_counters(workload: str):
     import glob
 
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*sweep_pmc.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern))):
         try:
             rec = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if rec.get("workload", "").startswith(workload):
+        if rec.get("workload", "") == workload or (pattern == "*sweep_pmc.json" and rec.get("workload", "").startswith(workload)):
             best = (os.path.basename(f), rec["per_step"])
     return best
 
@@ -807,6 +864,8 @@ def main():
                                                  light_cone=not args.no_light_cone), max(2, args.steps // 4))
     if world == 1 and not args.no_north_star:
         line["north_star_sweep"] = north_star_sweep(args.steps)
+    if world == 1 and not args.no_sweep_full:
+        line["sweep_full"] = sweep_full(max(3, args.steps // 4))
     if world == 1 and not args.no_cpu_baseline:
         if qs_host is not None:
             line["cpu_baseline"] = cpu_baseline_same(pipe, cut, qs_host)

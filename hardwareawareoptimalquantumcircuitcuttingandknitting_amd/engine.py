@@ -274,10 +274,12 @@ def _out_rate(ctx: Context, owner) -> float:
     return g.value
 
 
-def out_buffer(ctx: Context, n: int):
+def out_buffer(ctx: Context, n: int, select: bool = True):
     """(tensor [n] float64, owner or None): a ``qk_out_alloc`` mapping for outputs of at least
     OUT_MAPPED_MIN_BYTES (from OUT_SELECT_MIN_BYTES on, one that writes fast: see above), torch's
-    allocator below that. Contents are undefined."""
+    allocator below that. Contents are undefined. ``select=False``: the first mapping, not timed
+    (the drop-in's first call: the call's own write then says whether to replace it,
+    KnitPipeline.take_out)."""
     T = torch()
     if 8 * n < OUT_MAPPED_MIN_BYTES:
         return T.empty(n, dtype=T.float64, device=T.device("cuda", ctx.device)), None
@@ -294,7 +296,7 @@ def out_buffer(ctx: Context, n: int):
             warnings.warn(f"qk_out_alloc failed ({e}); large outputs fall back to torch allocations "
                           f"(out_stats: {out_stats()})", RuntimeWarning, stacklevel=2)
         return T.empty(n, dtype=T.float64, device=T.device("cuda", ctx.device)), None
-    if 8 * n < OUT_SELECT_MIN_BYTES or OUT_TRIES <= 1:
+    if 8 * n < OUT_SELECT_MIN_BYTES or OUT_TRIES <= 1 or not select:
         return first.tensor(), first
     with _out_select_lock:
         owner = first

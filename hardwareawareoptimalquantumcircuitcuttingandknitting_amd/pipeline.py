@@ -87,8 +87,10 @@ ROW_JOBS = int(os.environ.get("QKNIT_ROW_JOBS", "4"))
 # every step sees the same q) and bounds the change of every output of R = X_A^T X_B, X_f = W_f q_f:
 # with X_f = X'_f + D_f (kept rows / pruned rows),
 #   |R - R'|[a, b] <= sum_k  m_A[k] d_B[k] + d_A[k] m_B[k] + d_A[k] d_B[k],
-#   m_f[k] = max_x |X'_f[k, x]|,  d_f[k] = sum_{j pruned} |W_f[k, j]| max_x |q_f[j, x]|
-# (_prune_bound). Rows are pruned only when that bound is at most PRUNE_TOL; otherwise the threshold
+#   m_f[k] = sum_{j kept} |W_f[k, j]| max_x |q_f[j, x]|  (>= max_x |X'_f[k, x]|),
+#   d_f[k] = sum_{j pruned} |W_f[k, j]| max_x |q_f[j, x]|
+# (_prune_bound; round 5 formed m_f from X'_f itself with a GEMM, a tighter bound that waited for the
+# BLAS library's first use). Rows are pruned only when that bound is at most PRUNE_TOL; otherwise the threshold
 # is lowered tenfold (down to 1e-16) and, failing that, nothing is pruned. syc 32 5: see DESIGN §3.
 ROW_PRUNE = float(os.environ.get("QKNIT_ROW_PRUNE", "1e-12"))
 PRUNE_TOL = float(os.environ.get("QKNIT_PRUNE_TOL", "1e-13"))  # largest output change pruning may cause
@@ -390,9 +392,9 @@ class HipBackend:
     def npd_dense(self, dense, accuracy):
         return engine.nearest_probability_distribution(self.ctx, dense, accuracy)
 
-    def out_buffer(self, n: int):
+    def out_buffer(self, n: int, select: bool = True):
         """(tensor [n] float64, owner): the knit output, 1-GiB-mapped when large (engine.out_buffer)."""
-        return engine.out_buffer(self.ctx, n)
+        return engine.out_buffer(self.ctx, n, select=select)
 
     def event(self):
         return self.T.cuda.Event(enable_timing=True)
@@ -665,26 +667,30 @@ class KnitPipeline:
             bound = self._prune_bound(qs, keep)
             if bound <= PRUNE_TOL:
                 self.prune_bound = bound
+                del self._prune_mq
                 return pruned
             thr /= 10
+        self.__dict__.pop("_prune_mq", None)
         return {}
 
     def _prune_bound(self, qs: dict, keep: dict) -> float:
         """Bound on max |R - R'| over every output when only the ``keep`` rows of each side are swept
-        (the ROW_PRUNE comment): ``qs`` every swept row of both sides [rows, 2^m], exact."""
-        T = self.T
+        (the ROW_PRUNE comment): ``qs`` every swept row of both sides [rows, 2^m], exact. Only the rows'
+        largest entries are read back (one device reduction per side, no GEMM: the plan does not wait
+        for a BLAS library's first-use initialisation, ~0.2 s in a fresh process); with
+        ``mq[j] = max_x |q[j, x]|`` the kept part of each operand row is bounded by the triangle
+        inequality, ``max_x |X'_f[k, x]| <= sum_{j kept} |W_f[k, j]| mq[j]``, and
+        ``d_f[k] = sum_{j pruned} |W_f[k, j]| mq[j]`` as before."""
+        if not hasattr(self, "_prune_mq"):
+            self._prune_mq = {i: qs[i].abs().amax(dim=1).cpu().numpy() for i in sorted(keep)}
         m, d = [], []
         for i in sorted(keep):
-            q = qs[i]
-            Wi = T.as_tensor(np.ascontiguousarray(self.ops.transforms[i]), dtype=T.float64, device=q.device)
-            k = T.as_tensor(keep[i], device=q.device)
-            m.append((Wi[:, k] @ q[k]).abs().amax(dim=1))
-            gone = np.setdiff1d(np.arange(Wi.shape[1]), keep[i])
-            if gone.size:
-                g = T.as_tensor(gone, device=q.device)
-                d.append((Wi[:, g].abs() * q[g].abs().amax(dim=1)[None, :]).sum(dim=1))
-            else:
-                d.append(T.zeros(Wi.shape[0], dtype=T.float64, device=q.device))
+            W = np.abs(np.asarray(self.ops.transforms[i]))
+            mq = self._prune_mq[i]
+            kept = np.zeros(W.shape[1], dtype=bool)
+            kept[keep[i]] = True
+            m.append(W[:, kept] @ mq[kept])
+            d.append(W[:, ~kept] @ mq[~kept])
         return float((m[0] * d[1] + d[0] * m[1] + d[0] * d[1]).sum())
 
     def _swept_rows(self, i: int, fs, keep):
@@ -1721,16 +1727,17 @@ class KnitPipeline:
             n = max(hi - lo, 1) * mats[self.order[-1]].shape[1]
         return self.new_out(n, zero=self.mode == "gather" or not self.covers_outputs())
 
-    def new_out(self, n: int, zero: bool = False):
+    def new_out(self, n: int, zero: bool = False, select: bool = True):
         """A fresh [n] fp64 device buffer for the knit output (engine.out_buffer: 1-GiB-mapped when
-        large; a host backend's own allocation in the CPU tests). ``self.out_alloc`` records how."""
+        large; a host backend's own allocation in the CPU tests). ``self.out_alloc`` records how.
+        ``select=False``: a large mapping is not write-rate checked (take_out's first call)."""
         alloc = getattr(self.be, "out_buffer", None)
         if alloc is None:
             self.out_alloc = "backend"
             self._last_owner = None
             return self.be.zeros((n,), self.T.float64) if zero else self.be.empty((n,), self.T.float64)
         n_sel = len(engine.out_selections)
-        out, owner = alloc(n)
+        out, owner = alloc(n) if select else alloc(n, select=False)
         self.out_alloc = "qk_out_alloc (1-GiB mapped chunks)" if owner is not None else "torch"
         if len(engine.out_selections) > n_sel:  # candidates' write rates, the kept one first
             last = engine.out_selections[-1]
@@ -1745,21 +1752,54 @@ class KnitPipeline:
             out.zero_()
         return out
 
-    def take_out(self):
+    def take_out(self, defer_select: bool = False):
         """The output buffer of one drop-in call (run.run_virtual_circuit): the previous call's mapping
         again once the caller has dropped every tensor over it (the reference returns a fresh result
-        per call, and mapping 34 GB costs milliseconds), else a new buffer."""
+        per call, and mapping 34 GB costs milliseconds), else a new buffer. ``defer_select`` (one-GPU
+        drop-in): the first buffer is not write-rate checked; the caller times the call's write and
+        reports it (:meth:`note_call_write`), and a slow buffer is replaced at a later call."""
         n = self.slice[1] if self.mode == "slice" else 1 << self.N
         zero = not self.covers_outputs()
         own = getattr(self, "_call_owner", None)
         if own is not None and own.n == n and not own.in_use():
-            out = own.tensor()
-            if zero:
-                out.zero_()
-            return out
-        out = self.new_out(n, zero=zero)
+            if getattr(own, "write_gbs", None) is None or own.write_gbs >= engine.OUT_FAST_GBS:
+                out = own.tensor()
+                if zero:
+                    out.zero_()
+                return out
+            # the first call's own write into its un-timed mapping was slow (the buffer lottery, DESIGN
+            # §4): this call takes a write-rate-selected mapping instead
+            self._call_owner = own = None
+            select = True
+        else:
+            # the first call maps one buffer without timing it (engine.out_buffer select=False) and
+            # times its own write instead (note_call_write): the selection's extra mappings and probe
+            # launches (~20 ms at 2^32 outputs) move to a later call, and only if that write was slow
+            select = own is not None or not defer_select
+        out = self.new_out(n, zero=zero, select=select)
         self._call_owner = self._last_owner
+        if self._call_owner is not None and not select:
+            self._call_owner.write_gbs = None
+            self._time_call_write = True
         return out
+
+    def note_call_write(self, events_before: int):
+        """After a drop-in call whose output mapping was not write-rate checked (take_out): the rate of
+        the call's own write (its HIP events) decides whether later calls keep the mapping."""
+        if not getattr(self, "_time_call_write", False):
+            return
+        self._time_call_write = False
+        own = getattr(self, "_call_owner", None)
+        ev = self.events[events_before:]
+        if own is None or not ev:
+            return
+        ms = ev[-1][0].elapsed_time(ev[-1][1])
+        M, N, _ = self.gemm_shape()
+        own.write_gbs = 8.0 * M * N / (ms * 1e-3) / 1e9 if ms > 0 else float("inf")
+        if own.write_gbs < engine.OUT_FAST_GBS:
+            # a later call swaps it for a selected one (own.write_gbs stays below the stop)
+            engine.out_selections.append([f"drop-in first call: un-timed mapping wrote at {own.write_gbs:.1f} GB/s, "
+                                          "replaced on the next call"])
 
     def _contract(self, mats, skip=None):
         if self.mode != "gather":

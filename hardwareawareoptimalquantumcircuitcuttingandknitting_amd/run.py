@@ -241,21 +241,30 @@ def _planned_dense(virt: VirtualCircuit, device: int, out):
     t_plan = perf_counter()
     pipe.be.bind()
     if out is None:  # 1-GiB-mapped when large; the previous call's mapping once the caller dropped it
-        out = pipe.take_out()
+        out = pipe.take_out(defer_select=True)
     t_out = perf_counter()
     e0, e1 = T.cuda.Event(enable_timing=True), T.cuda.Event(enable_timing=True)
     host = perf_counter() - now
+    timed = getattr(pipe, "_time_call_write", False) and not pipe.record_events
+    n_ev = len(pipe.events)
     e0.record()
     pipe.out = out
     try:
+        if timed:  # the call's own write times its un-checked output mapping (KnitPipeline.take_out)
+            pipe.record_events = True
         qs = pipe.sweep()
         e1.record()
         pipe.knit(qs)
         out = pipe.out
     finally:
         pipe.out = None
+        if timed:
+            pipe.record_events = False
     _sync(device)
     wall = perf_counter() - now
+    if timed:
+        pipe.note_call_write(n_ev)
+        del pipe.events[n_ev:]
     if not pipe.plan_reused and not hasattr(pipe, "first_call_ms"):
         # where the first call's time goes: the plan's phases (KnitPipeline.plan_ms), the output buffer
         # (mapping + write-rate selection), the step itself (launches + device time to the sync)

@@ -865,6 +865,44 @@ def test_output_falls_back_to_an_ordinary_allocation(T, monkeypatch):
     assert pipe.out_alloc.startswith("torch (torch allocation")
 
 
+def test_drop_in_first_call_defers_the_output_selection(T, monkeypatch):
+    """The drop-in's first call maps its output without the write-rate check (no candidate mappings,
+    no probe launches) and times its own write instead; a write below OUT_FAST_GBS (forced: inf) makes
+    the next call take a write-rate-selected mapping; every call equals the oracle; qk_out_stats counts
+    the reservations (one for the first call, OUT_TRIES for the replacement)."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.run import cached_plan, clear_plan_cache
+
+    monkeypatch.setattr(engine, "OUT_MAPPED_MIN_BYTES", 0)
+    monkeypatch.setattr(engine, "OUT_SELECT_MIN_BYTES", 0)
+    monkeypatch.setattr(engine, "OUT_FAST_GBS", float("inf"))
+    monkeypatch.setattr(engine, "OUT_TRIES", 3)
+    cut = circuits.two_fragment("cx", 8, 8, n_cuts=4)[1]
+    ref = dense.run_dense(cut)
+    clear_plan_cache()
+    n_sel = len(engine.out_selections)
+    st0 = engine.out_stats()
+    out, _ = run_virtual_circuit(VirtualCircuit(cut), dense=True)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, atol=TOL, rtol=0)
+    pipe = cached_plan(VirtualCircuit(cut), 0)
+    own = pipe._call_owner
+    assert own is not None and own.write_gbs is not None and own.write_gbs > 0
+    assert engine.out_stats()["reserved"] - st0["reserved"] == 1  # no candidates, no probes
+    assert "replaced on the next call" in engine.out_selections[-1][0] and len(engine.out_selections) == n_sel + 1
+    first_ptr = own.ptr
+    del out, own
+    out, _ = run_virtual_circuit(VirtualCircuit(cut), dense=True)  # first result dropped: replaced, selected
+    np.testing.assert_allclose(out.cpu().numpy(), ref, atol=TOL, rtol=0)
+    assert pipe._call_owner.ptr != first_ptr and getattr(pipe._call_owner, "write_gbs", None) is None
+    assert len(engine.out_selections[-1]) == 3  # the three candidates' rates
+    assert engine.out_stats()["reserved"] - st0["reserved"] == 4
+    del out
+    out, _ = run_virtual_circuit(VirtualCircuit(cut), dense=True)  # the selected mapping is kept
+    assert out.data_ptr() == pipe._call_owner.ptr
+    np.testing.assert_allclose(out.cpu().numpy(), ref, atol=TOL, rtol=0)
+    del out
+    clear_plan_cache()
+
+
 def test_output_selection_keeps_fastest_and_frees_the_others(T, monkeypatch):
     """engine.out_buffer's write-rate selection (forced here on a 512-KiB output: every candidate
     tried): OUT_TRIES mappings are made and timed, the fastest is kept (its rate first in

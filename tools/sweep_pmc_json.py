@@ -50,13 +50,20 @@ def main():
     simd_cyc = sum(1024 * k["mean_ms"] * 1e-3 * k["effective_clock_GHz"] * 1e9 for k in kernels.values())
     f64_issue = sum(4 * k["f64_wave_instructions"] for k in kernels.values()) / simd_cyc
     valu_busy = sum(4 * k["valu_wave_instructions"] for k in kernels.values()) / simd_cyc
+    lds = sum(k["raw"].get("SQ_LDS_IDX_ACTIVE", 0.0) for k in kernels.values())
+    conf = sum(k["raw"].get("SQ_LDS_BANK_CONFLICT", 0.0) for k in kernels.values())
     rec = {
         "workload": workload, "kernels": kernels,
-        "note": "rocprofv3 --pmc, four passes (FETCH_SIZE; WRITE_SIZE; 8 SQ; 7 SQ + GRBM) over tools/sweep_bench.py; "
-                "derivations in tools/sweep_pmc_json.py",
+        "note": "rocprofv3 --pmc, four passes (FETCH_SIZE; WRITE_SIZE; 8 SQ; 7 SQ + GRBM) over tools/sweep_bench.py "
+                "or tools/sweep_run.py; derivations in tools/sweep_pmc_json.py",
         "per_step": {"ms": ms, "hbm_bytes": hbm, "hbm_frac_of_8TBs": hbm / (ms * 1e-3) / 8e12, "fp64_flops": flops,
                      "fp64_frac_of_78.6TF": flops / (ms * 1e-3) / 78.6e12, "f64_issue_frac": f64_issue,
-                     "valu_busy_frac": valu_busy},
+                     "valu_busy_frac": valu_busy, "lds_bank_conflict_frac": conf / lds if lds else None,
+                     "per_kernel": {name: {"ms": k["mean_ms"], "hbm_GBs": k["hbm_GBs"], "valu_busy_frac": k["valu_busy_frac"],
+                                           "f64_issue_frac": k["f64_issue_frac"],
+                                           "lds_bank_conflict_frac": k["lds_bank_conflict_frac"],
+                                           "wait_any_frac": k["wait_any_frac"], "waves": k["waves"]}
+                                    for name, k in kernels.items()}},
     }
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec["per_step"]))

@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
-"""Run the bench step (KnitPipeline, syc 32 5 by default) a few times, nothing else: the program a
-rocprofv3 pass profiles when only the step's kernels should appear (prep-chain counters,
-profiles/r03_prep_pmc.json via tools/prep_pmc.py).
+"""Run one plan's instance sweep a few times, nothing else: the program a rocprofv3 pass profiles
+when only the sweep kernels should appear (bench.py ``sweep_full`` counters,
+profiles/*_sweep_full_pmc.json via tools/sweep_pmc_json.py).
 
-    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_f -- python3 tools/step_run.py --steps 5
+    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_f -- python3 tools/sweep_run.py --full --steps 5
+
+``--full``: the direct plan (no basis reduction, no light cone, no row pruning): every unique instance
+of both 16-qubit fragments of syc 32 5 with all its branch jobs (2 x 625 instances, 2 x 1296 jobs);
+default: the bench plan's sweep (basis-reduced, light cone, pruned rows).
 """
 import argparse
 import os
@@ -15,10 +19,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="syc_32_5_p2")
+    ap.add_argument("--full", action="store_true")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--no-data-rank", action="store_true",
-                    help="the step without data-rank compression (bench.py knit_general: the K = 64 MFMA contraction)")
     args = ap.parse_args()
     import torch
 
@@ -27,12 +30,11 @@ def main():
 
     name, n, d, p, var = cutting.BASELINE_CONFIGS[args.workload]
     cut = cutting.config_cut_circuit(name, n, d, p, var)[1]
-    pipe = KnitPipeline(VirtualCircuit(cut), factored=True, data_rank=False if args.no_data_rank else None)
+    pipe = KnitPipeline(VirtualCircuit(cut), factored=not args.full)
     for _ in range(args.warmup + args.steps):
-        pipe.step()
+        pipe.sweep()
     torch.cuda.synchronize()
-    pipe.sync_stats()
-    print(f"steps {args.steps}, rank {pipe.last_rank}, fallbacks {pipe.rank_fallbacks}", flush=True)
+    print(pipe.instance_counts(), flush=True)
 
 
 if __name__ == "__main__":
