@@ -334,10 +334,29 @@ def knit_general(pipe_kw: dict, steps: int) -> dict:
     gemm_ms = sum(s.elapsed_time(e) for s, e in pipe.events) / max(len(pipe.events), 1)
     M, N, K = pipe.gemm_shape()
     flops = 2.0 * M * N * K
-    out = {"ms_per_step": ms, "kernel": "qk_gemm_glds_kernel (K = %d light-cone terms, fp64 MFMA)" % K,
+    out = {"ms_per_step": ms, "kernel": "qk_gemm_wave_kernel<16> (K = %d light-cone terms, fp64 MFMA "
+                                         "v_mfma_f64_16x16x4_f64, per-wave LDS rings)" % K,
            "gemm_mnk": [M, N, K], "avg_launch_ms": gemm_ms, "achieved_TFs": flops / (gemm_ms * 1e-3) / 1e12,
            "peak_TFs": FP64_MFMA_PEAK_TFLOPS, "frac": flops / (gemm_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
            "traffic": traffic_per_launch(M, N, K)}
+    # MFMA counters of the same contraction (profiles/*gemm_k64_pmc.json, tools/gemm_pmc_json.py): the
+    # counted fp64 MFMA flops (512 x SQ_INSTS_VALU_MFMA_MOPS_F64) over THIS run's launch time, and the
+    # profiled run's MFMA busy fraction and clock (the spec peak assumes 2.4 GHz; a power-limited clock
+    # lowers the reachable rate in proportion)
+    import glob
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*gemm_k64_pmc.json"))):
+        try:
+            rec = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if rec.get("gemm_mnk") == [M, N, K] and "mfma_busy_frac" in rec:
+            out["counters"] = {"source": os.path.basename(f), "flops_counted": rec["flops_counted"],
+                               "counted_TFs_this_run": rec["flops_counted"] / (gemm_ms * 1e-3) / 1e12,
+                               "frac_counted": rec["flops_counted"] / (gemm_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+                               "mfma_busy_frac_profiled": rec["mfma_busy_frac"],
+                               "effective_clock_GHz_profiled": rec["effective_clock_GHz"],
+                               "hbm_bytes_per_launch": rec["hbm_bytes_per_launch"]}
     del pipe
     torch.cuda.empty_cache()
     return out

@@ -29,12 +29,17 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 from time import perf_counter
 
 import numpy as np
 
 from . import _lib, engine
 from .fragment_program import JobTable
+
+
+_PROBES: dict = {}  # (columns, device) -> the fixed Gaussian probes [N_PROBES, n] (read-only; KnitPipeline._probes)
+_PROBES_LOCK = threading.Lock()
 
 
 def _mm_nt(X, Y):
@@ -966,9 +971,16 @@ class KnitPipeline:
         """The fixed Gaussian probes, TRANSPOSED: [N_PROBES, n] (products with the wide operands go
         through _mm_nt: a plain [K, 2^16] @ [2^16, 16] GEMM runs on a handful of workgroups)."""
         if self._probe is None or self._probe.shape[1] != n:
-            T = self.T
-            g = T.Generator().manual_seed(1234)
-            self._probe = T.randn((self.N_PROBES, n), generator=g, dtype=T.float64).to(device)
+            # the same fixed probes for every pipeline: drawn once per (n, device) in the process (the
+            # 16 x 2^16 host draw and upload took ~10 ms of each new plan's first step)
+            key = (n, str(device))
+            with _PROBES_LOCK:
+                hit = _PROBES.get(key)
+                if hit is None:
+                    T = self.T
+                    g = T.Generator().manual_seed(1234)
+                    hit = _PROBES[key] = T.randn((self.N_PROBES, n), generator=g, dtype=T.float64).to(device)
+            self._probe = hit
         return self._probe
 
     def _prep_step(self, qs) -> dict:

@@ -254,7 +254,9 @@ def _planned_dense(virt: VirtualCircuit, device: int, out):
             pipe.record_events = True
         qs = pipe.sweep()
         e1.record()
+        t_sweep = perf_counter()
         pipe.knit(qs)
+        t_knit = perf_counter()
         out = pipe.out
     finally:
         pipe.out = None
@@ -270,7 +272,8 @@ def _planned_dense(virt: VirtualCircuit, device: int, out):
         # (mapping + write-rate selection), the step itself (launches + device time to the sync)
         pipe.first_call_ms = {"plan": (t_plan - now) * 1e3, **{f"plan.{k}": v for k, v in pipe.plan_ms.items()},
                               "output_buffer": (t_out - t_plan) * 1e3, "step": (now + wall - t_out) * 1e3,
-                              "total": wall * 1e3}
+                              "step.sweep_launch": (t_sweep - t_out) * 1e3, "step.knit_launch": (t_knit - t_sweep) * 1e3,
+                              "step.device_wait": (now + wall - t_knit) * 1e3, "total": wall * 1e3}
     pipe.sync_stats()
     run_time = host + e0.elapsed_time(e1) * 1e-3
     return out, RunTimeInfo(run_time, max(wall - run_time, 0.0)), pipe

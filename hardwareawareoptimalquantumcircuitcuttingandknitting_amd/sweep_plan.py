@@ -117,29 +117,34 @@ class Pass:
     ops: list  # HostOps in order
 
 
-def _greedy_passes(ops: list, tile_bits: int, first_tile: set | None = None) -> list[Pass] | None:
+def _greedy_passes(ops: list, tile_bits: int, first_tile: set | None = None,
+                   needs: list | None = None) -> list[Pass] | None:
     """Greedy schedule: each pass takes ops in order while their non-diagonal qubits fit the tile
     (an op touching a qubit of a deferred op is deferred too). ``first_tile`` fixes the first
     pass's tile instead of growing it (None when that pass could take nothing)."""
-    remaining = list(ops)
+    # each op's (qubits, non-diagonal qubits), computed once per call (schedule_passes passes them in
+    # for its up to 200 candidate first tiles)
+    if needs is None:
+        needs = [(set(op.qubits), op_need(op)) for op in ops]
+    remaining = list(range(len(ops)))
     passes: list[Pass] = []
     fixed = first_tile
     while remaining:
         tile = set(fixed) if fixed is not None else set(range(LOW_BITS))
         taken, blocked, rest = [], set(), []
-        for op in remaining:
-            qs = set(op.qubits)
-            need = op_need(op)
+        for k in remaining:
+            op = ops[k]
+            qs, need = needs[k]
             if qs & blocked:
                 blocked |= qs
-                rest.append(op)
+                rest.append(k)
                 continue
             if need <= tile or (fixed is None and len(tile | need) <= tile_bits):
                 tile |= need
                 taken.append(op)
             else:
                 blocked |= qs
-                rest.append(op)
+                rest.append(k)
         if not taken:
             if fixed is not None:
                 return None
@@ -162,12 +167,13 @@ def schedule_passes(prog: FragmentProgram, tile_bits: int = TILE_BITS) -> list[P
     traced = set(range(prog.m, n))
     if len(traced) > tile_bits - LOW_BITS:
         raise NotImplementedError("more traced qubits than a tile can hold")
-    passes = _greedy_passes(prog.ops, tile_bits)
+    needs = [(set(op.qubits), op_need(op)) for op in prog.ops]
+    passes = _greedy_passes(prog.ops, tile_bits, needs=needs)
     free = list(range(LOW_BITS, n))
     extra = tile_bits - LOW_BITS
     if len(passes) > 2 and 0 < extra < len(free) and math.comb(len(free), extra) <= 200:
         for combo in itertools.combinations(free, extra):
-            cand = _greedy_passes(prog.ops, tile_bits, set(range(LOW_BITS)) | set(combo))
+            cand = _greedy_passes(prog.ops, tile_bits, set(range(LOW_BITS)) | set(combo), needs=needs)
             if cand is not None and len(cand) < len(passes):
                 passes = cand
                 if len(passes) <= 2:
