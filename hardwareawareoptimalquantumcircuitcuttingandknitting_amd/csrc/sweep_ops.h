@@ -165,6 +165,41 @@ __device__ __forceinline__ void ap_d2r(double2 (&v)[PER], const double* d) {
     }
 }
 
+// Cross-lane exchange of one fiber (register) bit with lane bit 4 or 5 (CDNA4 v_permlane16_swap /
+// v_permlane32_swap: lanes 16-31 (48-63) of the first operand trade places with lanes 0-15 (32-47) of the
+// second). Applied to the register pairs (r, r | 1 << I) it transposes register bit I with lane bit T:
+// afterwards register bit I holds the qubit lane bit T held, and lane bit T the one register bit I held.
+// The per-program kernels use it where the next fiber group needs at most two qubits that sit on lane
+// bits 4 / 5 (a 1-2-bit butterfly boundary): 8 x 4 dword swaps per bit instead of the tile's round trip
+// through LDS (16 writes, a barrier, 16 reads).
+template <int T>
+__device__ __forceinline__ void lane_swap(double& a, double& b) {
+    static_assert(T == 4 || T == 5, "lane bit 4 or 5");
+    const unsigned alo = (unsigned)__double2loint(a), ahi = (unsigned)__double2hiint(a);
+    const unsigned blo = (unsigned)__double2loint(b), bhi = (unsigned)__double2hiint(b);
+    if constexpr (T == 5) {
+        const auto lo = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+        const auto hi = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+        a = __hiloint2double((int)hi[0], (int)lo[0]);
+        b = __hiloint2double((int)hi[1], (int)lo[1]);
+    } else {
+        const auto lo = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+        const auto hi = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+        a = __hiloint2double((int)hi[0], (int)lo[0]);
+        b = __hiloint2double((int)hi[1], (int)lo[1]);
+    }
+}
+
+template <int I, int T>
+__device__ __forceinline__ void xchg_lane_bit(double2 (&v)[PER]) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if (r & (1 << I)) continue;
+        lane_swap<T>(v[r].x, v[r | (1 << I)].x);
+        lane_swap<T>(v[r].y, v[r | (1 << I)].y);
+    }
+}
+
 }  // namespace qk_sweep_ops
 
 #endif  // QKNIT_SWEEP_OPS_H

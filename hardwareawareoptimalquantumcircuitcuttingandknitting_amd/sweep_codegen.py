@@ -392,7 +392,12 @@ def _fiber(enc, gi: int, TB: int, bitpos: list) -> dict:
     ``lo`` (expression of tid) and ``hi`` (constants), so amplitude r sits at state index
     ``tbase | lo | hi[r]``."""
     pos = [int(x) for x in enc.groups[gi]["pos"]]
-    nonfib = [p for p in range(TB) if p not in pos]
+    return _layout(pos, [p for p in range(TB) if p not in pos], TB, bitpos)
+
+
+def _layout(pos: list, nonfib: list, TB: int, bitpos: list) -> dict:
+    """A register / lane layout of the tile: register bit k holds tile position ``pos[k]``, thread-index
+    bit j tile position ``nonfib[j]`` (any order: a cross-lane exchange leaves the lanes permuted)."""
     return {
         "pos": pos,
         "nonfib": nonfib,
@@ -403,8 +408,99 @@ def _fiber(enc, gi: int, TB: int, bitpos: list) -> dict:
     }
 
 
+_ONE_Q = (sp.K_U1, sp.K_D1, sp.K_SLOT, sp.K_U1R, sp.K_U1X, sp.K_D1R)
+_TWO_Q = (sp.K_U2, sp.K_D2, sp.K_CX, sp.K_SWAP, sp.K_D2R)
+
+
+def _group_used(enc, gi: int) -> list:
+    """Tile positions the ops of group ``gi`` act on (a group's fiber may hold unused positions)."""
+    gpos = [int(x) for x in enc.groups[gi]["pos"]]
+    used = []
+    gr = enc.groups[gi]
+    for oi in range(int(gr["op_begin"]), int(gr["op_end"])):
+        op = enc.ops[oi]
+        kind = int(op["kind"])
+        idx = [int(op["a"])] if kind in _ONE_Q else [int(op["a"]), int(op["b"])] if kind in _TWO_Q else []
+        for a in idx:
+            if gpos[a] not in used:
+                used.append(gpos[a])
+    return used
+
+
+def _group_ext_positions(enc, gi: int, bitpos: list) -> set:
+    """Tile positions of the state bits that select the variants of group ``gi``'s ops (e1 / e2):
+    they must stay thread bits (a register bit would make the op's matrix differ per register)."""
+    out = set()
+    gr = enc.groups[gi]
+    for oi in range(int(gr["op_begin"]), int(gr["op_end"])):
+        for fld in ("e1", "e2"):
+            eb = int(enc.ops[oi][fld])
+            if eb >= 0 and eb in bitpos:
+                out.add(bitpos.index(eb))
+    return out
+
+
+def lane_exchange_enabled() -> bool:
+    """QKNIT_SWEEP_LANE_XCHG=0: every fiber-group boundary goes through LDS (round 5's kernels)."""
+    return os.environ.get("QKNIT_SWEEP_LANE_XCHG", "1") != "0"
+
+
+def _plan_layouts(enc, gids: list, TB: int, bitpos: list) -> tuple:
+    """Per group of a direct-form pass: its register / lane layout and how it is reached from the
+    previous group's — ``"lds"`` (the tile's round trip through LDS, any layout) or a list of
+    ``(register bit, lane bit)`` cross-lane exchanges (sweep_ops.h ``xchg_lane_bit``). An exchange
+    applies when the group's ops need at most two tile positions that are not in the previous fiber
+    and those sit on thread bits 4 / 5 (lane bits of one wave; the previous layout's lane order is
+    chosen so they do, unless it came from an exchange itself): the wavefront butterfly of a 1-2-bit
+    boundary (syc 32 5: the last group of each FINAL pass touches two new qubits)."""
+    layouts = [_fiber(enc, gids[0], TB, bitpos)]
+    trans = [None]
+    free = [True]  # whether the layout's lane order may still be chosen (not fixed by an exchange)
+    for k in range(1, len(gids)):
+        cur = layouts[-1]
+        used = _group_used(enc, gids[k])
+        need = [p for p in used if p not in cur["pos"]]
+        ok = lane_exchange_enabled() and TB - 4 >= 6 and 0 < len(need) <= 2 and len(used) <= 4
+        if ok and not set(need) <= {cur["nonfib"][4], cur["nonfib"][5]}:
+            if free[-1]:  # put the needed positions on thread bits 5 (then 4), the rest ascending
+                rest = [p for p in sorted(cur["nonfib"]) if p not in need]
+                tail = (need + [p for p in rest if p > max(need)][:2 - len(need)]) if len(need) < 2 else need
+                rest = [p for p in rest if p not in tail]
+                order = rest[:4] + ([tail[1], tail[0]] if len(tail) == 2 else tail) + rest[4:]
+                cur = _layout(cur["pos"], order, TB, bitpos)
+                layouts[-1] = cur
+            else:
+                ok = False
+        if not ok:
+            layouts.append(_fiber(enc, gids[k], TB, bitpos))
+            trans.append("lds")
+            free.append(True)
+            continue
+        pos, nonfib = list(cur["pos"]), list(cur["nonfib"])
+        ext = _group_ext_positions(enc, gids[k], bitpos)
+        # evict variant-selecting positions first: they must end on thread bits
+        evict = sorted((i for i in range(4) if pos[i] not in used), key=lambda i: pos[i] not in ext)
+        steps = []
+        for p in need:
+            t = nonfib.index(p)
+            i = evict.pop(0)
+            steps.append((i, t))
+            pos[i], nonfib[t] = p, pos[i]
+        if ext & set(pos):
+            layouts.append(_fiber(enc, gids[k], TB, bitpos))
+            trans.append("lds")
+            free.append(True)
+            continue
+        layouts.append(_layout(pos, nonfib, TB, bitpos))
+        trans.append(steps)
+        free.append(False)
+    return layouts, trans
+
+
 def _emit_group_ops(e: _Emitter, enc, gi: int, f: dict, bitpos: list) -> None:
     nonfib = f["nonfib"]
+    gpos = [int(x) for x in enc.groups[gi]["pos"]]
+    remap = None if list(f["pos"]) == gpos else [f["pos"].index(p) if p in f["pos"] else -1 for p in gpos]
 
     def ext(ebit):
         if ebit in bitpos:
@@ -416,13 +512,22 @@ def _emit_group_ops(e: _Emitter, enc, gi: int, f: dict, bitpos: list) -> None:
 
     gr = enc.groups[gi]
     for oi in range(int(gr["op_begin"]), int(gr["op_end"])):
-        _emit_op(e, enc.ops[oi], enc.mats, ext, enc.n_slots)
+        op = enc.ops[oi]
+        if remap is not None:  # the group runs in an exchanged layout: its fiber indices move
+            op = op.copy()
+            kind = int(op["kind"])
+            for fld in ("a",) if kind in _ONE_Q else ("a", "b") if kind in _TWO_Q else ():
+                op[fld] = remap[int(op[fld])]
+                assert op[fld] >= 0
+        _emit_op(e, op, enc.mats, ext, enc.n_slots)
 
 
 def _pass_body_direct(e: _Emitter, enc, ps, gids: list, TB: int, NT: int, n: int, m: int, bitpos: list,
                       init: bool, final: bool, zero_tile: bool, zero_mask: int) -> list:
     """Body of a pass kernel in the direct form (see _pass_kernel)."""
-    first, last = _fiber(enc, gids[0], TB, bitpos), _fiber(enc, gids[-1], TB, bitpos)
+    lays, trans = _plan_layouts(enc, gids, TB, bitpos)
+    first, last = lays[0], lays[-1]
+    uses_lds = any(t == "lds" for t in trans)
     mmask = (1 << m) - 1
     if final:
         e(f"const unsigned long long xlo = (tbase | {last['lo']}) & 0x{mmask:x}ull;")
@@ -451,15 +556,18 @@ def _pass_body_direct(e: _Emitter, enc, ps, gids: list, TB: int, NT: int, n: int
     if zero_tile:
         e("if (tbase == 0ull) {")
     for k, gi in enumerate(gids):
-        f = first if k == 0 else (last if k == len(gids) - 1 else _fiber(enc, gi, TB, bitpos))
+        f = lays[k]
         e("{")
-        if k > 0:
+        if k > 0 and trans[k] == "lds":
             e(f"const unsigned sbb = 16u * swz({f['base']});", 2)
             for r in range(PER):
                 e(f"v[{r}] = {_lds_at(f, r)};", 2)
+        elif k > 0:  # cross-lane butterfly: register bit i <-> lane bit t
+            for i, t in trans[k]:
+                e(f"xchg_lane_bit<{i}, {t}>(v);", 2)
         _emit_group_ops(e, enc, gi, f, bitpos)
-        if k < len(gids) - 1:
-            if k == 0:
+        if k < len(gids) - 1 and trans[k + 1] == "lds":
+            if k == 0 or trans[k] != "lds":
                 e(f"const unsigned sbb = 16u * swz({f['base']});", 2)
             for r in range(PER):
                 e(f"{_lds_at(f, r)} = v[{r}];", 2)
@@ -472,7 +580,7 @@ def _pass_body_direct(e: _Emitter, enc, ps, gids: list, TB: int, NT: int, n: int
         e(f"const double sgn = job_sign[job] * {_lit(program_scale(enc) ** 2)};")
         for r in range(PER):
             e(f"out{r} = fma(sgn, fma(v[{r}].x, v[{r}].x, v[{r}].y * v[{r}].y), out{r});")
-        if len(gids) > 1:
+        if uses_lds:
             e("__syncthreads();  // the next branch job's first LDS writes follow this job's last reads")
         e("}")
         for r in range(PER):

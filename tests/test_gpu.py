@@ -1668,3 +1668,29 @@ def ctypes_size(ctx, comm):
     n, r = ctypes.c_int(), ctypes.c_int()
     ctx.check(ctx.lib.qk_comm_size(comm.handle, ctypes.byref(n), ctypes.byref(r)), "qk_comm_size")
     return n.value, r.value
+
+
+@pytest.mark.parametrize("key", ["syc_32_5_p2", "syc_32_1_p2", "syc_32_1_p2_forced", "qft_16_1_p3"])
+def test_lane_exchange_sweep_is_bit_identical(T, monkeypatch, key):
+    """Per-program sweep kernels with cross-lane butterflies (v_permlane16/32_swap at 1-2-bit fiber-group
+    boundaries, sweep_codegen._plan_layouts) against the same kernels through LDS only
+    (QKNIT_SWEEP_LANE_XCHG=0): the exchange only moves amplitudes between lanes, so every swept row is
+    bit-identical; the bench plan (basis-reduced) and, for syc 32 5, the full direct plan."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import sweep_codegen
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    name, n, d, p, var = cutting.BASELINE_CONFIGS[key]
+    cut = cutting.config_cut_circuit(name, n, d, p, var)[1]
+    plans = [True, False] if key == "syc_32_5_p2" else [var == "forced" or key == "syc_32_5_p2"]
+    for factored in plans:
+        rows = {}
+        for x in ("1", "0"):
+            monkeypatch.setenv("QKNIT_SWEEP_LANE_XCHG", x)
+            pipe = KnitPipeline(VirtualCircuit(cut), factored=factored, jit=True)
+            rows[x] = [q.clone() for q in pipe.sweep()]
+            del pipe
+        assert len(rows["1"]) == len(rows["0"])
+        for a, b in zip(rows["1"], rows["0"]):
+            assert T.equal(a, b)
+    monkeypatch.setenv("QKNIT_SWEEP_LANE_XCHG", "1")
+    assert sweep_codegen.lane_exchange_enabled()
