@@ -1927,10 +1927,14 @@ class KnitPipeline:
         operands (qk_knit_select on the slice's column ranges: its keys are the slice-local outputs'
         keys plus the slice start, since the slice's fixed bits and the ranges' own bits are disjoint)
         or, after a rejected compression, from its exact dense slice (qk_select_above) —, the kept
-        pairs of all ranks are all-gathered (their union is exactly the single-GPU selection: the
-        slices partition the outputs, the values are bit-identical), and every rank runs the NPD of
-        the union (qk_npd_pairs: sorted by key, then by value, so the order of the union does not
-        matter)."""
+        pairs of all ranks are all-gathered, and every rank runs the NPD of the union (qk_npd_pairs:
+        sorted by key, then by value, so the order of the union does not matter). The slices partition
+        the outputs, so the union is exactly the single-GPU selection, bit for bit, whenever every
+        rank's compression verdict matches the single-GPU one. Replicated preparation: each rank checks
+        only its own slice's rows (against a bound scaled by the probes' ||R p|| over those rows), so
+        a rank may accept where the single-GPU check rejects or the reverse; every kept entry is then
+        still within the check's 10 tol of the exact knit, but not necessarily the
+        single-GPU bits. (Sharded preparation takes the MIN verdict over the ranks.)"""
         import torch.distributed as dist
 
         T, be = self.T, self.be
