@@ -200,6 +200,33 @@ __device__ __forceinline__ void xchg_lane_bit(double2 (&v)[PER]) {
     }
 }
 
+// The same transposition for any lane bit L of the wave (0..5) through __shfl_xor (ds_bpermute / DPP):
+// per dword one cross-lane move and three selects, where the swap instructions above take one. The
+// FINAL passes use it for the positions that cannot be put on lane bits 4 / 5, so that no transition
+// of theirs needs the LDS tile (QKNIT_SWEEP_LANE_XCHG=2).
+template <int L>
+__device__ __forceinline__ void lane_xor_swap(double& a, double& b, bool hi) {
+    const double s = hi ? a : b;
+    const double t = __shfl_xor(s, 1 << L, 64);
+    a = hi ? t : a;
+    b = hi ? b : t;
+}
+
+template <int I, int L>
+__device__ __forceinline__ void xchg_lane_bit_any(double2 (&v)[PER]) {
+    if constexpr (L == 4 || L == 5) {
+        xchg_lane_bit<I, L>(v);
+    } else {
+        const bool hi = (__lane_id() >> L) & 1;
+#pragma unroll
+        for (int r = 0; r < PER; ++r) {
+            if (r & (1 << I)) continue;
+            lane_xor_swap<L>(v[r].x, v[r | (1 << I)].x, hi);
+            lane_xor_swap<L>(v[r].y, v[r | (1 << I)].y, hi);
+        }
+    }
+}
+
 }  // namespace qk_sweep_ops
 
 #endif  // QKNIT_SWEEP_OPS_H

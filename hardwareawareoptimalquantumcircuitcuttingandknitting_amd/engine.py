@@ -296,7 +296,8 @@ def out_buffer(ctx: Context, n: int, select: bool = True):
             warnings.warn(f"qk_out_alloc failed ({e}); large outputs fall back to torch allocations "
                           f"(out_stats: {out_stats()})", RuntimeWarning, stacklevel=2)
         return T.empty(n, dtype=T.float64, device=T.device("cuda", ctx.device)), None
-    if 8 * n < OUT_SELECT_MIN_BYTES or OUT_TRIES <= 1 or not select:
+    if 8 * n < max(OUT_SELECT_MIN_BYTES, 1 << 19) or OUT_TRIES <= 1 or not select:
+        # (qk_out_write_rate times whole 512-KiB blocks: nothing smaller is selected)
         return first.tensor(), first
     with _out_select_lock:
         owner = first

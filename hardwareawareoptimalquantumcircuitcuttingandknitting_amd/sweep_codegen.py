@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import hashlib
 import os
+import re
 
 from . import sweep_plan as sp
 
@@ -440,19 +441,35 @@ def _group_ext_positions(enc, gi: int, bitpos: list) -> set:
     return out
 
 
+def lane_exchange_mode() -> int:
+    """QKNIT_SWEEP_LANE_XCHG: 0 = every fiber-group boundary through LDS (round 5's kernels); 1 = lane
+    bits 4 / 5 by permlane swaps where at most two positions change (default); 2 = also the other lane
+    bits of a single-wave tile (shuffles), so that FINAL passes never touch LDS."""
+    return int(os.environ.get("QKNIT_SWEEP_LANE_XCHG", "1"))
+
+
+def opaque_tid() -> bool:
+    """QKNIT_SWEEP_OPAQUE_TID=0: the FINAL pass's branch-job loop uses the thread index directly."""
+    return os.environ.get("QKNIT_SWEEP_OPAQUE_TID", "1") != "0"
+
+
 def lane_exchange_enabled() -> bool:
-    """QKNIT_SWEEP_LANE_XCHG=0: every fiber-group boundary goes through LDS (round 5's kernels)."""
-    return os.environ.get("QKNIT_SWEEP_LANE_XCHG", "1") != "0"
+    return lane_exchange_mode() != 0
 
 
-def _plan_layouts(enc, gids: list, TB: int, bitpos: list) -> tuple:
+def _plan_layouts(enc, gids: list, TB: int, bitpos: list, final: bool = False) -> tuple:
     """Per group of a direct-form pass: its register / lane layout and how it is reached from the
     previous group's — ``"lds"`` (the tile's round trip through LDS, any layout) or a list of
-    ``(register bit, lane bit)`` cross-lane exchanges (sweep_ops.h ``xchg_lane_bit``). An exchange
-    applies when the group's ops need at most two tile positions that are not in the previous fiber
-    and those sit on thread bits 4 / 5 (lane bits of one wave; the previous layout's lane order is
-    chosen so they do, unless it came from an exchange itself): the wavefront butterfly of a 1-2-bit
-    boundary (syc 32 5: the last group of each FINAL pass touches two new qubits)."""
+    ``(register bit, lane bit)`` cross-lane exchanges (sweep_ops.h ``xchg_lane_bit_any``). Mode 1: an
+    exchange applies when the group's ops need at most two tile positions that are not in the
+    previous fiber and those sit on thread bits 4 / 5 (the previous layout's lane order is chosen so
+    they do, unless it came from an exchange itself): the wavefront butterfly of a 1-2-bit boundary
+    (syc 32 5: the last group of each FINAL pass touches two new qubits). Mode 2, FINAL passes of
+    single-wave tiles: any lane bit (bits 4 / 5 preferred), up to four positions, so the pass needs
+    no LDS."""
+    mode = lane_exchange_mode()
+    general = mode >= 2 and final and TB - 4 == 6
+    fast = (5, 4)  # lane bits the permlane swaps reach
     layouts = [_fiber(enc, gids[0], TB, bitpos)]
     trans = [None]
     free = [True]  # whether the layout's lane order may still be chosen (not fixed by an exchange)
@@ -460,17 +477,20 @@ def _plan_layouts(enc, gids: list, TB: int, bitpos: list) -> tuple:
         cur = layouts[-1]
         used = _group_used(enc, gids[k])
         need = [p for p in used if p not in cur["pos"]]
-        ok = lane_exchange_enabled() and TB - 4 >= 6 and 0 < len(need) <= 2 and len(used) <= 4
-        if ok and not set(need) <= {cur["nonfib"][4], cur["nonfib"][5]}:
-            if free[-1]:  # put the needed positions on thread bits 5 (then 4), the rest ascending
-                rest = [p for p in sorted(cur["nonfib"]) if p not in need]
-                tail = (need + [p for p in rest if p > max(need)][:2 - len(need)]) if len(need) < 2 else need
-                rest = [p for p in rest if p not in tail]
-                order = rest[:4] + ([tail[1], tail[0]] if len(tail) == 2 else tail) + rest[4:]
-                cur = _layout(cur["pos"], order, TB, bitpos)
-                layouts[-1] = cur
-            else:
-                ok = False
+        ok = mode >= 1 and TB - 4 >= 6 and 0 < len(need) <= (4 if general else 2) and len(used) <= 4
+        on_fast = lambda lay: [p for p in need if lay["nonfib"].index(p) in fast]  # noqa: E731
+        if ok and len(on_fast(cur)) < min(len(need), 2) and free[-1]:
+            # put the needed positions on thread bits 5, 4 (then 3, 2, 1, 0), the rest ascending
+            slots = list(fast) + [3, 2, 1, 0]
+            order = [None] * len(cur["nonfib"])
+            for p, t in zip(need, slots):
+                order[t] = p
+            rest = iter(p for p in sorted(cur["nonfib"]) if p not in need)
+            order = [p if p is not None else next(rest) for p in order]
+            cur = _layout(cur["pos"], order, TB, bitpos)
+            layouts[-1] = cur
+        if ok and not general and len(on_fast(cur)) < len(need):
+            ok = False
         if not ok:
             layouts.append(_fiber(enc, gids[k], TB, bitpos))
             trans.append("lds")
@@ -525,7 +545,7 @@ def _emit_group_ops(e: _Emitter, enc, gi: int, f: dict, bitpos: list) -> None:
 def _pass_body_direct(e: _Emitter, enc, ps, gids: list, TB: int, NT: int, n: int, m: int, bitpos: list,
                       init: bool, final: bool, zero_tile: bool, zero_mask: int) -> list:
     """Body of a pass kernel in the direct form (see _pass_kernel)."""
-    lays, trans = _plan_layouts(enc, gids, TB, bitpos)
+    lays, trans = _plan_layouts(enc, gids, TB, bitpos, final=final)
     first, last = lays[0], lays[-1]
     uses_lds = any(t == "lds" for t in trans)
     mmask = (1 << m) - 1
@@ -538,6 +558,7 @@ def _pass_body_direct(e: _Emitter, enc, ps, gids: list, TB: int, NT: int, n: int
         e("for (long long job = j0; job < j1; ++job) {")
     else:
         e("const long long job = grp;")
+    loop_start = len(e.lines)
     e(_state_ptr(enc, ps))
     e("(void)st;")
     e("double2 v[16];")
@@ -564,7 +585,7 @@ def _pass_body_direct(e: _Emitter, enc, ps, gids: list, TB: int, NT: int, n: int
                 e(f"v[{r}] = {_lds_at(f, r)};", 2)
         elif k > 0:  # cross-lane butterfly: register bit i <-> lane bit t
             for i, t in trans[k]:
-                e(f"xchg_lane_bit<{i}, {t}>(v);", 2)
+                e(f"xchg_lane_bit_any<{i}, {t}>(v);", 2)
         _emit_group_ops(e, enc, gi, f, bitpos)
         if k < len(gids) - 1 and trans[k + 1] == "lds":
             if k == 0 or trans[k] != "lds":
@@ -582,6 +603,13 @@ def _pass_body_direct(e: _Emitter, enc, ps, gids: list, TB: int, NT: int, n: int
             e(f"out{r} = fma(sgn, fma(v[{r}].x, v[{r}].x, v[{r}].y * v[{r}].y), out{r});")
         if uses_lds:
             e("__syncthreads();  // the next branch job's first LDS writes follow this job's last reads")
+        if opaque_tid():
+            # the thread index enters each branch job through an opaque zero, so the compiler cannot
+            # hoist the job's index arithmetic out of the loop and keep it live across the whole body
+            # (the FINAL multi kernel of syc 32 5: 172 -> 128 VGPRs, tools/sweep_vgpr.py)
+            e.lines[loop_start:] = [re.sub(r"\btid\b", "tidq", ln) for ln in e.lines[loop_start:]]
+            e.lines.insert(loop_start, "    unsigned qz; asm volatile(\"v_mov_b32 %0, 0\" : \"=v\"(qz)); "
+                                       "const unsigned tidq = tid + qz;")
         e("}")
         for r in range(PER):
             e(f"pjob[(grp << {m}) + (long long)(xlo | 0x{last['hi'][r] & mmask:x}ull)] = out{r};")

@@ -1674,8 +1674,10 @@ def ctypes_size(ctx, comm):
 def test_lane_exchange_sweep_is_bit_identical(T, monkeypatch, key):
     """Per-program sweep kernels with cross-lane butterflies (v_permlane16/32_swap at 1-2-bit fiber-group
     boundaries, sweep_codegen._plan_layouts) against the same kernels through LDS only
-    (QKNIT_SWEEP_LANE_XCHG=0): the exchange only moves amplitudes between lanes, so every swept row is
-    bit-identical; the bench plan (basis-reduced) and, for syc 32 5, the full direct plan."""
+    (QKNIT_SWEEP_LANE_XCHG=0), the shuffle form that keeps FINAL passes out of LDS (=2) and the opaque
+    thread index of the FINAL job loop (QKNIT_SWEEP_OPAQUE_TID): the variants only move amplitudes
+    between lanes or change register allocation, so every swept row is bit-identical; the bench plan
+    (basis-reduced) and, for syc 32 5, the full direct plan."""
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import sweep_codegen
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
 
@@ -1684,14 +1686,16 @@ def test_lane_exchange_sweep_is_bit_identical(T, monkeypatch, key):
     plans = [True, False] if key == "syc_32_5_p2" else [var == "forced" or key == "syc_32_5_p2"]
     for factored in plans:
         rows = {}
-        for x in ("1", "0"):
+        for x, ot in (("0", "0"), ("1", "0"), ("1", "1"), ("2", "1")):
             monkeypatch.setenv("QKNIT_SWEEP_LANE_XCHG", x)
+            monkeypatch.setenv("QKNIT_SWEEP_OPAQUE_TID", ot)
             pipe = KnitPipeline(VirtualCircuit(cut), factored=factored, jit=True)
-            rows[x] = [q.clone() for q in pipe.sweep()]
+            rows[x + ot] = [q.clone() for q in pipe.sweep()]
             del pipe
-        assert len(rows["1"]) == len(rows["0"])
-        for a, b in zip(rows["1"], rows["0"]):
-            assert T.equal(a, b)
+        for v in ("10", "11", "21"):
+            assert len(rows[v]) == len(rows["00"])
+            for a, b in zip(rows[v], rows["00"]):
+                assert T.equal(a, b), v
     monkeypatch.setenv("QKNIT_SWEEP_LANE_XCHG", "1")
     assert sweep_codegen.lane_exchange_enabled()
 
@@ -1715,7 +1719,7 @@ def test_reference_truncation_refuses_huge_third_fragment_merges(T, monkeypatch)
 def test_slice_buffers_selected_across_worlds_without_sync(T, monkeypatch):
     """Slice-mode pipelines of 2, then 4, then 8 ranks stepped in ONE process (rank 0's slice each;
     replicated preparation, no collective), every slice buffer chosen as the best of OUT_TRIES
-    write-rate-checked mappings (forced on these 2^16-entry outputs), no synchronisation or collection
+    write-rate-checked mappings (forced on these 2^20-entry outputs), no synchronisation or collection
     between the worlds — the sequence of round 5's once-faulting rank_sim run (profiles/r05bb_*): every
     step's slice equals the oracle's, and qk_out_stats sees no failed reservation and no error left
     for a write-rate probe."""
@@ -1726,7 +1730,7 @@ def test_slice_buffers_selected_across_worlds_without_sync(T, monkeypatch):
     monkeypatch.setattr(engine, "OUT_FAST_GBS", float("inf"))
     monkeypatch.setattr(engine, "OUT_TRIES", 3)
     monkeypatch.setenv("QKNIT_SLICE_PREP", "replicated")
-    cut = circuits.two_fragment("cx", 8, 8, n_cuts=4)[1]
+    cut = circuits.two_fragment("cx", 10, 10, n_cuts=4)[1]  # 2^20 outputs: 1-MiB slices at 8 ranks
     ref = dense.run_dense(cut)
     st0 = engine.out_stats()
     stream = T.cuda.Stream()

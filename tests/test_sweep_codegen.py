@@ -48,10 +48,11 @@ def _programs():
     return out
 
 
-@pytest.mark.parametrize("lane_xchg", ["1", "0"])
+@pytest.mark.parametrize("lane_xchg", ["2", "1", "0"])
 def test_lane_exchange_layouts_track_every_amplitude(monkeypatch, lane_xchg):
     monkeypatch.setenv("QKNIT_SWEEP_LANE_XCHG", lane_xchg)
     exchanges = 0
+    final_lds = 0
     for key, enc in _programs():
         for ip, ps in enumerate(enc.passes):
             TB = enc.pass_tile_bits(ip)
@@ -59,7 +60,10 @@ def test_lane_exchange_layouts_track_every_amplitude(monkeypatch, lane_xchg):
             gids = list(range(int(ps["group_begin"]), int(ps["group_end"])))
             if not gids:
                 continue
-            lays, trans = sc._plan_layouts(enc, gids, TB, bitpos)
+            final = bool(int(ps["flags"]) & sp.PASS_FINAL)
+            lays, trans = sc._plan_layouts(enc, gids, TB, bitpos, final=final)
+            if final and TB == 10:
+                final_lds += sum(t == "lds" for t in trans)
             held = _where(lays[0], TB)
             for k, gi in enumerate(gids):
                 if k > 0 and trans[k] == "lds":
@@ -76,9 +80,11 @@ def test_lane_exchange_layouts_track_every_amplitude(monkeypatch, lane_xchg):
                 assert not sc._group_ext_positions(enc, gi, bitpos) & set(lays[k]["pos"])
                 # a layout is a bijection onto the tile
                 assert sorted(lays[k]["pos"] + lays[k]["nonfib"]) == list(range(TB))
+    if lane_xchg == "2":
+        assert final_lds == 0  # no FINAL pass of a 10-bit tile touches LDS
     if lane_xchg == "1":
         assert exchanges >= 4  # syc 32 5: both FINAL passes end in a two-bit butterfly
-    else:
+    if lane_xchg == "0":
         assert exchanges == 0
 
 
@@ -87,4 +93,5 @@ def test_generated_kernels_use_lane_exchanges_only_when_enabled(monkeypatch):
     src_on, _ = sc.generate(enc)
     monkeypatch.setenv("QKNIT_SWEEP_LANE_XCHG", "0")
     src_off, _ = sc.generate(enc)
-    assert "xchg_lane_bit<" in src_on and "xchg_lane_bit<" not in src_off.split("}  // namespace qk_sweep_ops")[1]
+    body = lambda src: src.split("}  // namespace qk_sweep_ops")[-1]  # noqa: E731
+    assert "xchg_lane_bit_any<" in body(src_on) and "xchg_lane_bit_any<" not in body(src_off)
