@@ -444,13 +444,19 @@ def _group_ext_positions(enc, gi: int, bitpos: list) -> set:
 def lane_exchange_mode() -> int:
     """QKNIT_SWEEP_LANE_XCHG: 0 = every fiber-group boundary through LDS (round 5's kernels); 1 = lane
     bits 4 / 5 by permlane swaps where at most two positions change (default); 2 = also the other lane
-    bits of a single-wave tile (shuffles), so that FINAL passes never touch LDS."""
+    bits of a single-wave tile (shuffles), so that FINAL passes never touch LDS. Same box, interleaved,
+    bit-identical rows (profiles/r06f_sweep_ab_variants.json): bench-plan sweep 0.0482 / 0.0474 / 0.0505
+    ms and full sweep 0.349 / 0.347 / 0.351 ms for modes 0 / 1 / 2 — the shuffles for lane bits 0-3 cost
+    three selects per dword and their LDS-free FINAL pass gains nothing: it is VALU-issue bound."""
     return int(os.environ.get("QKNIT_SWEEP_LANE_XCHG", "1"))
 
 
 def opaque_tid() -> bool:
-    """QKNIT_SWEEP_OPAQUE_TID=0: the FINAL pass's branch-job loop uses the thread index directly."""
-    return os.environ.get("QKNIT_SWEEP_OPAQUE_TID", "1") != "0"
+    """QKNIT_SWEEP_OPAQUE_TID=1: the FINAL pass's branch-job loop takes the thread index through an
+    opaque zero (172 -> 128 VGPRs on syc 32 5). Measured and not the default: the sweep took 0.0483 vs
+    0.0474 ms (bench plan) and 0.354 vs 0.347 ms (full plan) — recomputing the index arithmetic per job
+    costs more than the occupancy gains (profiles/r06f_sweep_ab_variants.json)."""
+    return os.environ.get("QKNIT_SWEEP_OPAQUE_TID", "0") == "1"
 
 
 def lane_exchange_enabled() -> bool:
