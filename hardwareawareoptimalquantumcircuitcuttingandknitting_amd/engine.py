@@ -883,6 +883,9 @@ def fold_traced(ctx: Context, x, fold: int):
     return reduce_labels(ctx, x.contiguous().view(rows * fold, w // fold), off, rows)
 
 
+_planning_tls = threading.local()
+
+
 @contextlib.contextmanager
 def host_planning():
     """Context of the host side of planning: endpoint side programs memoised for the plan
@@ -891,15 +894,26 @@ def host_planning():
     one SVD spinning up its pool against 2.5 ms on one thread (measured in the build container)."""
     from .fragment_program import planning_memo
 
+    if getattr(_planning_tls, "depth", 0):  # nested (the pipeline's plan around prepare / operands)
+        _planning_tls.depth += 1
+        try:
+            yield
+        finally:
+            _planning_tls.depth -= 1
+        return
     with contextlib.ExitStack() as st:
         st.enter_context(planning_memo())
         try:
             from threadpoolctl import threadpool_limits
 
-            st.enter_context(threadpool_limits(1, user_api="blas"))
+            st.enter_context(threadpool_limits(1, user_api="blas"))  # ~0.5 ms to enter: once per plan
         except ImportError:  # threadpoolctl absent: planning still works, only slower
             pass
-        yield
+        _planning_tls.depth = 1
+        try:
+            yield
+        finally:
+            _planning_tls.depth = 0
 
 
 def prepare_fragments(virt, device: int = 0, upload: bool = True, dedup: bool = True,
