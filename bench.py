@@ -820,10 +820,11 @@ def main():
                       "jobs, labels heaviest first, XCD-grouped tile order (all fragments, per step, this rank)",
             "bound": "latency: 250 branch jobs after row pruning (the column side's 192 rows the knit does not "
                      "depend on are not swept; 750 before): the FINAL pass is 8320 single-wave workgroups at 2 "
-                     "waves per SIMD (170 VGPRs), VALU busy 0.46 of its cycles, f64 issue 0.37 (mostly adds: the "
-                     "normalised +-1/+-i gate entries fold multiplies away), waves waiting 0.33 of their cycles; "
-                     "the INIT pass is one wave's serial op chain per prefix; HBM ~0.09 GB per step (counters, "
-                     "profiles/r04s2_sweep_pmc.json; before pruning r04d_sweep_pmc.json: VALU busy 0.63)",
+                     "waves per SIMD (172 VGPRs, 16-KiB tiles), VALU busy 0.46 of its cycles, f64 issue 0.37 "
+                     "(mostly adds: the normalised +-1/+-i gate entries fold multiplies away), waves waiting 0.33 "
+                     "of their cycles; its last fiber group is reached by v_permlane16/32_swap butterflies, not "
+                     "LDS (round 6); the INIT pass is one wave's serial op chain per prefix; HBM ~0.09 GB per step "
+                     "(counters, profiles/r04s2_sweep_pmc.json); at scale see sweep_full",
             "ms_per_step": sweep_ms,
             "branch_jobs": counts["branch_jobs"],
             "hbm_bytes_model": traffic["hbm"],
