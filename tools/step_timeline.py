@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One pipelined step's kernels from a rocprofv3 --kernel-trace CSV, by stream, in time order.
 
-  python tools/step_timeline.py run_kernel_trace.csv [--steps N]
+  python tools/step_timeline.py run_kernel_trace.csv|run_results.db [--steps N]
 
 Takes the write kernel launches (qk_knit_outer_*) as step markers and prints, for the step
 interval in the middle of the run, every kernel that started in it: its stream, start
@@ -14,8 +14,16 @@ from collections import defaultdict
 
 def main():
     path = sys.argv[1]
-    rows = list(csv.DictReader(open(path)))
-    ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Stream_Id"], r["Queue_Id"]) for r in rows]
+    if path.endswith(".db"):  # rocprofv3's default rocpd database (its kernels view)
+        import sqlite3
+
+        con = sqlite3.connect(path)
+        ks = [(int(a), int(b), n, str(s), str(q)) for a, b, n, s, q in
+              con.execute("select start, end, name, stream_id, queue_id from kernels")]
+    else:
+        rows = list(csv.DictReader(open(path)))
+        ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Stream_Id"], r["Queue_Id"])
+              for r in rows]
     ks.sort()
     writes = [k for k in ks if "qk_knit_outer" in k[2]]
     if len(writes) < 3:
