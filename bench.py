@@ -368,8 +368,10 @@ def drop_in_timing(cut, ref_out, steps: int, device: int) -> dict:
     engine. ``first_call_ms``: plan cache empty (fragment compile, job tables, transforms, uploads;
     the hiprtc sweep modules are already cached in this process by the bench's own pipeline);
     ``steady_ms``: later calls on a fresh ``VirtualCircuit`` of the same cut (the plan is found by the
-    circuit's content hash), each result freed before the next call. ``max_abs_diff_vs_step``: the
-    drop-in's distribution against the bench step's output, every one of the 2^N entries."""
+    circuit's content hash), each result freed before the next call; ``reselect_calls_ms``: a call
+    that replaced the first call's un-checked output mapping (its write was below the write-rate stop)
+    by a selected one, reported apart from the steady state. ``max_abs_diff_vs_step``: the drop-in's
+    distribution against the bench step's output, every one of the 2^N entries."""
     import torch
 
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit
@@ -392,15 +394,24 @@ def drop_in_timing(cut, ref_out, steps: int, device: int) -> dict:
     for i in range(0, out.numel(), chunk):
         diff = max(diff, float((out[i:i + chunk] - ref_out[i:i + chunk]).abs().max()))
     del out
-    times, infos, builds = [], [], []
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import engine
+
+    times, infos, builds, reselect = [], [], [], []
     for _ in range(max(steps, 3)):
         tb = time.perf_counter()
         virt = VirtualCircuit(cut)  # the reference builds one per call (Utilities.py:74-79)
         builds.append(time.perf_counter() - tb)
+        n_sel = len(engine.out_selections)
         t0 = time.perf_counter()
         out, info = run_virtual_circuit(virt, dense=True, device=device)
-        times.append(time.perf_counter() - t0)
-        infos.append(info)
+        dt = time.perf_counter() - t0
+        if len(engine.out_selections) > n_sel:
+            # this call replaced the first call's un-checked output mapping by a write-rate-selected one
+            # (its own write was slow: run.py / KnitPipeline.take_out): reported apart
+            reselect.append(dt)
+        else:
+            times.append(dt)
+            infos.append(info)
         del out
     # the reference-shaped result (run.py:71): entries above ACCURACY + NPD, thresholded knit
     dict_times, entries = [], 0
@@ -426,9 +437,10 @@ def drop_in_timing(cut, ref_out, steps: int, device: int) -> dict:
             "dict_steady_ms": float(sum(dict_times) / len(dict_times)) * 1e3, "dict_min_ms": min(dict_times) * 1e3,
             "dict_entries": entries, "accuracy": quasi_distr.ACCURACY,
             "steady_ms": float(sum(times) / len(times)) * 1e3, "steady_min_ms": min(times) * 1e3,
+            "reselect_calls_ms": [round(x * 1e3, 2) for x in reselect],
             "run_time_ms": float(sum(i.run_time for i in infos) / len(infos)) * 1e3,
             "knit_time_ms": float(sum(i.knit_time for i in infos) / len(infos)) * 1e3,
-            "calls": len(times), "max_abs_diff_vs_step": diff, "out_alloc": placement,
+            "calls": len(times) + len(reselect), "max_abs_diff_vs_step": diff, "out_alloc": placement,
             # host: VirtualCircuit(cut) per call (fragment circuits + the cut's content hash, the plan key)
             "virtual_circuit_ms": float(sum(builds) / len(builds)) * 1e3}
 
