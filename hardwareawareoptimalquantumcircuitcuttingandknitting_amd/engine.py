@@ -247,6 +247,7 @@ OUT_SELECT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_SELECT_MIN_BYTES", str(4 <<
 OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "6850"))
 OUT_TRIES = int(os.environ.get("QKNIT_OUT_TRIES", "3"))
 out_selections: list = []  # per selected output: the candidates' write rates (GB/s), the kept one first
+out_selection_log: list = []  # per selected output: host ms of each mapping, each rate check, the frees
 _out_select_lock = threading.Lock()  # one selection at a time per process: two threads' candidates never stack
 
 
@@ -300,23 +301,35 @@ def out_buffer(ctx: Context, n: int, select: bool = True):
         # (qk_out_write_rate times whole 512-KiB blocks: nothing smaller is selected)
         return first.tensor(), first
     with _out_select_lock:
+        from time import perf_counter
+
         owner = first
         first = None
+        t = perf_counter()
         tried = [(_out_rate(ctx, owner), owner)]
+        log = {"bytes": 8 * n, "rate_ms": [(perf_counter() - t) * 1e3], "map_ms": []}
         while tried[-1][0] < OUT_FAST_GBS and len(tried) < OUT_TRIES:
             free, _ = T.cuda.mem_get_info(ctx.device)
             if free < 8 * n + (2 << 30):
+                log["stopped"] = f"free {free / 2**30:.1f} GiB"
                 break
+            t = perf_counter()
             try:  # memory taken meanwhile (another thread / process): keep the best so far
                 cand = MappedOut(ctx, n)
             except _lib.QknitError:
                 break
+            log["map_ms"].append((perf_counter() - t) * 1e3)
+            t = perf_counter()
             tried.append((_out_rate(ctx, cand), cand))
+            log["rate_ms"].append((perf_counter() - t) * 1e3)
         best = max(range(len(tried)), key=lambda i: tried[i][0])
         owner = tried[best][1]
         out_selections.append([round(tried[best][0], 1)] + [round(r, 1) for i, (r, _) in enumerate(tried) if i != best])
+        t = perf_counter()
         del tried  # the others are unmapped here (cand: the last candidate's name)
         cand = None
+        log["free_ms"] = (perf_counter() - t) * 1e3
+        out_selection_log.append(log)
     return owner.tensor(), owner
 
 
