@@ -246,6 +246,12 @@ OUT_SELECT_MIN_BYTES = int(os.environ.get("QKNIT_OUT_SELECT_MIN_BYTES", str(4 <<
 # and qk_out_stats counts reservations (DESIGN.md §4 for what the reruns found)
 OUT_FAST_GBS = float(os.environ.get("QKNIT_OUT_FAST_GBS", "6850"))
 OUT_TRIES = int(os.environ.get("QKNIT_OUT_TRIES", "3"))
+# A candidate mapping that took longer than this (host ms) ends the selection after its rate check:
+# memory a process released moments before (e.g. the previous process on the device) is handed out
+# again only after the driver has cleared it, and a mapping that reaches into it blocks for seconds
+# (tools/map_stall_probe.py --seq: 3.3 s for one 32-GiB mapping right after a process holding 192 GiB
+# exited, 0.6-0.8 ms 30 s later; profiles/r06k_*). The next candidate would wait the same way.
+OUT_MAP_SLOW_MS = float(os.environ.get("QKNIT_OUT_MAP_SLOW_MS", "200"))
 out_selections: list = []  # per selected output: the candidates' write rates (GB/s), the kept one first
 out_selection_log: list = []  # per selected output: host ms of each mapping, each rate check, the frees
 _out_select_lock = threading.Lock()  # one selection at a time per process: two threads' candidates never stack
@@ -322,6 +328,9 @@ def out_buffer(ctx: Context, n: int, select: bool = True):
             t = perf_counter()
             tried.append((_out_rate(ctx, cand), cand))
             log["rate_ms"].append((perf_counter() - t) * 1e3)
+            if log["map_ms"][-1] > OUT_MAP_SLOW_MS:
+                log["stopped"] = f"mapping took {log['map_ms'][-1]:.0f} ms"
+                break
         best = max(range(len(tried)), key=lambda i: tried[i][0])
         owner = tried[best][1]
         out_selections.append([round(tried[best][0], 1)] + [round(r, 1) for i, (r, _) in enumerate(tried) if i != best])

@@ -937,6 +937,28 @@ def test_output_selection_keeps_fastest_and_frees_the_others(T, monkeypatch):
         assert (rc == 0) == (ptr == kept)
 
 
+def test_output_selection_stops_after_a_slow_mapping(T, monkeypatch):
+    """A candidate mapping slower than OUT_MAP_SLOW_MS ends the selection after its rate check (memory
+    the driver is still clearing after another process: tools/map_stall_probe.py); forced here with a
+    negative limit, so of OUT_TRIES = 3 only the first output and one candidate are made, the faster is
+    kept, and the knit into it equals the oracle."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    monkeypatch.setattr(engine, "OUT_MAPPED_MIN_BYTES", 0)
+    monkeypatch.setattr(engine, "OUT_SELECT_MIN_BYTES", 0)
+    monkeypatch.setattr(engine, "OUT_FAST_GBS", float("inf"))
+    monkeypatch.setattr(engine, "OUT_TRIES", 3)
+    monkeypatch.setattr(engine, "OUT_MAP_SLOW_MS", -1.0)
+    cut = circuits.two_fragment("cx", 8, 8, n_cuts=4)[1]
+    pipe = KnitPipeline(VirtualCircuit(cut), factored=True)
+    got = pipe.step().cpu().numpy()
+    np.testing.assert_allclose(got, dense.run_dense(cut), atol=1e-12, rtol=0)
+    sel = engine.out_selections[-1]
+    assert len(sel) == 2 and sel[0] == max(sel)
+    log = engine.out_selection_log[-1]
+    assert len(log["map_ms"]) == 1 and log["stopped"].startswith("mapping took")
+
+
 def test_mapped_outputs_freed_and_remapped_read_back_exactly(T, monkeypatch):
     """Drop-in calls that keep some results and drop others: mappings are freed and new ones made
     between calls. Each result equals the oracle (1e-12) read back by the D2H copy. Freed ranges'
