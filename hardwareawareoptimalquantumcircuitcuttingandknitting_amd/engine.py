@@ -26,6 +26,7 @@ import logging
 import os
 import threading
 from dataclasses import dataclass, field
+from time import perf_counter
 
 import numpy as np
 
@@ -307,8 +308,6 @@ def out_buffer(ctx: Context, n: int, select: bool = True):
         # (qk_out_write_rate times whole 512-KiB blocks: nothing smaller is selected)
         return first.tensor(), first
     with _out_select_lock:
-        from time import perf_counter
-
         owner = first
         first = None
         t = perf_counter()
