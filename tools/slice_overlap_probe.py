@@ -21,7 +21,9 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--launches", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--modes", nargs="+", default=["serial_all", "rot2_all", "rot3_all", "serial_w128", "rot3_w128"])
+    ap.add_argument("--modes", nargs="+", default=["serial_all", "rot2_all", "rot3_all", "serial_w128", "rot3_w128"],
+                    help="..._w128 modes may end in +empty (10 tiny kernels per write on a stream over the other "
+                         "128 CUs: kernel boundaries alone) or +chain (the step's real sweep + preparation chain there)")
     args = ap.parse_args()
     import torch
 
@@ -38,7 +40,8 @@ def main():
     ia, ib = pipe.order[0], pipe.order[-1]
     cA, cB = pipe.ops.clbits[ia], pipe.ops.clbits[ib]
     N = pipe.N
-    del pipe, qs
+    chain_pipe = pipe  # kept for +chain modes (its sweep and preparation re-run beside the writes)
+    del qs
     torch.cuda.empty_cache()
     ctx = engine.get_context(0)
     total = engine.device_cu_count(0)
@@ -46,7 +49,23 @@ def main():
     bufs = [engine.out_buffer(ctx, n_out) for _ in range(3)]
     write_cus = tuple(range(total - 128))
 
+    prep_cus = tuple(range(total - 128, total))
+    side = engine.cu_masked_stream(0, prep_cus, tag=400)
+    tiny = torch.zeros(64, dtype=torch.float64, device="cuda")
+
+    def side_work(kind):
+        with torch.cuda.stream(side):
+            if kind == "empty":
+                for _ in range(10):
+                    tiny.add_(1.0)
+            elif kind == "chain":
+                chain_pipe.be.bind()
+                q = chain_pipe.sweep()
+                chain_pipe._prep_dev_rank(q)
+        ctx.bind_stream()
+
     def streams(mode):
+        mode = mode.split("+")[0]
         nb = 1 if mode.startswith("serial") else int(mode[3])
         if mode.endswith("_all"):
             return [torch.cuda.Stream() for _ in range(nb)]
@@ -64,7 +83,10 @@ def main():
             for warm in (True, False):
                 cnt = 3 if warm else args.launches
                 t0 = time.perf_counter()
+                extra = mode.split("+")[1] if "+" in mode else None
                 for i in range(cnt):
+                    if extra:
+                        side_work(extra)
                     s = ss[i % len(ss)]
                     with torch.cuda.stream(s):
                         ctx.bind_stream()
