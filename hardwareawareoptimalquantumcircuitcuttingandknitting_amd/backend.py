@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .circuit import ClassicalRegister, QuantumCircuit
+from .circuit import QuantumCircuit
 
 
 class MI355XBackend:

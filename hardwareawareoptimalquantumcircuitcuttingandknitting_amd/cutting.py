@@ -21,7 +21,6 @@ choices for the BASELINE configs (derivation: SURVEY.md App. C).
 """
 from __future__ import annotations
 
-import math
 from dataclasses import dataclass, field
 
 from .circuit import CircuitInstruction, Gate, QuantumCircuit, QuantumRegister

@@ -17,7 +17,7 @@ def main():
     args = ap.parse_args()
     import torch
 
-    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting, pipeline
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd import VirtualCircuit, cutting
     from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline, _mm_nt
 
     name, n, d, p, var = cutting.BASELINE_CONFIGS[args.workload]
