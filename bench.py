@@ -716,6 +716,9 @@ def main():
 
     for _ in range(args.warmup):
         pipe.step()
+    # pipelined steps: their rotating output buffers are made and selected here, not in a timed step
+    # (with --warmup 1 the second step would make them)
+    pipe.prepare_pipelined()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()

@@ -744,6 +744,36 @@ def test_pipelined_steps_order_writes_after_caller_reads(T, buffers):
         np.testing.assert_allclose(c.cpu().numpy(), ref, atol=1e-12, rtol=0)
 
 
+@pytest.mark.parametrize("buffers", [2, 3])
+def test_prepare_pipelined_makes_every_buffer_before_the_steps(T, monkeypatch, buffers):
+    """bench.py's call after its warmup steps: with one step done, prepare_pipelined makes the rotating
+    output buffers (mapped and write-rate selected: forced here on small outputs) and their streams, so
+    the pipelined steps after it map nothing (qk_out_stats' reservation count unchanged), and every one of
+    them equals the oracle; before any step it does nothing."""
+    from hardwareawareoptimalquantumcircuitcuttingandknitting_amd.pipeline import KnitPipeline
+
+    monkeypatch.setattr(engine, "OUT_MAPPED_MIN_BYTES", 0)
+    monkeypatch.setattr(engine, "OUT_SELECT_MIN_BYTES", 0)
+    cut = circuits.two_fragment("cx", 8, 8, n_cuts=2)[1]
+    ref = dense.run_dense(cut)
+    with T.cuda.stream(T.cuda.Stream()):
+        pipe = KnitPipeline(VirtualCircuit(cut), factored=True, data_rank=True)
+        assert pipe.overlap_ok()
+        pipe.overlap, pipe.out_buffers = True, buffers
+        pipe.prepare_pipelined()
+        assert pipe.out is None and pipe._outs is None
+        outs = [pipe.step().clone()]
+        pipe.prepare_pipelined()
+        assert len(pipe._outs) == buffers and len({o.data_ptr() for o in pipe._outs}) == buffers
+        reserved = engine.out_stats()["reserved"]
+        for _ in range(2 * buffers):
+            outs.append(pipe.step().clone())
+        T.cuda.current_stream().synchronize()
+        assert engine.out_stats()["reserved"] == reserved
+    for o in outs:
+        np.testing.assert_allclose(o.cpu().numpy(), ref, atol=1e-12, rtol=0)
+
+
 @pytest.mark.slow
 def test_syc_32_5_data_rank_step_matches_exact_step(T):
     """The bench step (factored knit, light-cone basis, data-rank compression: the rank-64
